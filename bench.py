@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident packed encode+decode of independent units.
+
+BASELINE.json metric: "GiB/s device-resident packed encode+decode, 1M x 4KiB
+segments, 1/2/4/8 GPU". One step = one batch pass of the hot path:
+  encode (packPacked, message.zig:200-271) of every unit into capacity slots,
+  decode (unpackPacked, message.zig:88-145) straight from those slots,
+  per-rank packed total + RCCL all-gather of the per-rank totals (N > 1).
+value = sum over ranks of unpacked bytes per step / max-over-ranks step time, in GiB/s.
+
+Inputs are generated on device before timing (synthetic, counter-based hash:
+DESIGN.md §4). After timing, decode(encode(x)) == x is checked on device.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "capnp-zig_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import capnp_packed as cp  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, 8.0 TB/s (MI355X_MICROARCH.md, chip table)
+META_BYTES_PER_UNIT = 44  # in_off, in_len, out_off, out_cap (4 x 8 B read) + out_len (8 B) + status (4 B)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--units", type=int, default=1 << 20, help="units per GPU")
+    ap.add_argument("--unit-bytes", type=int, default=4096)
+    ap.add_argument("--zero-thresh", type=int, default=128, help="zero-byte probability x 256 (128 = 0.5)")
+    ap.add_argument("--seed", type=int, default=0xC0DE0003)
+    ap.add_argument("--sweep", action="store_true", help="also time p = 0.1 / 0.9 (extra fields)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
+    return ap.parse_args()
+
+
+class Workload:
+    def __init__(self, n, ub, seed, thr, unit_base, dev):
+        self.n, self.ub = n, ub
+        self.d_in = cp.generate(n, ub, seed=seed, zero_thresh=thr, unit_base=unit_base, device=dev)
+        self.in_off, self.in_len = cp.uniform_layout(n, ub, device=dev)
+        self.slot = cp.encode_bound(ub)
+        self.pk_off, self.pk_cap = cp.uniform_layout(n, self.slot, device=dev)
+        self.d_pk = torch.empty(n * self.slot, dtype=torch.uint8, device=dev)
+        self.plen = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.pst = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.d_out = torch.empty(n * ub, dtype=torch.uint8, device=dev)
+        self.ulen = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.ust = torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def encode(self, stream):
+        cp.encode_batch(self.d_in, self.in_off, self.in_len, self.d_pk, self.pk_off, self.pk_cap,
+                        self.plen, self.pst, stream=stream)
+
+    def decode(self, stream):
+        cp.decode_batch(self.d_pk, self.pk_off, self.plen, self.d_out, self.in_off, self.in_len,
+                        self.ulen, self.ust, stream=stream)
+
+    def verify(self):
+        ok = bool((self.pst == 0).all().item() and (self.ust == 0).all().item()
+                  and (self.ulen == self.ub).all().item() and torch.equal(self.d_out, self.d_in))
+        return ok
+
+
+def time_steps(wl, steps, warmup, world, dev):
+    stream = torch.cuda.current_stream()
+    gathered = torch.zeros(world, dtype=torch.int64, device=dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        wl.encode(stream)
+        if ev is not None:
+            ev[1].record(stream)
+        wl.decode(stream)
+        if ev is not None:
+            ev[2].record(stream)
+        total = wl.plen.sum()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, total.view(1))
+        else:
+            gathered[0] = total
+
+    for _ in range(warmup):
+        step()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / steps
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return float(elapsed.item()), enc_ms, dec_ms, gathered
+
+
+def cpu_baseline(args, budget_s):
+    """Oracle (C restatement of message.zig:88-271) on the host cores, OpenMP over
+    units, same generator, same unit size/density, bounded sample."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import numpy as np
+    import oracle
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    ub = args.unit_bytes
+    n = 4096
+    data = oracle.generate(n, ub, seed=args.seed, zero_thresh=args.zero_thresh, threads=threads)
+    in_off = np.arange(0, n * ub + 1, ub, dtype=np.uint64)
+    slot = 10 * ub // 8
+    pk_off = np.arange(0, n * slot + 1, slot, dtype=np.uint64)
+    reps, t_total = 0, 0.0
+    packed_dense = None
+    while t_total < budget_s and reps < 1000:
+        t0 = time.perf_counter()
+        out, out_len, st = oracle.pack_batch(data, in_off, pk_off, threads=threads)
+        if packed_dense is None:
+            dense = np.zeros(n + 1, dtype=np.uint64)
+            dense[1:] = np.cumsum(out_len)
+            packed_dense = (np.concatenate([out[int(pk_off[i]):int(pk_off[i]) + int(out_len[i])]
+                                            for i in range(n)]), dense)
+            t0 = time.perf_counter()  # exclude the one-time dense repacking from the timing
+            out, out_len, st = oracle.pack_batch(data, in_off, pk_off, threads=threads)
+        pk, dense = packed_dense
+        dec, dec_len, dst = oracle.unpack_batch(pk, dense, in_off, threads=threads)
+        t_total += time.perf_counter() - t0
+        reps += 1
+    assert (st == 0).all() and (dst == 0).all() and (dec[:n * ub] == data).all()
+    gib = reps * n * ub / t_total / 2 ** 30
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x ({n} units x {ub} B, same generator/seed/density) pack+unpack via "
+                      f"oracle/packed_oracle.c (-O3, OpenMP {threads} threads), {t_total:.1f} s"}
+
+
+def load_traffic(config_key):
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(config_key)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    n, ub = args.units, args.unit_bytes
+    wl = Workload(n, ub, args.seed, args.zero_thresh, unit_base=rank * n, dev=dev)
+    elapsed, enc_ms, dec_ms, gathered = time_steps(wl, args.steps, args.warmup, world, dev)
+    ok = wl.verify()
+    ok_t = torch.tensor([1 if ok else 0], device=dev)
+    if world > 1:
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+    packed_local = int(wl.plen.sum().item())
+    packed_all = int(gathered.sum().item())
+
+    extra = {}
+    if args.sweep:
+        for thr, name in ((26, "p0.1"), (230, "p0.9")):
+            del wl
+            torch.cuda.empty_cache()
+            wl = Workload(n, ub, args.seed, thr, unit_base=rank * n, dev=dev)
+            e, em, dm, g = time_steps(wl, max(3, args.steps // 2), 1, world, dev)
+            extra[name] = {"GiB_s": round(world * n * ub / (e / max(3, args.steps // 2)) / 2 ** 30, 2),
+                           "encode_ms": round(em, 4), "decode_ms": round(dm, 4),
+                           "packed_ratio": round(int(g.sum().item()) / (world * n * ub), 4),
+                           "bit_exact_roundtrip": wl.verify()}
+
+    if rank == 0:
+        steps = args.steps
+        ms_per_step = elapsed / steps * 1e3
+        U_total = world * n * ub
+        value = U_total / (elapsed / steps) / 2 ** 30
+        P = packed_local
+        alg_bytes = n * ub + P + META_BYTES_PER_UNIT * n  # per launch on one GPU, same for enc and dec
+        dom, dom_ms = ("decode_kernel", dec_ms) if dec_ms >= enc_ms else ("encode_kernel", enc_ms)
+        achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+        cfg_key = f"{n}x{ub}_t{args.zero_thresh}"
+        traffic = load_traffic(cfg_key)
+        line = {
+            "metric": "GiB/s device-resident packed encode+decode, 1M x 4KiB segments",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device counter-hash generator, DESIGN.md §4)",
+            "config": {"workload": f"{n} units x {ub} B per GPU, zero-byte p={args.zero_thresh}/256, "
+                                   "encode into capacity slots + decode from slots",
+                       "units_per_gpu": n, "unit_bytes": ub, "zero_thresh": args.zero_thresh,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic, "alg_bytes_per_launch": alg_bytes},
+            "encode_ms": round(enc_ms, 4),
+            "decode_ms": round(dec_ms, 4),
+            "encode_GiB_s": round(world * 0 + n * ub / (enc_ms * 1e-3) / 2 ** 30, 2),
+            "decode_GiB_s": round(n * ub / (dec_ms * 1e-3) / 2 ** 30, 2),
+            "packed_ratio": round(packed_all / U_total, 4),
+            "packed_total_all_ranks": packed_all,
+            "bit_exact_roundtrip": bool(ok_t.item()),
+        }
+        line.update(extra)
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,370 @@
+"""Host-side mirror of the reference's packed read/write surface over the C-ABI.
+
+The reference (nullstyle/capnp-zig) exposes packing through
+  MessageBuilder.toPackedBytes / writePackedTo   src/serialization/message.zig:2175-2213
+  Message.initPacked                             message.zig:400-408
+  Reader.initPacked                              src/serialization/reader.zig:18-23
+over the file-private packPacked / unpackPacked / estimateUnpackedSize
+(message.zig:88-271). This module keeps those names, argument meanings and error
+names, and routes every byte through libcapnp_packed.so (HIP kernels for gfx950).
+There is no CPU fallback: if the library or a gfx950 device is missing, calls
+raise NoDevice / RuntimeError.
+
+Batch functions take torch tensors that live in device memory (torch is used only
+for device memory and streams): uint8 byte buffers, int64 offset/length tensors
+(bit-identical to the ABI's u64), int32 status tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+
+try:  # load torch first so libcapnp_packed.so binds to the same HIP runtime instance
+    import torch
+except ImportError:  # pragma: no cover - the ABI still loads for symbol checks
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcapnp_packed.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "capnp_packed.h")
+
+OK = 0
+INVALID_MESSAGE_SIZE = 1
+UNEXPECTED_EOF = 2
+OVERFLOW = 3
+OUT_OF_SPACE = 4
+INVALID_ARGUMENT = 5
+DEVICE_ERROR = 6
+NO_DEVICE = 7
+
+
+class PackedError(Exception):
+    status = -1
+
+
+class InvalidMessageSize(PackedError):  # message.zig:201
+    status = INVALID_MESSAGE_SIZE
+
+
+class UnexpectedEof(PackedError):  # message.zig:152-191
+    status = UNEXPECTED_EOF
+
+
+class Overflow(PackedError):  # message.zig:163
+    status = OVERFLOW
+
+
+class OutOfSpace(PackedError):
+    status = OUT_OF_SPACE
+
+
+class InvalidArgument(PackedError):
+    status = INVALID_ARGUMENT
+
+
+class DeviceError(PackedError):
+    status = DEVICE_ERROR
+
+
+class NoDevice(PackedError):
+    status = NO_DEVICE
+
+
+_ERRORS = {c.status: c for c in (InvalidMessageSize, UnexpectedEof, Overflow, OutOfSpace,
+                                 InvalidArgument, DeviceError, NoDevice)}
+
+# Message.init errors (message.zig:341-394)
+class EndOfStream(Exception):
+    pass
+
+
+class InvalidSegmentCount(Exception):
+    pass
+
+
+class SegmentCountLimitExceeded(Exception):
+    pass
+
+
+class TruncatedMessage(Exception):
+    pass
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+# exported symbol -> (restype, argtypes)
+SIGNATURES = {
+    "capnp_packed_abi_version": (ctypes.c_uint32, []),
+    "capnp_packed_last_error": (ctypes.c_char_p, []),
+    "capnp_packed_status_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "capnp_packed_encode_bound": (_sz, [_sz]),
+    "capnp_packed_encode": (ctypes.c_int, [_vp, _sz, _vp, _sz, ctypes.POINTER(_sz)]),
+    "capnp_packed_decoded_size": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_sz)]),
+    "capnp_packed_decode": (ctypes.c_int, [_vp, _sz, _vp, _sz, ctypes.POINTER(_sz)]),
+    "capnp_packed_encode_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "capnp_packed_encoded_size_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
+    "capnp_packed_decode_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "capnp_packed_decoded_size_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
+    "capnp_packed_scan_scratch_bytes": (_sz, [ctypes.c_uint32]),
+    "capnp_packed_lengths_to_offsets": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp,
+                                                       _sz, _vp]),
+    "capnp_packed_generate": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_uint32, _vp]),
+}
+
+
+def lib():
+    """Load libcapnp_packed.so (built by `make -C capnp-zig_amd`). Fails loudly."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C capnp-zig_amd` "
+                               "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().capnp_packed_last_error().decode()
+
+
+def _raise(st: int, what: str = ""):
+    if st == OK:
+        return
+    cls = _ERRORS.get(st, PackedError)
+    raise cls(f"{what}: {lib().capnp_packed_status_name(st).decode()} ({last_error()})")
+
+
+def _cbuf(data) -> ctypes.Array:
+    b = bytes(data)
+    return ctypes.create_string_buffer(b, max(1, len(b)))
+
+
+# ---------------------------------------------------------------------------
+# single-buffer API (host bytes in, host bytes out; one unit through the GPU)
+# ---------------------------------------------------------------------------
+
+def encode_bound(n: int) -> int:
+    return lib().capnp_packed_encode_bound(n)
+
+
+def pack_packed(data) -> bytes:
+    """packPacked (message.zig:200-271). Raises InvalidMessageSize if len % 8."""
+    data = bytes(data)
+    cap = encode_bound(len(data))
+    out = ctypes.create_string_buffer(max(1, cap))
+    n = _sz()
+    st = lib().capnp_packed_encode(_cbuf(data), len(data), out, cap, ctypes.byref(n))
+    _raise(st, "packPacked")
+    return out.raw[:n.value]
+
+
+def estimate_unpacked_size(packed) -> int:
+    """estimateUnpackedSize (message.zig:152-191)."""
+    packed = bytes(packed)
+    n = _sz()
+    st = lib().capnp_packed_decoded_size(_cbuf(packed), len(packed), ctypes.byref(n))
+    _raise(st, "estimateUnpackedSize")
+    return n.value
+
+
+def unpack_packed(packed) -> bytes:
+    """unpackPacked (message.zig:88-145). Raises UnexpectedEof on truncation."""
+    packed = bytes(packed)
+    size = estimate_unpacked_size(packed)
+    out = ctypes.create_string_buffer(max(1, size))
+    n = _sz()
+    st = lib().capnp_packed_decode(_cbuf(packed), len(packed), out, size, ctypes.byref(n))
+    _raise(st, "unpackPacked")
+    return out.raw[:n.value]
+
+
+# ---------------------------------------------------------------------------
+# framing mirror: MessageBuilder / Message / Reader (packed entry points only)
+# ---------------------------------------------------------------------------
+
+MAX_SEGMENT_COUNT = 512  # message.zig:310
+
+
+def frame_segments(segments) -> bytes:
+    """MessageBuilder.toBytes (message.zig:2123-2170): segment table + segments."""
+    segs = [bytes(s) for s in segments] or [b""]
+    n = len(segs)
+    for s in segs:
+        if len(s) % 8:
+            raise InvalidMessageSize("segment length is not a multiple of 8")
+    hdr = struct.pack("<I", n - 1) + b"".join(struct.pack("<I", len(s) // 8) for s in segs)
+    if n % 2 == 0:
+        hdr += b"\x00\x00\x00\x00"
+    return hdr + b"".join(segs)
+
+
+class MessageBuilder:
+    """Segment-level mirror of MessageBuilder (message.zig:1643). Only the
+    serialization surface is mirrored; struct/list building is out of scope."""
+
+    def __init__(self):
+        self.segments: list[bytearray] = []
+
+    def create_segment(self, data=b"") -> int:
+        self.segments.append(bytearray(data))
+        return len(self.segments) - 1
+
+    def to_bytes(self) -> bytes:
+        if not self.segments:
+            self.create_segment()
+        return frame_segments(self.segments)
+
+    def to_packed_bytes(self) -> bytes:
+        """message.zig:2175-2179: packPacked(toBytes())."""
+        return pack_packed(self.to_bytes())
+
+    def write_to(self, writer) -> None:
+        writer.write(self.to_bytes())
+
+    def write_packed_to(self, writer) -> None:
+        """message.zig:2209-2213."""
+        writer.write(self.to_packed_bytes())
+
+
+class Message:
+    """Mirror of Message (message.zig:309-418): segment views over backing data."""
+
+    def __init__(self, segments, backing_data):
+        self.segments = segments
+        self.backing_data = backing_data
+
+    @classmethod
+    def init(cls, data) -> "Message":
+        """message.zig:341-394 segment-table parse; borrows `data`."""
+        mv = memoryview(bytes(data) if not isinstance(data, (bytes, bytearray, memoryview)) else data)
+        if len(mv) < 4:
+            raise EndOfStream()
+        (minus_one,) = struct.unpack_from("<I", mv, 0)
+        if minus_one == 0xFFFFFFFF:
+            raise InvalidSegmentCount()
+        count = minus_one + 1
+        if count > MAX_SEGMENT_COUNT:
+            raise SegmentCountLimitExceeded()
+        header_bytes = (1 + count + (1 if count % 2 == 0 else 0)) * 4
+        if header_bytes > len(mv):
+            raise TruncatedMessage()
+        sizes = struct.unpack_from(f"<{count}I", mv, 4)
+        off = header_bytes
+        segs = []
+        for sw in sizes:
+            end = off + 8 * sw
+            if end > len(mv):
+                raise TruncatedMessage()
+            segs.append(mv[off:end])
+            off = end
+        return cls(segs, None)
+
+    @classmethod
+    def init_packed(cls, packed) -> "Message":
+        """message.zig:400-408: unpackPacked then Message.init; owns the buffer."""
+        unpacked = unpack_packed(packed)
+        msg = cls.init(unpacked)
+        msg.backing_data = unpacked
+        return msg
+
+    def deinit(self) -> None:
+        self.segments = []
+        self.backing_data = None
+
+
+class Reader:
+    """Mirror of Reader.init / Reader.initPacked (reader.zig:11-23)."""
+
+    def __init__(self, msg: Message):
+        self.msg = msg
+
+    @classmethod
+    def init(cls, data) -> "Reader":
+        return cls(Message.init(data))
+
+    @classmethod
+    def init_packed(cls, data) -> "Reader":
+        return cls(Message.init_packed(data))
+
+
+# ---------------------------------------------------------------------------
+# device-resident batch API (torch tensors in HBM)
+# ---------------------------------------------------------------------------
+
+def _ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def encode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None) -> None:
+    """Batch packPacked: unit i = d_in[in_off[i] : in_off[i]+in_len[i]] -> slot
+    d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit."""
+    n = in_off.numel()
+    _raise(lib().capnp_packed_encode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out), _ptr(out_off),
+                                           _ptr(out_cap), _ptr(out_len), _ptr(status), _stream(stream)),
+           "encode_batch")
+
+
+def encoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> None:
+    n = in_off.numel()
+    _raise(lib().capnp_packed_encoded_size_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(out_len),
+                                                 _ptr(status), _stream(stream)), "encoded_size_batch")
+
+
+def decode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None) -> None:
+    """Batch unpackPacked: unit i = d_in[in_off[i] : in_off[i]+in_len[i]] -> slot
+    d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit."""
+    n = in_off.numel()
+    _raise(lib().capnp_packed_decode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out), _ptr(out_off),
+                                           _ptr(out_cap), _ptr(out_len), _ptr(status), _stream(stream)),
+           "decode_batch")
+
+
+def decoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> None:
+    n = in_off.numel()
+    _raise(lib().capnp_packed_decoded_size_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(out_len),
+                                                 _ptr(status), _stream(stream)), "decoded_size_batch")
+
+
+def lengths_to_offsets(lengths, base: int = 0, out=None, stream=None):
+    """Exclusive scan of lengths -> n+1 offsets (dense output layout), on device."""
+    n = lengths.numel()
+    if out is None:
+        out = torch.empty(n + 1, dtype=torch.int64, device=lengths.device)
+    nbytes = lib().capnp_packed_scan_scratch_bytes(n)
+    scratch = torch.empty((nbytes + 7) // 8, dtype=torch.int64, device=lengths.device)
+    _raise(lib().capnp_packed_lengths_to_offsets(_ptr(lengths), n, base, _ptr(out), _ptr(scratch), nbytes,
+                                                 _stream(stream)), "lengths_to_offsets")
+    return out
+
+
+def generate(n_units: int, unit_bytes: int, seed: int, zero_thresh: int, unit_base: int = 0,
+             out=None, device="cuda", stream=None):
+    """Device-side synthetic units; twin of the oracle generator."""
+    if out is None:
+        out = torch.empty(n_units * unit_bytes, dtype=torch.uint8, device=device)
+    _raise(lib().capnp_packed_generate(_ptr(out), n_units, unit_bytes, unit_base, seed, zero_thresh,
+                                       _stream(stream)), "generate")
+    return out
+
+
+def uniform_layout(n_units: int, unit_bytes: int, device="cuda"):
+    """(offsets, lengths) of n equal units laid out densely; also the capacity-slot
+    layout of an encode output (unit_bytes = encode_bound(unit size))."""
+    off = torch.arange(0, n_units * unit_bytes, unit_bytes, dtype=torch.int64, device=device)
+    ln = torch.full((n_units,), unit_bytes, dtype=torch.int64, device=device)
+    return off, ln

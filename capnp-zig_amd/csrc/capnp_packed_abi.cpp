@@ -1,0 +1,278 @@
+// capnp_packed_abi.cpp — the C-ABI boundary (include/capnp_packed.h).
+//
+// Conventions follow the reference's only FFI, src/wasm/capnp_host_abi.zig:
+// integer status codes, a last-error message (:165-184), and a version query
+// (:60-70). Single-buffer calls run ONE unit through the GPU via a small
+// mutex-guarded device context; batch calls only enqueue kernels on the
+// caller's stream. There is no CPU code path: without a gfx950 device every
+// compute entry point returns CAPNP_PACKED_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "capnp_packed.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int status, const std::string& msg) {
+    g_last_error = msg;
+    return status;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(CAPNP_PACKED_DEVICE_ERROR, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+std::once_flag g_init_once;
+int g_init_status = CAPNP_PACKED_NO_DEVICE;
+std::string g_init_error;
+
+void device_init() {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) {
+        g_init_status = CAPNP_PACKED_NO_DEVICE;
+        g_init_error = "no HIP device visible";
+        return;
+    }
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) {
+        g_init_status = CAPNP_PACKED_DEVICE_ERROR;
+        g_init_error = std::string("hipGetDeviceProperties: ") + hipGetErrorString(e);
+        return;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_init_status = CAPNP_PACKED_NO_DEVICE;
+        g_init_error = std::string("device is ") + prop.gcnArchName + ", this library is built for gfx950 only";
+        return;
+    }
+    g_init_status = CAPNP_PACKED_OK;
+}
+
+int ensure_device() {
+    std::call_once(g_init_once, device_init);
+    if (g_init_status != CAPNP_PACKED_OK) return fail(g_init_status, g_init_error);
+    return CAPNP_PACKED_OK;
+}
+
+// Device context for the single-buffer host entry points.
+struct HostCtx {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    uint64_t* d_meta = nullptr;  // in_off[2], out_off[2], len, status(as u64)
+
+    int init() {
+        if (stream) return CAPNP_PACKED_OK;
+        hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        e = hipMalloc(&d_meta, 8 * sizeof(uint64_t));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(meta)");
+        return CAPNP_PACKED_OK;
+    }
+    int reserve(uint8_t** p, size_t* cap, size_t need) {
+        if (need <= *cap && *p) return CAPNP_PACKED_OK;
+        size_t want = need < 4096 ? 4096 : need + need / 2;
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        hipError_t e = hipMalloc(p, want);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+        *cap = want;
+        return CAPNP_PACKED_OK;
+    }
+};
+
+HostCtx g_ctx;
+
+// Run one unit through a batch kernel. kind: 0 encode, 1 decode, 2 decoded size, 3 encoded size.
+int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out) {
+    int st = g_ctx.init();
+    if (st) return st;
+    if ((st = g_ctx.reserve(&g_ctx.d_in, &g_ctx.in_cap, n + 16))) return st;
+    const bool write = (kind == 0 || kind == 1);
+    if (write && (st = g_ctx.reserve(&g_ctx.d_out, &g_ctx.out_cap, slot + 16))) return st;
+    uint64_t meta[6] = {0, n, 0, slot, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status
+    hipStream_t s = g_ctx.stream;
+    hipError_t e = hipSuccess;
+    if (n) e = hipMemcpyAsync(g_ctx.d_in, in, n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(g_ctx.d_meta, meta, sizeof(meta), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(H2D)");
+    uint64_t* m = g_ctx.d_meta;
+    int32_t* d_status = reinterpret_cast<int32_t*>(m + 5);
+    if (kind == 0 || kind == 3)
+        e = cpk::launch_encode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
+    else
+        e = cpk::launch_decode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    e = hipMemcpyAsync(meta, g_ctx.d_meta, sizeof(meta), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H)");
+    int32_t status;
+    std::memcpy(&status, &meta[5], sizeof(status));
+    *len_out = meta[4];
+    if (status == CAPNP_PACKED_OK && write && meta[4]) {
+        e = hipMemcpy(out, g_ctx.d_out, meta[4], hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy(D2H out)");
+    }
+    if (status != CAPNP_PACKED_OK) g_last_error = capnp_packed_status_name(status);
+    return status;
+}
+
+int check_batch(const void* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len, uint32_t n,
+                const uint64_t* d_len, const int32_t* d_status) {
+    if (n == 0) return CAPNP_PACKED_OK;
+    if (!d_in_off || !d_in_len || !d_len || !d_status) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null batch pointer");
+    (void)d_in;
+    return ensure_device();
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t capnp_packed_abi_version(void) { return CAPNP_PACKED_ABI_VERSION; }
+
+const char* capnp_packed_last_error(void) { return g_last_error.c_str(); }
+
+const char* capnp_packed_status_name(int status) {
+    switch (status) {
+        case CAPNP_PACKED_OK: return "Ok";
+        case CAPNP_PACKED_INVALID_MESSAGE_SIZE: return "InvalidMessageSize";
+        case CAPNP_PACKED_UNEXPECTED_EOF: return "UnexpectedEof";
+        case CAPNP_PACKED_OVERFLOW: return "Overflow";
+        case CAPNP_PACKED_OUT_OF_SPACE: return "OutOfSpace";
+        case CAPNP_PACKED_INVALID_ARGUMENT: return "InvalidArgument";
+        case CAPNP_PACKED_DEVICE_ERROR: return "DeviceError";
+        case CAPNP_PACKED_NO_DEVICE: return "NoDevice";
+        default: return "Unknown";
+    }
+}
+
+size_t capnp_packed_encode_bound(size_t n) { return 10 * (n / 8); }
+
+int capnp_packed_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!out_len) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "out_len is null");
+    *out_len = 0;
+    if ((n && !in) || (cap && !out)) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null buffer");
+    if (n % 8) return fail(CAPNP_PACKED_INVALID_MESSAGE_SIZE, "InvalidMessageSize");  // message.zig:201
+    int st = ensure_device();
+    if (st) return st;
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    size_t bound = capnp_packed_encode_bound(n);
+    uint64_t len = 0;
+    st = run_single(0, in, n, out, cap < bound ? cap : bound, &len);
+    *out_len = (size_t)len;
+    return st;
+}
+
+int capnp_packed_decoded_size(const uint8_t* in, size_t n, size_t* out_size) {
+    if (!out_size) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "out_size is null");
+    *out_size = 0;
+    if (n && !in) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null buffer");
+    int st = ensure_device();
+    if (st) return st;
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    uint64_t len = 0;
+    st = run_single(2, in, n, nullptr, 0, &len);
+    if (st == CAPNP_PACKED_OK) *out_size = (size_t)len;
+    return st;
+}
+
+int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!out_len) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "out_len is null");
+    *out_len = 0;
+    if ((n && !in) || (cap && !out)) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null buffer");
+    int st = ensure_device();
+    if (st) return st;
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    uint64_t need = 0;
+    st = run_single(2, in, n, nullptr, 0, &need);  // message.zig:90 size pass first
+    if (st != CAPNP_PACKED_OK) return st;
+    if (need > cap) {
+        *out_len = (size_t)need;
+        return fail(CAPNP_PACKED_OUT_OF_SPACE, "OutOfSpace");
+    }
+    uint64_t len = 0;
+    st = run_single(1, in, n, out, (size_t)need, &len);
+    *out_len = (size_t)len;
+    return st;
+}
+
+int capnp_packed_encode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                              uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                              uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
+    if (st || n == 0) return st;
+    if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
+    hipError_t e = cpk::launch_encode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                                      d_status, true, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "encode launch");
+}
+
+int capnp_packed_encoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
+    if (st || n == 0) return st;
+    hipError_t e = cpk::launch_encode(d_in, d_in_off, d_in_len, n, nullptr, nullptr, nullptr, d_out_len, d_status,
+                                      false, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "encode-size launch");
+}
+
+int capnp_packed_decode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                              uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                              uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
+    if (st || n == 0) return st;
+    if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
+    hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                                      d_status, true, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode launch");
+}
+
+int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
+    if (st || n == 0) return st;
+    hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, nullptr, nullptr, nullptr, d_out_len, d_status,
+                                      false, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode-size launch");
+}
+
+size_t capnp_packed_scan_scratch_bytes(uint32_t n) { return cpk::scan_scratch_bytes(n); }
+
+int capnp_packed_lengths_to_offsets(const uint64_t* d_len, uint32_t n, uint64_t base, uint64_t* d_off,
+                                    void* d_scratch, size_t scratch_bytes, void* stream) {
+    if (!d_off || !d_scratch || (n && !d_len)) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null pointer");
+    if (scratch_bytes < cpk::scan_scratch_bytes(n)) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "scratch too small");
+    int st = ensure_device();
+    if (st) return st;
+    hipError_t e = cpk::launch_scan(d_len, n, base, d_off, static_cast<uint64_t*>(d_scratch),
+                                    static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "scan launch");
+}
+
+int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
+                          uint64_t seed, uint32_t zero_thresh, void* stream) {
+    if (!d_out && n_units) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null d_out");
+    if (unit_bytes % 8) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "unit_bytes % 8 != 0");
+    int st = ensure_device();
+    if (st) return st;
+    hipError_t e = cpk::launch_generate(d_out, n_units, unit_bytes, unit_base, seed, zero_thresh,
+                                        static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "generate launch");
+}
+
+}  // extern "C"

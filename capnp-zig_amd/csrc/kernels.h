@@ -1,0 +1,26 @@
+// kernels.h — internal launcher interface between the C-ABI (capnp_packed_abi.cpp)
+// and the gfx950 kernels (packed_kernels.hip). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace cpk {
+
+hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                         uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
+                         int32_t* status, bool write, hipStream_t stream);
+
+hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                         uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
+                         int32_t* status, bool write, hipStream_t stream);
+
+hipError_t launch_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
+                           uint64_t seed, uint32_t thr, hipStream_t stream);
+
+size_t scan_scratch_bytes(uint32_t n);
+
+hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t* off, uint64_t* scratch,
+                       hipStream_t stream);
+
+}  // namespace cpk

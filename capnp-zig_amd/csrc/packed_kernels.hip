@@ -1,0 +1,923 @@
+// packed_kernels.hip — CDNA4 (gfx950) kernels for the Cap'n Proto packed codec.
+//
+// Reference semantics (Zig rules, NOT canonical C++ capnp):
+//   encode  nullstyle/capnp-zig src/serialization/message.zig:200-271 (packPacked)
+//   decode  message.zig:88-145 (unpackPacked) with the size pass of :152-191
+//
+// Execution model: one 64-lane wave owns one unit (one packPacked
+// / unpackPacked call). A unit is staged in the wave's private LDS slice with
+// coalesced 16-B global loads, processed with wave-wide scans, assembled in LDS
+// and written back with coalesced 16-B stores. No MFMA: this is byte compaction.
+//
+//   encode: lane j owns words [8j, 8j+8). Each word's zero-byte tag is formed
+//           with SWAR + a multiply gather; zero/literal runs (greedy, 256-capped)
+//           are resolved with wave max/min scans of break positions; a wave sum
+//           scan gives every lane its output byte offset; each lane appends its
+//           records to a byte stream in LDS (u64 ds_or at 8-B granularity).
+//   decode: the record chain (tag -> record length) is serial. Lanes walk
+//           64-byte chunks of the staged packed bytes speculatively from the
+//           chunk start; a fix-up loop re-walks lanes whose true entry point is
+//           not on their speculative chain (walks couple after a few records,
+//           so 1-2 rounds are typical, 64 worst case). Record starts become one
+//           u64 bitmask per lane; a wave sum scan of words-per-record gives
+//           output word offsets; mixed words are expanded with v_perm_b32 and a
+//           selector LUT; zero runs cost nothing (the LDS window is pre-zeroed).
+//
+// Units larger than the fast-path limits run a serial per-wave path (lane 0)
+// that reads and writes global memory directly (correct for any size; slow).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "capnp_packed.h"
+#include "kernels.h"
+
+namespace cpk {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+// ---- encode fast path ------------------------------------------------------
+constexpr uint32_t kEncMaxWords = 512;                 // 4 KiB unpacked unit
+constexpr uint32_t kEncRow = 80;                       // 64 B words + 16 B pad per lane row
+constexpr uint32_t kEncLds = 64 * kEncRow;             // 5120 B; reused for the packed output
+// max packed size of 512 words is 9*512+1 = 4609 B; + 16 B align slack + 16 B round-up <= 5120
+
+// ---- decode fast path ------------------------------------------------------
+constexpr uint32_t kDecIn = 4864;                      // staged packed bytes
+constexpr uint32_t kDecPMax = kDecIn - 16 - 32;        // 4816 B of packed input per unit
+constexpr uint32_t kDecWinWords = 512;                 // output window (words)
+constexpr uint32_t kDecOut = kDecWinWords * 8 + 16;    // 4112 B
+
+enum : int32_t {
+    ST_OK = CAPNP_PACKED_OK,
+    ST_SIZE = CAPNP_PACKED_INVALID_MESSAGE_SIZE,
+    ST_EOF = CAPNP_PACKED_UNEXPECTED_EOF,
+    ST_SPACE = CAPNP_PACKED_OUT_OF_SPACE,
+    ST_ARG = CAPNP_PACKED_INVALID_ARGUMENT,
+};
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+
+// Order LDS traffic between lanes of ONE wave (the wave owns its LDS slice).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, kWave);
+        if (lane >= (uint32_t)d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, kWave);
+        if (lane >= (uint32_t)d) v = max(v, t);
+    }
+    return v;
+}
+
+// inclusive min over lanes >= this lane
+__device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t t = __shfl_down(v, d, kWave);
+        if (lane + d < (uint32_t)kWave) v = min(v, t);
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
+    return __builtin_amdgcn_readlane(v, l);
+}
+
+// Zero-byte tag of a little-endian word: bit k set <=> byte k != 0
+// (message.zig:257-262 builds the same tag byte-by-byte).
+__device__ __forceinline__ uint32_t nonzero_tag32(uint32_t x) {
+    uint32_t y = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // byte high bit <=> byte != 0
+    return ((y & 0x80808080u) * 0x00204081u) >> 28;        // gather the 4 high bits
+}
+__device__ __forceinline__ uint32_t nonzero_tag(uint64_t w) {
+    return nonzero_tag32((uint32_t)w) | (nonzero_tag32((uint32_t)(w >> 32)) << 4);
+}
+
+// v_perm_b32 over the 8 bytes of d: selector byte r in 0..7 picks byte r, 0x0C gives 0.
+__device__ __forceinline__ uint64_t perm64(uint64_t d, uint64_t sel) {
+    uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
+    uint32_t a = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
+    uint32_t b = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+    return (uint64_t)a | ((uint64_t)b << 32);
+}
+
+// Selector that gathers the nonzero bytes of a word with tag t into bytes 0..popc-1.
+__device__ inline uint64_t compact_selector(uint32_t t) {
+    uint64_t sel = 0x0C0C0C0C0C0C0C0CULL;
+    int r = 0;
+    for (int k = 0; k < 8; ++k) {
+        if ((t >> k) & 1u) {
+            sel = (sel & ~(0xFFULL << (8 * r))) | ((uint64_t)k << (8 * r));
+            ++r;
+        }
+    }
+    return sel;
+}
+
+// Selector that scatters popc(t) packed bytes back to the set-bit positions of t.
+__device__ inline uint64_t expand_selector(uint32_t t) {
+    uint64_t sel = 0;
+    int r = 0;
+    for (int k = 0; k < 8; ++k) {
+        uint64_t s = 0x0C;
+        if ((t >> k) & 1u) s = (uint64_t)(r++);
+        sel |= s << (8 * k);
+    }
+    return sel;
+}
+
+// Unaligned 8-byte read from an LDS byte array (two aligned ds_read_b64 + funnel).
+__device__ __forceinline__ uint64_t lds_read_u64_unaligned(const uint8_t* base, uint32_t p) {
+    uint32_t a = p & ~7u;
+    uint64_t lo = *reinterpret_cast<const uint64_t*>(base + a);
+    uint64_t hi = *reinterpret_cast<const uint64_t*>(base + a + 8);
+    uint32_t sh = (p & 7u) * 8u;
+    return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+}
+
+// Per-lane byte stream into a zero-initialised LDS buffer. Every flushed u64 is
+// OR-ed (ds_or_b64) so the partial words a lane shares with its neighbours merge.
+struct LdsByteStream {
+    uint8_t* lds;
+    uint32_t addr;  // 8-aligned byte address of acc
+    uint32_t fill;  // bytes already in acc (0..7)
+    uint64_t acc;
+
+    __device__ __forceinline__ void init(uint8_t* base, uint32_t start) {
+        lds = base;
+        addr = start & ~7u;
+        fill = start & 7u;
+        acc = 0;
+    }
+    __device__ __forceinline__ void flush(uint64_t v) {
+        atomicOr(reinterpret_cast<unsigned long long*>(lds + addr), (unsigned long long)v);
+    }
+    // append k (<= 8) bytes held in the low bytes of v (bytes >= k must be zero)
+    __device__ __forceinline__ void put(uint64_t v, uint32_t k) {
+        if (k == 0) return;
+        uint32_t sh = fill * 8u;
+        uint64_t a = fill ? (acc | (v << sh)) : v;
+        uint32_t nf = fill + k;
+        if (nf >= 8) {
+            flush(a);
+            addr += 8;
+            acc = fill ? (v >> (64u - sh)) : 0;
+            fill = nf - 8;
+        } else {
+            acc = a;
+            fill = nf;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (fill) flush(acc);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Serial per-wave fallback (lane 0), any unit size. Restates message.zig
+// directly over global memory. Used for units beyond the fast-path limits.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t gload64(const uint8_t* p) {  // 8-aligned
+    return *reinterpret_cast<const uint64_t*>(p);
+}
+__device__ __forceinline__ int word_has_zero_byte(uint64_t v) {  // message.zig:196-198
+    return ((v - 0x0101010101010101ULL) & ~v & 0x8080808080808080ULL) != 0;
+}
+
+// message.zig:200-271; when out == nullptr only the size is computed.
+__device__ uint64_t serial_pack(const uint8_t* in, uint64_t words, uint8_t* out) {
+    uint64_t o = 0, i = 0;
+    while (i < words) {
+        uint64_t w = gload64(in + 8 * i);
+        if (w == 0) {
+            uint64_t run = 1;
+            while (run < 256 && i + run < words && gload64(in + 8 * (i + run)) == 0) ++run;
+            if (out) { out[o] = 0; out[o + 1] = (uint8_t)(run - 1); }
+            o += 2;
+            i += run;
+            continue;
+        }
+        if (!word_has_zero_byte(w)) {
+            uint64_t run = 1;
+            while (run < 256 && i + run < words && !word_has_zero_byte(gload64(in + 8 * (i + run)))) ++run;
+            if (out) {
+                out[o] = 0xFF;
+                for (int k = 0; k < 8; ++k) out[o + 1 + k] = (uint8_t)(w >> (8 * k));
+                out[o + 9] = (uint8_t)(run - 1);
+                for (uint64_t b = 0; b < 8 * (run - 1); ++b) out[o + 10 + b] = in[8 * (i + 1) + b];
+            }
+            o += 10 + 8 * (run - 1);
+            i += run;
+            continue;
+        }
+        uint32_t tag = 0, nz = 0;
+        for (int k = 0; k < 8; ++k) {
+            uint8_t b = (uint8_t)(w >> (8 * k));
+            if (b) {
+                tag |= 1u << k;
+                if (out) out[o + 1 + nz] = b;
+                ++nz;
+            }
+        }
+        if (out) out[o] = (uint8_t)tag;
+        o += 1 + nz;
+        i += 1;
+    }
+    return o;
+}
+
+// message.zig:152-191; returns ST_OK / ST_EOF and the decoded size.
+__device__ int32_t serial_decoded_size(const uint8_t* p, uint64_t n, uint64_t* size) {
+    uint64_t i = 0, total = 0;
+    while (i < n) {
+        uint32_t t = p[i++];
+        if (t == 0x00) {
+            if (i >= n) return ST_EOF;
+            total += 8 * (1 + (uint64_t)p[i++]);
+        } else if (t == 0xFF) {
+            if (i + 8 > n) return ST_EOF;
+            i += 8;
+            if (i >= n) return ST_EOF;
+            uint64_t c = p[i++];
+            if (i + 8 * c > n) return ST_EOF;
+            total += 8 * (1 + c);
+            i += 8 * c;
+        } else {
+            uint32_t k = __popc(t);
+            if (i + k > n) return ST_EOF;
+            total += 8;
+            i += k;
+        }
+    }
+    *size = total;
+    return ST_OK;
+}
+
+// message.zig:97-142 (input already validated by serial_decoded_size).
+__device__ void serial_unpack(const uint8_t* p, uint64_t n, uint8_t* out) {
+    uint64_t i = 0, o = 0;
+    while (i < n) {
+        uint32_t t = p[i++];
+        if (t == 0x00) {
+            uint64_t z = 8 * (1 + (uint64_t)p[i++]);
+            for (uint64_t b = 0; b < z; ++b) out[o + b] = 0;
+            o += z;
+        } else if (t == 0xFF) {
+            for (int b = 0; b < 8; ++b) out[o + b] = p[i + b];
+            o += 8;
+            i += 8;
+            uint64_t c = p[i++];
+            for (uint64_t b = 0; b < 8 * c; ++b) out[o + b] = p[i + b];
+            o += 8 * c;
+            i += 8 * c;
+        } else {
+            for (int k = 0; k < 8; ++k) out[o + k] = ((t >> k) & 1u) ? p[i++] : 0;
+            o += 8;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ENCODE
+// ---------------------------------------------------------------------------
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint64_t* __restrict__ in_len,
+                                                        uint32_t n, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint64_t* __restrict__ out_cap,
+                                                        uint64_t* __restrict__ out_len,
+                                                        int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * (WRITE ? kEncLds : kEncLds)];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    const uint32_t unit = blockIdx.x * kWavesPerBlock + wave;
+    if (unit >= n) return;
+    uint8_t* lds = smem + wave * kEncLds;
+
+    const uint64_t b0 = in_off[unit];
+    const uint64_t nbytes = in_len[unit];
+    uint64_t ob = 0, cap = 0;
+    int32_t st = ST_OK;
+    if (WRITE) {
+        ob = out_off[unit];
+        cap = out_cap[unit];
+    }
+    if (reinterpret_cast<uintptr_t>(in + b0) & 7) st = ST_ARG;
+    if (st == ST_OK && (nbytes & 7)) st = ST_SIZE;  // message.zig:201
+    if (st != ST_OK) {
+        if (lane == 0) { out_len[unit] = 0; status[unit] = st; }
+        return;
+    }
+    if (nbytes / 8 > kEncMaxWords) {
+        // serial fallback
+        if (lane == 0) {
+            uint64_t P = serial_pack(in + b0, nbytes / 8, nullptr);
+            int32_t s2 = ST_OK;
+            if (WRITE) {
+                if (P > cap) s2 = ST_SPACE;
+                else serial_pack(in + b0, nbytes / 8, out + ob);
+            }
+            out_len[unit] = P;
+            status[unit] = s2;
+        }
+        return;
+    }
+    const uint32_t words = (uint32_t)(nbytes >> 3);
+
+    // ---- stage the unit into LDS, word w at row (w>>3)*80 + (w&7)*8 ------------
+    {
+        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(in + b0) & 15);  // 0 or 8
+        const uint8_t* g = in + b0 - s;
+        const uint32_t nch = (s + (uint32_t)nbytes + 15) >> 4;
+        uint4 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch) v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch) {
+                if (s == 0) {
+                    uint32_t w = 2 * c;
+                    *reinterpret_cast<uint4*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = v[k];
+                } else {
+                    uint64_t lo = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+                    uint64_t hi = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+                    if (c > 0) {
+                        uint32_t w = 2 * c - 1;
+                        *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = lo;
+                    }
+                    uint32_t w = 2 * c;
+                    if (w < words) *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = hi;
+                }
+            }
+        }
+    }
+    wave_lds_sync();
+
+    // ---- lane j owns words [8j, 8j+8) ------------------------------------------
+    const uint32_t base = lane * 8;
+    const uint32_t nw = base < words ? min(8u, words - base) : 0u;
+    uint64_t w[8];
+    if (nw) {
+        const uint4* row = reinterpret_cast<const uint4*>(lds + lane * kEncRow);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint4 r = row[q];
+            w[2 * q] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+            w[2 * q + 1] = (uint64_t)r.z | ((uint64_t)r.w << 32);
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) w[t] = 0;
+    }
+
+    uint32_t tag[8];
+    uint32_t zmask = 0, fmask = 0;  // bit t: word t is all-zero / has no zero byte
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        tag[t] = nonzero_tag(w[t]);
+        if ((uint32_t)t < nw) {
+            if (tag[t] == 0) zmask |= 1u << t;
+            if (tag[t] == 0xFF) fmask |= 1u << t;
+        }
+    }
+    // break positions for the zero-run (Z) and literal-run (F) classes
+    uint32_t lbz = 0, lbf = 0, fbz = words, fbf = words;
+#pragma unroll
+    for (int t = 7; t >= 0; --t) {
+        uint32_t i = base + t;
+        if (!((zmask >> t) & 1u)) { lbz = max(lbz, i + 1); fbz = i; }
+        if (!((fmask >> t) & 1u)) { lbf = max(lbf, i + 1); fbf = i; }
+    }
+    fbz = min(fbz, words);
+    fbf = min(fbf, words);
+    // run start carried into this lane = last break before it (+1); run end = first break after it
+    uint32_t cz = __shfl_up(wave_incl_max(lbz, lane), 1, kWave);
+    uint32_t cf = __shfl_up(wave_incl_max(lbf, lane), 1, kWave);
+    uint32_t ez = __shfl_down(wave_incl_suffix_min(fbz, lane), 1, kWave);
+    uint32_t ef = __shfl_down(wave_incl_suffix_min(fbf, lane), 1, kWave);
+    if (lane == 0) { cz = 0; cf = 0; }
+    if (lane == 63) { ez = words; ef = words; }
+    ez = min(ez, words);
+    ef = min(ef, words);
+
+    uint32_t rs[8];  // run start of word t's class run (Z or F)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        uint32_t i = base + t;
+        rs[t] = ((zmask >> t) & 1u) ? cz : cf;
+        if (!((zmask >> t) & 1u)) cz = i + 1;
+        if (!((fmask >> t) & 1u)) cf = i + 1;
+    }
+    uint32_t re[8];  // run end (first break after word t) of its class
+#pragma unroll
+    for (int t = 7; t >= 0; --t) {
+        uint32_t i = base + t;
+        re[t] = ((zmask >> t) & 1u) ? ez : ef;
+        if (!((zmask >> t) & 1u)) ez = i;
+        if (!((fmask >> t) & 1u)) ef = i;
+    }
+    uint32_t sz[8], cnt[8];
+    uint32_t total = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        uint32_t i = base + t;
+        uint32_t head = ((i - rs[t]) & 255u) == 0;
+        cnt[t] = min(256u, re[t] - i) - 1;  // message.zig:214-223 / 236-245
+        uint32_t s;
+        if ((uint32_t)t >= nw) s = 0;
+        else if ((zmask >> t) & 1u) s = head ? 2 : 0;
+        else if ((fmask >> t) & 1u) s = head ? 10 : 8;
+        else s = 1 + __popc(tag[t]);
+        sz[t] = s;
+        total += s;
+    }
+    const uint32_t incl = wave_incl_sum(total, lane);
+    const uint32_t P = readlane(incl, 63);
+    const uint32_t o = incl - total;
+
+    if (!WRITE) {
+        if (lane == 0) { out_len[unit] = P; status[unit] = ST_OK; }
+        return;
+    }
+    if ((uint64_t)P > cap) {
+        if (lane == 0) { out_len[unit] = P; status[unit] = ST_SPACE; }
+        return;
+    }
+
+    // ---- assemble the packed bytes in LDS (reusing the staging slice) -------------
+    const uint32_t so = (uint32_t)(reinterpret_cast<uintptr_t>(out + ob) & 15);
+    const uint32_t nch_out = (so + P + 15) >> 4;
+    wave_lds_sync();  // every lane has its words in registers
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        uint32_t c = lane + 64 * k;
+        if (c < nch_out) *reinterpret_cast<uint4*>(lds + 16 * c) = make_uint4(0, 0, 0, 0);
+    }
+    wave_lds_sync();
+    {
+        LdsByteStream bs;
+        bs.init(lds, so + o);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (sz[t] == 0) continue;
+            if ((zmask >> t) & 1u) {
+                bs.put((uint64_t)cnt[t] << 8, 2);                       // 00 <count>
+            } else if ((fmask >> t) & 1u) {
+                if (sz[t] == 10) {                                       // FF w0..w7 <count>
+                    bs.put(0xFFULL | (w[t] << 8), 8);
+                    bs.put((w[t] >> 56) | ((uint64_t)cnt[t] << 8), 2);
+                } else {
+                    bs.put(w[t], 8);                                     // literal run body
+                }
+            } else {                                                     // tag + nonzero bytes
+                uint64_t comp = perm64(w[t], lut[tag[t]]);
+                bs.put((uint64_t)tag[t] | (comp << 8), sz[t]);
+            }
+        }
+        bs.finish();
+    }
+    wave_lds_sync();
+
+    // ---- coalesced write-back ------------------------------------------------------
+    {
+        uint8_t* gdst = out + ob - so;  // 16-B aligned
+        const uint32_t lo = so, hi = so + P;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch_out) {
+                uint32_t cb = 16 * c, ce = cb + 16;
+                if (cb >= lo && ce <= hi) {
+                    *reinterpret_cast<uint4*>(gdst + cb) = *reinterpret_cast<const uint4*>(lds + cb);
+                } else {
+                    uint32_t a = max(cb, lo), e = min(ce, hi);
+                    for (uint32_t b = a; b < e; ++b) gdst[b] = lds[b];
+                }
+            }
+        }
+    }
+    if (lane == 0) { out_len[unit] = P; status[unit] = ST_OK; }
+}
+
+// ---------------------------------------------------------------------------
+// DECODE
+// ---------------------------------------------------------------------------
+
+// Walk record starts of one 64-byte chunk [cs, ce) from entry e.
+// Record length: 00 -> 2, FF -> 10 + 8*count, other -> 1 + popc(tag)  (message.zig:152-191)
+__device__ __forceinline__ void walk_chunk(const uint8_t* lds, uint32_t e, uint32_t cs, uint32_t ce,
+                                           uint64_t& mask, uint32_t& exit_pos) {
+    uint32_t pos = e;
+    uint64_t m = 0;
+    while (pos < ce) {
+        m |= 1ULL << (pos - cs);
+        uint32_t t = lds[pos];
+        uint32_t len = (t == 0) ? 2u : (t == 0xFF ? 10u + 8u * (uint32_t)lds[pos + 9] : 1u + __popc(t));
+        pos += len;
+    }
+    mask = m;
+    exit_pos = pos;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint64_t* __restrict__ in_len,
+                                                        uint32_t n, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint64_t* __restrict__ out_cap,
+                                                        uint64_t* __restrict__ out_len,
+                                                        int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kWavesPerBlock * kDecIn];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[kWavesPerBlock * (WRITE ? kDecOut : 16)];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = expand_selector(threadIdx.x);
+        __syncthreads();
+    }
+    const uint32_t unit = blockIdx.x * kWavesPerBlock + wave;
+    if (unit >= n) return;
+    uint8_t* lin = s_in + wave * kDecIn;
+    uint8_t* lout = s_out + wave * (WRITE ? kDecOut : 16);
+
+    const uint64_t b0 = in_off[unit];
+    uint64_t ob = 0, cap = 0;
+    int32_t st = ST_OK;
+    if (WRITE) {
+        ob = out_off[unit];
+        cap = out_cap[unit];
+        if (reinterpret_cast<uintptr_t>(out + ob) & 7) st = ST_ARG;
+    }
+    if (st != ST_OK) {
+        if (lane == 0) { out_len[unit] = 0; status[unit] = st; }
+        return;
+    }
+    const uint64_t P64 = in_len[unit];
+    if (P64 > kDecPMax) {
+        if (lane == 0) {
+            uint64_t U = 0;
+            int32_t s2 = serial_decoded_size(in + b0, P64, &U);
+            if (s2 != ST_OK) U = 0;
+            else if (WRITE) {
+                if (U > cap) s2 = ST_SPACE;
+                else serial_unpack(in + b0, P64, out + ob);
+            }
+            out_len[unit] = U;
+            status[unit] = s2;
+        }
+        return;
+    }
+    const uint32_t P = (uint32_t)P64;
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(in + b0) & 15);
+    const uint32_t end = s + P;
+
+    // ---- stage packed bytes (16-B aligned chunks; bytes outside [s, end) are ignored)
+    {
+        const uint8_t* g = in + b0 - s;
+        const uint32_t nch = (end + 15) >> 4;
+        uint4 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch) v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch) *reinterpret_cast<uint4*>(lin + 16 * c) = v[k];
+        }
+    }
+    wave_lds_sync();
+
+    // ---- record discovery: speculative chunk walks + fix-up ---------------------------
+    const uint32_t nc = (P + 63) >> 6;  // 64-byte chunks (<= 76)
+    uint64_t m[2] = {0, 0};
+    uint32_t carry = s;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        if ((uint32_t)(64 * r) >= nc) break;
+        const uint32_t c = 64 * r + lane;
+        const bool active = c < nc;
+        const uint32_t cs = s + 64 * c;
+        const uint32_t ce = min(cs + 64, end);
+        uint64_t mask = 0;
+        uint32_t ex = cs;
+        if (active) walk_chunk(lin, lane == 0 ? carry : cs, cs, ce, mask, ex);
+        uint32_t entry = carry;
+        for (int it = 0; it < 66; ++it) {
+            uint32_t prev = __shfl_up(ex, 1, kWave);
+            entry = (lane == 0) ? carry : prev;
+            bool ok = true;
+            if (active) {
+                if (entry >= ce) ok = (mask == 0 && ex == entry);
+                else ok = (entry >= cs) && ((mask >> (entry - cs)) & 1ULL);
+            }
+            if (__all(ok)) break;
+            if (!ok) walk_chunk(lin, entry, cs, ce, mask, ex);
+        }
+        if (active && entry < ce && entry > cs) mask &= ~0ULL << (entry - cs);
+        m[r] = mask;
+        const uint32_t last = min(nc - 64 * r, 64u) - 1;
+        carry = readlane(ex, last);
+    }
+    const bool eof = (carry != end);  // the record chain must end exactly at the last byte
+
+    // ---- words per lane, output word offsets ----------------------------------------
+    uint32_t wc[2] = {0, 0};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        uint64_t bits = m[r];
+        const uint32_t cs = s + 64 * (64 * r + lane);
+        while (bits) {
+            uint32_t b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            uint32_t pos = cs + b;
+            uint32_t t = lin[pos];
+            wc[r] += (t == 0) ? 1u + lin[pos + 1] : (t == 0xFF ? 1u + lin[pos + 9] : 1u);
+        }
+    }
+    const uint32_t inc0 = wave_incl_sum(wc[0], lane);
+    const uint32_t tot0 = readlane(inc0, 63);
+    const uint32_t inc1 = wave_incl_sum(wc[1], lane);
+    const uint32_t W = tot0 + readlane(inc1, 63);
+    const uint32_t wbase[2] = {inc0 - wc[0], tot0 + inc1 - wc[1]};
+
+    if (eof) {
+        if (lane == 0) { out_len[unit] = 0; status[unit] = ST_EOF; }
+        return;
+    }
+    const uint64_t U = 8ULL * W;
+    if (!WRITE) {
+        if (lane == 0) { out_len[unit] = U; status[unit] = ST_OK; }
+        return;
+    }
+    if (U > cap) {
+        if (lane == 0) { out_len[unit] = U; status[unit] = ST_SPACE; }
+        return;
+    }
+
+    // ---- expansion, one 512-word output window at a time -------------------------------
+    const uint32_t so = (uint32_t)(reinterpret_cast<uintptr_t>(out + ob) & 15);  // 0 or 8
+    for (uint32_t win = 0; win < W; win += kDecWinWords) {
+        const uint32_t nwin = min(kDecWinWords, W - win);
+        const uint32_t nbytes = so + 8 * nwin;
+        const uint32_t nch = (nbytes + 15) >> 4;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch) *reinterpret_cast<uint4*>(lout + 16 * c) = make_uint4(0, 0, 0, 0);
+        }
+        wave_lds_sync();
+        const uint32_t wend = win + nwin;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            uint64_t bits = m[r];
+            const uint32_t cs = s + 64 * (64 * r + lane);
+            uint32_t wo = wbase[r];
+            while (bits && wo < wend) {
+                uint32_t b = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                uint32_t pos = cs + b;
+                uint32_t t = lin[pos];
+                if (t == 0) {
+                    wo += 1u + lin[pos + 1];                         // zero run: window is pre-zeroed
+                } else if (t == 0xFF) {
+                    uint32_t c = lin[pos + 9];
+                    uint32_t k0 = wo < win ? win - wo : 0u;
+                    uint32_t k1 = min(c + 1, wend - wo);
+                    for (uint32_t k = k0; k < k1; ++k) {
+                        uint32_t src = k == 0 ? pos + 1 : pos + 10 + 8 * (k - 1);
+                        *reinterpret_cast<uint64_t*>(lout + so + 8 * (wo + k - win)) =
+                            lds_read_u64_unaligned(lin, src);
+                    }
+                    wo += 1 + c;
+                } else {
+                    if (wo >= win) {
+                        uint64_t d = lds_read_u64_unaligned(lin, pos + 1);
+                        *reinterpret_cast<uint64_t*>(lout + so + 8 * (wo - win)) = perm64(d, lut[t]);
+                    }
+                    wo += 1;
+                }
+            }
+        }
+        wave_lds_sync();
+        uint8_t* gdst = out + ob + 8ULL * win - so;  // 16-B aligned
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t c = lane + 64 * k;
+            if (c < nch) {
+                uint32_t cb = 16 * c;
+                if (cb >= so && cb + 16 <= nbytes) {
+                    *reinterpret_cast<uint4*>(gdst + cb) = *reinterpret_cast<const uint4*>(lout + cb);
+                } else {  // one valid 8-byte half
+                    uint32_t h = cb < so ? cb + 8 : cb;
+                    *reinterpret_cast<uint64_t*>(gdst + h) = *reinterpret_cast<const uint64_t*>(lout + h);
+                }
+            }
+        }
+        wave_lds_sync();
+    }
+    if (lane == 0) { out_len[unit] = U; status[unit] = ST_OK; }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic generator and offset scan
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t seed, uint64_t unit, uint64_t word) {
+    uint64_t x = seed ^ (unit * 0x9E3779B97F4A7C15ULL) ^ (word * 0xC2B2AE3D27D4EB4FULL);
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__global__ void generate_kernel(uint8_t* __restrict__ out, uint64_t n_units, uint64_t words_per_unit,
+                                uint64_t unit_base, uint64_t seed, uint32_t thr) {
+    const uint64_t total = n_units * words_per_unit;
+    for (uint64_t gw = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gw < total;
+         gw += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t u = gw / words_per_unit, w = gw - u * words_per_unit;
+        uint64_t h = mix64(seed, unit_base + u, w);
+        uint64_t h2 = mix64(seed ^ 0xA5A5A5A5A5A5A5A5ULL, unit_base + u, w);
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            uint32_t r = (uint32_t)(h >> (8 * k)) & 0xFF;
+            uint32_t x = (uint32_t)(h2 >> (8 * k)) & 0xFF;
+            uint64_t b = (r < thr) ? 0 : (1 + x % 255);
+            v |= b << (8 * k);
+        }
+        *reinterpret_cast<uint64_t*>(out + 8 * gw) = v;
+    }
+}
+
+constexpr int kScanItems = 8;
+constexpr int kScanTile = 256 * kScanItems;
+
+// block-local exclusive scan of u64 lengths; writes the block total to partial[blockIdx.x]
+__global__ __launch_bounds__(256) void scan_local_kernel(const uint64_t* __restrict__ len, uint32_t n,
+                                                         uint64_t* __restrict__ off,
+                                                         uint64_t* __restrict__ partial) {
+    __shared__ uint64_t wsum[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + tid * kScanItems;
+    uint64_t v[kScanItems];
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = (base + k < n) ? len[base + k] : 0;
+        t += v[k];
+    }
+    uint64_t x = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t pre = 0;
+    for (uint32_t q = 0; q < wave; ++q) pre += wsum[q];
+    uint64_t run = pre + x - t;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        if (base + k < n) off[base + k] = run;
+        run += v[k];
+    }
+    if (tid == 255) partial[blockIdx.x] = pre + x;
+}
+
+// single-block exclusive scan of the partials (in place), then base added
+__global__ __launch_bounds__(1024) void scan_partials_kernel(uint64_t* __restrict__ partial, uint32_t np,
+                                                             uint64_t base, uint64_t* __restrict__ off_last,
+                                                             uint32_t n) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry_s;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) carry_s = base;
+    __syncthreads();
+    for (uint32_t b = 0; b < np; b += 1024) {
+        uint64_t v = (b + tid < np) ? partial[b + tid] : 0;
+        uint64_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint64_t pre = carry_s;
+        for (uint32_t q = 0; q < wave; ++q) pre += wsum[q];
+        if (b + tid < np) partial[b + tid] = pre + x - v;
+        __syncthreads();
+        if (tid == 1023) carry_s = pre + x;
+        __syncthreads();
+    }
+    if (tid == 0) off_last[n] = carry_s;
+}
+
+__global__ __launch_bounds__(256) void scan_apply_kernel(uint64_t* __restrict__ off, uint32_t n,
+                                                         const uint64_t* __restrict__ partial) {
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    const uint64_t add = partial[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < n) off[base + k] += add;
+}
+
+}  // namespace cpk
+
+// ---------------------------------------------------------------------------
+// launchers (kernels.h)
+// ---------------------------------------------------------------------------
+namespace cpk {
+
+static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) / kWavesPerBlock; }
+
+hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                         uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
+                         int32_t* status, bool write, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (write)
+        encode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                   out_len, status);
+    else
+        encode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                    out_len, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                         uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
+                         int32_t* status, bool write, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (write)
+        decode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                   out_len, status);
+    else
+        decode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                    out_len, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
+                           uint64_t seed, uint32_t thr, hipStream_t stream) {
+    const uint64_t total = n_units * (unit_bytes / 8);
+    if (total == 0) return hipSuccess;
+    uint64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    generate_kernel<<<(uint32_t)blocks, 256, 0, stream>>>(out, n_units, unit_bytes / 8, unit_base, seed, thr);
+    return hipGetLastError();
+}
+
+size_t scan_scratch_bytes(uint32_t n) {
+    return ((size_t)(n + kScanTile - 1) / kScanTile + 1) * sizeof(uint64_t);
+}
+
+hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t* off, uint64_t* scratch,
+                       hipStream_t stream) {
+    const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+    if (n == 0) {
+        scan_partials_kernel<<<1, 1024, 0, stream>>>(scratch, 0, base, off, 0);
+        return hipGetLastError();
+    }
+    scan_local_kernel<<<nb, 256, 0, stream>>>(len, n, off, scratch);
+    scan_partials_kernel<<<1, 1024, 0, stream>>>(scratch, nb, base, off, n);
+    scan_apply_kernel<<<nb, 256, 0, stream>>>(off, n, scratch);
+    return hipGetLastError();
+}
+
+}  // namespace cpk

@@ -1,0 +1,151 @@
+/*
+ * capnp_packed.h — C-ABI of the MI355X-native Cap'n Proto *packed* codec.
+ *
+ * This is the drop-in boundary for the reference's packed read/write surface
+ * (nullstyle/capnp-zig, src/serialization/message.zig). Every entry point below
+ * names the reference function it replaces. The reference functions are
+ * file-private Zig functions; INTEGRATION.md shows the `extern fn` binding and the
+ * three-line patch a maintainer applies to message.zig to route them here.
+ *
+ * Signatures use plain pointers, sizes and an opaque stream handle only.
+ *
+ * Codec rules are the Zig rules (NOT canonical C++ capnp): see DESIGN.md §1.
+ *
+ * Ownership: the caller owns every buffer. Output capacity is passed in; the
+ * library never allocates caller-visible memory. A Zig caller allocates
+ * `capnp_packed_encode_bound(n)` (or the size from `capnp_packed_decoded_size`)
+ * and shrinks with `allocator.realloc`, which keeps Zig's exact-length free
+ * contract (message.zig:144/270 `toOwnedSlice`).
+ *
+ * Threading: all functions are thread-safe. The single-buffer host functions
+ * serialise on one internal device context; batch functions are reentrant for
+ * distinct streams. One-time device init is guarded by std::call_once.
+ */
+#ifndef CAPNP_PACKED_H
+#define CAPNP_PACKED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAPNP_PACKED_ABI_VERSION 1u
+
+/* Status codes. The first four mirror the reference's error set
+ * (message.zig:201 InvalidMessageSize, :105/:115/:121/:127/:137 UnexpectedEof,
+ * :163/:168 Overflow, allocator OutOfMemory -> OUT_OF_SPACE because the caller
+ * supplies capacity). */
+enum capnp_packed_status {
+    CAPNP_PACKED_OK = 0,
+    CAPNP_PACKED_INVALID_MESSAGE_SIZE = 1, /* encode input length % 8 != 0 (message.zig:201) */
+    CAPNP_PACKED_UNEXPECTED_EOF = 2,       /* truncated packed input (message.zig:152-191) */
+    CAPNP_PACKED_OVERFLOW = 3,             /* decoded size overflows size_t (message.zig:163); unreachable for < 2^60-byte inputs */
+    CAPNP_PACKED_OUT_OF_SPACE = 4,         /* output capacity too small; *out_len holds the required size */
+    CAPNP_PACKED_INVALID_ARGUMENT = 5,     /* null pointer, decreasing offsets, or a misaligned word-side offset */
+    CAPNP_PACKED_DEVICE_ERROR = 6,         /* HIP runtime error; see capnp_packed_last_error() */
+    CAPNP_PACKED_NO_DEVICE = 7             /* no gfx950 device / HIP code object not loadable */
+};
+
+/* Version / capability query (precedent: src/wasm/capnp_host_abi.zig:60-70). */
+uint32_t capnp_packed_abi_version(void);
+
+/* Message of the last failing call on this thread (precedent:
+ * capnp_host_abi.zig:165-184 last-error). Never NULL. */
+const char* capnp_packed_last_error(void);
+
+/* Name of a status code, e.g. "UnexpectedEof" (the reference's error names). */
+const char* capnp_packed_status_name(int status);
+
+/* Upper bound on the packed size of an n-byte input: 10 * (n / 8).
+ * Replaces the implicit growth of std.ArrayList in packPacked (message.zig:204-270). */
+size_t capnp_packed_encode_bound(size_t n);
+
+/* ------------------------------------------------------------------------
+ * Single-buffer functions on HOST memory (one unit through the GPU).
+ * ------------------------------------------------------------------------ */
+
+/* Replaces `fn packPacked(allocator, bytes) ![]u8` (message.zig:200-271).
+ * Writes the packed bytes to out[0..*out_len). On OUT_OF_SPACE, *out_len is the
+ * required size and out is untouched. */
+int capnp_packed_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+
+/* Replaces `fn estimateUnpackedSize(packed) !usize` (message.zig:152-191). */
+int capnp_packed_decoded_size(const uint8_t* in, size_t n, size_t* out_size);
+
+/* Replaces `fn unpackPacked(allocator, packed) ![]u8` (message.zig:88-145).
+ * Errors are raised before any output byte is written, as in the reference
+ * (size pass first). On OUT_OF_SPACE, *out_len is the required size. */
+int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+
+/* ------------------------------------------------------------------------
+ * Batch functions on DEVICE memory (the hot path).
+ *
+ * A batch is n independent units. Unit i's input is
+ *   d_in[d_in_off[i] .. d_in_off[i] + d_in_len[i])
+ * and its output goes to the capacity slot
+ *   d_out[d_out_off[i] .. d_out_off[i] + d_out_cap[i])
+ * d_out_len[i] receives the produced (or, on OUT_OF_SPACE, required) length and
+ * d_status[i] the unit's status. All arrays have n entries and live in device
+ * memory; offsets/lengths are u64 bytes. Because lengths are separate arrays,
+ * an encode's d_out_off/d_out_len can be passed unchanged as a decode's
+ * d_in_off/d_in_len (decode straight from the capacity slots), and dense
+ * streams come from capnp_packed_lengths_to_offsets.
+ *
+ * Word-side alignment: the unpacked side of every unit (encode input, decode
+ * output) must start at a multiple of 8 bytes (INVALID_ARGUMENT otherwise); the
+ * packed side may start anywhere (dense packed streams are supported).
+ *
+ * `stream` is a hipStream_t (NULL = default stream). Calls are asynchronous:
+ * they enqueue kernels and return. The return value reports launch errors only;
+ * per-unit results are in d_status / d_out_len. Nothing is allocated inside, so
+ * the calls can be captured in a hipGraph.
+ * ------------------------------------------------------------------------ */
+
+/* Batch packPacked (message.zig:200-271), one unit = one packPacked call. */
+int capnp_packed_encode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                              uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                              const uint64_t* d_out_cap, uint64_t* d_out_len, int32_t* d_status,
+                              void* stream);
+
+/* Packed sizes only (no output written): the first half of a dense encode
+ * (sizes -> exclusive scan -> capnp_packed_encode_batch with dense offsets). */
+int capnp_packed_encoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Batch unpackPacked (message.zig:88-145). */
+int capnp_packed_decode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                              uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                              const uint64_t* d_out_cap, uint64_t* d_out_len, int32_t* d_status,
+                              void* stream);
+
+/* Batch estimateUnpackedSize (message.zig:152-191). */
+int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Exclusive scan of n lengths into n+1 offsets (d_off[0] = base, d_off[n] =
+ * base + total), on device.
+ * Turns capnp_packed_*_size_batch results into dense output offsets. The
+ * caller supplies device scratch of capnp_packed_scan_scratch_bytes(n) bytes
+ * (no allocation inside, so the call can be captured in a hipGraph). */
+size_t capnp_packed_scan_scratch_bytes(uint32_t n);
+int capnp_packed_lengths_to_offsets(const uint64_t* d_len, uint32_t n, uint64_t base,
+                                    uint64_t* d_off, void* d_scratch, size_t scratch_bytes,
+                                    void* stream);
+
+/* Synthetic unit generator used by the benchmark and the parity tests:
+ * n units of unit_bytes each, laid out densely from d_out (unit i at
+ * i*unit_bytes). Byte k of word w of global unit u = unit_base + i is
+ *   h  = mix64(seed, u, w); h2 = mix64(seed ^ 0xA5A5..., u, w)
+ *   b  = ((h >> 8k) & 0xFF) < zero_thresh ? 0 : 1 + (((h2 >> 8k) & 0xFF) % 255)
+ * i.e. zero with probability zero_thresh/256. */
+int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
+                          uint64_t unit_base, uint64_t seed, uint32_t zero_thresh,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CAPNP_PACKED_H */

@@ -1,0 +1,69 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol that
+include/capnp_packed.h declares, and refuses to compute without a device
+(there is no CPU fallback in the product path)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import capnp_packed as cp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "capnp_packed.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(capnp_packed_\w+)\s*\(", text)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ("capnp_packed_encode", "capnp_packed_decode", "capnp_packed_decoded_size",
+                 "capnp_packed_encode_batch", "capnp_packed_decode_batch", "capnp_packed_encode_bound"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = cp.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert set(declared_functions()) == set(cp.SIGNATURES), "ctypes signature table out of sync with header"
+
+
+def test_exports_are_c_symbols():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", cp.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for name in declared_functions():
+        assert name in exported, f"{name} not exported unmangled"
+
+
+def test_version_and_status_names():
+    assert cp.lib().capnp_packed_abi_version() == 1
+    names = [cp.lib().capnp_packed_status_name(i).decode() for i in range(8)]
+    assert names == ["Ok", "InvalidMessageSize", "UnexpectedEof", "Overflow", "OutOfSpace",
+                     "InvalidArgument", "DeviceError", "NoDevice"]
+    assert cp.encode_bound(4096) == 5120 and cp.encode_bound(0) == 0
+
+
+def test_gfx950_code_object_present():
+    blob = open(cp.LIB_PATH, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob  # the offload bundle carries a gfx950 code object
+
+
+def test_argument_validation_without_device():
+    n = ctypes.c_size_t(123)
+    assert cp.lib().capnp_packed_encode(None, 8, None, 0, ctypes.byref(n)) == cp.INVALID_ARGUMENT
+    assert n.value == 0
+    assert cp.lib().capnp_packed_encode(b"1234567", 7, None, 0, ctypes.byref(n)) == cp.INVALID_MESSAGE_SIZE
+
+
+@pytest.mark.skipif(__import__("torch").cuda.is_available(), reason="checks the no-device behaviour")
+def test_no_cpu_fallback_without_device():
+    with pytest.raises(cp.NoDevice):
+        cp.pack_packed(bytes(16))
+    with pytest.raises(cp.NoDevice):
+        cp.unpack_packed(b"\x00\x00")
