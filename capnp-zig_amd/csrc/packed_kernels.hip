@@ -27,6 +27,7 @@
 // that reads and writes global memory directly (correct for any size; slow).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "capnp_packed.h"
 #include "kernels.h"
@@ -152,6 +153,26 @@ __device__ __forceinline__ uint64_t lds_read_u64_unaligned(const uint8_t* base, 
     uint64_t hi = *reinterpret_cast<const uint64_t*>(base + a + 8);
     uint32_t sh = (p & 7u) * 8u;
     return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+}
+
+// Stage nch 16-B chunks from global g[0 .. 16*nch) into lds[0 .. 16*nch):
+// lane l moves chunks l, l+64, ... All K loads are issued before the first LDS
+// store (addresses clamped to the last chunk, guards wave-uniform) so they stay
+// in VGPRs and overlap in flight.
+template <int K>
+__device__ __forceinline__ void stage_linear(uint8_t* lds, const uint8_t* g, uint32_t nch, uint32_t lane) {
+    if (nch == 0) return;
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {  // unconditional: clamped lanes re-read the last chunk (same line)
+        uint32_t c = min(lane + 64u * k, nch - 1);
+        v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint32_t c = lane + 64u * k;
+        if ((uint32_t)(64 * k) < nch && c < nch) *reinterpret_cast<uint4*>(lds + 16 * c) = v[k];
+    }
 }
 
 // Per-lane byte stream into a zero-initialised LDS buffer. Every flushed u64 is
@@ -359,13 +380,15 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
         uint4 v[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            uint32_t c = lane + 64 * k;
-            if (c < nch) v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
+            if ((uint32_t)(64 * k) < nch) {
+                uint32_t c = min(lane + 64u * k, nch - 1);
+                v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
+            }
         }
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             uint32_t c = lane + 64 * k;
-            if (c < nch) {
+            if ((uint32_t)(64 * k) < nch && c < nch) {
                 if (s == 0) {
                     uint32_t w = 2 * c;
                     *reinterpret_cast<uint4*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = v[k];
@@ -605,21 +628,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
     const uint32_t end = s + P;
 
     // ---- stage packed bytes (16-B aligned chunks; bytes outside [s, end) are ignored)
-    {
-        const uint8_t* g = in + b0 - s;
-        const uint32_t nch = (end + 15) >> 4;
-        uint4 v[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            uint32_t c = lane + 64 * k;
-            if (c < nch) v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
-        }
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            uint32_t c = lane + 64 * k;
-            if (c < nch) *reinterpret_cast<uint4*>(lin + 16 * c) = v[k];
-        }
-    }
+    stage_linear<5>(lin, in + b0 - s, (end + 15) >> 4, lane);
     wave_lds_sync();
 
     // ---- record discovery: speculative chunk walks + fix-up ---------------------------
@@ -754,6 +763,295 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// DECODE, lane per unit
+// ---------------------------------------------------------------------------
+// The record chain (tag -> record length) is inherently serial and speculative
+// chunk walks couple with it too slowly on packed data, so each
+// lane owns ONE unit and walks its chain exactly once, expanding every record as
+// it is found. The lane keeps a sliding window of its packed bytes in registers:
+// a 32-byte view (q0..q3) plus one 16-byte piece in flight (n0, n1). A CU holds
+// thousands of units in flight, which hides the memory latency of each lane's
+// dependent chain.
+
+// View helpers take the window by value so the selects stay register selects
+// (members selected through `this` were turned into an indexed alloca in LDS).
+__device__ __forceinline__ uint32_t view_byte(uint64_t q0, uint64_t q1, uint64_t q2, uint64_t q3, uint32_t o) {
+    uint64_t a = (o & 8) ? q1 : q0;  // o < 32
+    uint64_t b = (o & 8) ? q3 : q2;
+    uint64_t q = (o & 16) ? b : a;
+    return (uint32_t)(q >> (8 * (o & 7))) & 0xFFu;
+}
+__device__ __forceinline__ uint64_t view_word8(uint64_t q0, uint64_t q1, uint64_t q2, uint64_t q3, uint32_t o) {
+    // 8 bytes at view offset o, o <= 24
+    uint32_t i = o >> 3;
+    uint64_t lo = (i == 0) ? q0 : ((i == 1) ? q1 : q2);
+    uint64_t hi = (i == 0) ? q1 : ((i == 1) ? q2 : q3);
+    uint32_t sh = 8 * (o & 7);
+    return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+}
+__device__ __forceinline__ void load_piece(const uint8_t* base, uint32_t npieces, uint32_t idx, uint64_t& a,
+                                           uint64_t& b) {
+    if (idx < npieces) {
+        uint4 v = *reinterpret_cast<const uint4*>(base + 16 * (uint64_t)idx);
+        a = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        b = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    } else {
+        a = 0;
+        b = 0;
+    }
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len,
+                                                             uint32_t n, uint8_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ out_off,
+                                                             const uint64_t* __restrict__ out_cap,
+                                                             uint64_t* __restrict__ out_len,
+                                                             int32_t* __restrict__ status) {
+    __shared__ uint64_t lut[256];
+    if (WRITE) {
+        lut[threadIdx.x] = expand_selector(threadIdx.x);
+        __syncthreads();
+    }
+    const uint32_t unit = blockIdx.x * kBlock + threadIdx.x;
+    if (unit >= n) return;
+    const uint8_t* src = in + in_off[unit];
+    const uint64_t P = in_len[unit];
+    uint64_t* dst = nullptr;
+    uint64_t capw = 0;
+    if (WRITE) {
+        uint8_t* o = out + out_off[unit];
+        if (reinterpret_cast<uintptr_t>(o) & 7) {
+            out_len[unit] = 0;
+            status[unit] = ST_ARG;
+            return;
+        }
+        dst = reinterpret_cast<uint64_t*>(o);
+        capw = out_cap[unit] >> 3;
+    }
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint64_t end64 = s + P;
+    const uint8_t* base = src - s;
+    const uint32_t npieces = (uint32_t)((end64 + 15) >> 4);
+    // window: q0..q3 = pieces wb/16, wb/16+1; n0,n1 = piece wb/16+2 (in flight)
+    uint64_t q0, q1, q2, q3, n0, n1;
+    uint32_t wb = 0;
+    load_piece(base, npieces, 0, q0, q1);
+    load_piece(base, npieces, 1, q2, q3);
+    load_piece(base, npieces, 2, n0, n1);
+    auto ensure = [&](uint32_t p) {
+        while (p - wb >= 16) {
+            q0 = q2; q1 = q3; q2 = n0; q3 = n1;
+            wb += 16;
+            load_piece(base, npieces, (wb >> 4) + 2, n0, n1);
+        }
+    };
+    uint64_t pos = s;
+    uint64_t wo = 0;
+    int32_t st = ST_OK;
+    auto put = [&](uint64_t w) {
+        if (WRITE && wo < capw) dst[wo] = w;
+        ++wo;
+    };
+    while (pos < end64) {
+        ensure((uint32_t)pos);
+        const uint32_t o = (uint32_t)pos - wb;
+        const uint32_t t = view_byte(q0, q1, q2, q3, o);
+        if (t == 0x00) {  // message.zig:101-110
+            if (pos + 2 > end64) { st = ST_EOF; break; }
+            const uint32_t c = view_byte(q0, q1, q2, q3, o + 1);
+            for (uint32_t k = 0; k <= c; ++k) put(0);
+            pos += 2;
+        } else if (t == 0xFF) {  // message.zig:112-128
+            if (pos + 10 > end64) { st = ST_EOF; break; }
+            const uint64_t w = view_word8(q0, q1, q2, q3, o + 1);
+            const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
+            if (pos + 10 + 8ULL * c > end64) { st = ST_EOF; break; }
+            put(w);
+            pos += 10;
+            for (uint32_t k = 0; k < c; ++k) {
+                ensure((uint32_t)pos);
+                put(view_word8(q0, q1, q2, q3, (uint32_t)pos - wb));
+                pos += 8;
+            }
+        } else {  // message.zig:131-141
+            const uint32_t k = __popc(t);
+            if (pos + 1 + k > end64) { st = ST_EOF; break; }
+            if (WRITE) put(perm64(view_word8(q0, q1, q2, q3, o + 1), lut[t]));
+            else put(0);
+            pos += 1 + k;
+        }
+    }
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    const uint64_t U = 8 * wo;
+    out_len[unit] = U;
+    status[unit] = (WRITE && wo > capw) ? ST_SPACE : ST_OK;
+}
+
+// ---------------------------------------------------------------------------
+// DECODE, lane per unit, lockstep output rounds (the production decoder)
+// ---------------------------------------------------------------------------
+// Lane l of a wave owns unit wave_base + l and walks its record chain exactly
+// once (input side: per-lane register window, as in decode_lane_kernel). The
+// OUTPUT side is made regular: in every round each live lane emits exactly
+// kRoundWords words (one 128-B line) into its row of an LDS ring; zero runs and
+// literal runs that cross a round boundary carry over as pending counts. After
+// each round the wave stores the ring cooperatively: 8 lanes per 128-B line,
+// 8 lines per store instruction (fully coalesced), instead of 64 scattered
+// 8-byte stores per instruction.
+constexpr int kRoundWords = 16;                 // 128 B of output per lane per round
+constexpr int kRingRow = kRoundWords * 8 + 16;  // 144 B: 16-B aligned, staggers LDS banks
+constexpr int kStreamWaves = 2;                 // waves per block
+constexpr int kStreamBlock = kStreamWaves * kWave;
+
+__global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8_t* __restrict__ in,
+                                                                     const uint64_t* __restrict__ in_off,
+                                                                     const uint64_t* __restrict__ in_len,
+                                                                     uint32_t n, uint8_t* __restrict__ out,
+                                                                     const uint64_t* __restrict__ out_off,
+                                                                     const uint64_t* __restrict__ out_cap,
+                                                                     uint64_t* __restrict__ out_len,
+                                                                     int32_t* __restrict__ status) {
+    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kStreamWaves * kWave * kRingRow];
+    for (uint32_t i = threadIdx.x; i < 256; i += kStreamBlock) lut[i] = expand_selector(i);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* ring = ring_all + wave * (kWave * kRingRow);
+    const uint32_t unit = (blockIdx.x * kStreamWaves + wave) * kWave + lane;
+    const bool valid = unit < n;
+
+    // ---- per-lane unit state -------------------------------------------------------
+    const uint8_t* src = in;
+    uint64_t P = 0, capw = 0;
+    uint8_t* dstb = out;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P = in_len[unit];
+        dstb = out + out_off[unit];
+        capw = out_cap[unit] >> 3;
+        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+    }
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint64_t end64 = valid ? s + P : 0;
+    const uint8_t* base = src - s;
+    const uint32_t npieces = (uint32_t)((end64 + 15) >> 4);
+    uint64_t q0, q1, q2, q3, n0, n1;
+    uint32_t wb = 0;
+    load_piece(base, npieces, 0, q0, q1);
+    load_piece(base, npieces, 1, q2, q3);
+    load_piece(base, npieces, 2, n0, n1);
+    auto ensure = [&](uint32_t p) {
+        while (p - wb >= 16) {
+            q0 = q2; q1 = q3; q2 = n0; q3 = n1;
+            wb += 16;
+            load_piece(base, npieces, (wb >> 4) + 2, n0, n1);
+        }
+    };
+    uint64_t pos = s;          // next tag
+    uint64_t lit = 0;          // next literal word (valid while pend_lit)
+    uint32_t pend_zero = 0, pend_lit = 0;
+    uint64_t wo = 0;           // words emitted so far
+    bool live = valid && st == ST_OK;
+
+    uint64_t* myrow = reinterpret_cast<uint64_t*>(ring + lane * kRingRow);
+    while (__any(live)) {
+        // ---- one round: each live lane emits up to kRoundWords words -----------------
+        uint32_t nw = 0;
+#pragma unroll 2
+        for (int k = 0; k < kRoundWords; ++k) {
+            if (!live) break;
+            uint64_t word = 0;
+            bool have = true;
+            if (pend_zero) {
+                --pend_zero;
+            } else if (pend_lit) {
+                ensure((uint32_t)lit);
+                word = view_word8(q0, q1, q2, q3, (uint32_t)lit - wb);
+                lit += 8;
+                --pend_lit;
+            } else if (pos < end64) {
+                ensure((uint32_t)pos);
+                const uint32_t o = (uint32_t)pos - wb;
+                const uint32_t t = view_byte(q0, q1, q2, q3, o);
+                if (t == 0x00) {  // message.zig:101-110
+                    if (pos + 2 > end64) { st = ST_EOF; have = false; }
+                    else { pend_zero = view_byte(q0, q1, q2, q3, o + 1); pos += 2; }
+                } else if (t == 0xFF) {  // message.zig:112-128
+                    if (pos + 10 > end64) { st = ST_EOF; have = false; }
+                    else {
+                        const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
+                        if (pos + 10 + 8ULL * c > end64) { st = ST_EOF; have = false; }
+                        else {
+                            word = view_word8(q0, q1, q2, q3, o + 1);
+                            pend_lit = c;
+                            lit = pos + 10;
+                            pos += 10 + 8ULL * c;
+                        }
+                    }
+                } else {  // message.zig:131-141
+                    const uint32_t kk = __popc(t);
+                    if (pos + 1 + kk > end64) { st = ST_EOF; have = false; }
+                    else {
+                        word = perm64(view_word8(q0, q1, q2, q3, o + 1), lut[t]);
+                        pos += 1 + kk;
+                    }
+                }
+            } else {
+                have = false;  // unit finished
+            }
+            if (!have) { live = false; break; }
+            myrow[nw++] = word;
+        }
+        wave_lds_sync();
+        // ---- cooperative store: lane L moves 16 B of unit row (L>>3)+8j ---------------
+        const uint64_t wo_round = wo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t r = (lane >> 3) + 8 * j;  // ring row (= lane of the owning unit)
+            const uint32_t i = lane & 7;             // 16-B piece within the row
+            const uint32_t rnw = __shfl(nw, r, kWave);
+            const uint64_t rwo = __shfl(wo_round, r, kWave);
+            const uint64_t rcap = __shfl(capw, r, kWave);
+            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
+            const uint32_t w0 = 2 * i;  // first word of this piece
+            if (w0 < rnw) {
+                const uint8_t* rp = ring + r * kRingRow + 16 * i;
+                const uint64_t g = rwo + w0;  // unit word index
+                uint8_t* gp = rdst + 8 * g;
+                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
+                if (g < rcap) {
+                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
+                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rp);
+                    } else {
+                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rp);
+                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rp + 8);
+                    }
+                }
+            }
+        }
+        wo += nw;
+        wave_lds_sync();
+    }
+    if (!valid) return;
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8 * wo;
+    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
+}
+
+// ---------------------------------------------------------------------------
 // synthetic generator and offset scan
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t seed, uint64_t unit, uint64_t word) {
@@ -880,10 +1178,36 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     return hipGetLastError();
 }
 
+static int decode_variant() {
+    static int v = [] {
+        const char* e = getenv("CPK_DECODE_VARIANT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    if (decode_variant() == 2 || (decode_variant() == 1 && write)) {
+        if (write) {
+            const uint32_t per = kStreamBlock;
+            decode_stream_kernel<<<(n + per - 1) / per, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out,
+                                                                                  out_off, out_cap, out_len, status);
+            return hipGetLastError();
+        }
+    }
+    if (decode_variant() >= 1) {
+        const uint32_t blocks = (n + kBlock - 1) / kBlock;
+        if (write)
+            decode_lane_kernel<true><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                     out_len, status);
+        else
+            decode_lane_kernel<false><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                      out_len, status);
+        return hipGetLastError();
+    }
     if (write)
         decode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status);
