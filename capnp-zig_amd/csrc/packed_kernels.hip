@@ -175,6 +175,18 @@ __device__ __forceinline__ void stage_linear(uint8_t* lds, const uint8_t* g, uin
     }
 }
 
+// expand: packed bytes d (byte r = r-th nonzero byte) -> word with zeros where tag bit is clear
+__device__ __forceinline__ uint64_t expand_word(uint64_t d, uint32_t t) {
+    const uint32_t s_lo = ((t & 0xFu) * 0x00204081u) & 0x01010101u;        // byte k = bit k
+    const uint32_t s_hi = (((t >> 4) & 0xFu) * 0x00204081u) & 0x01010101u;
+    const uint32_t inc_lo = s_lo * 0x01010101u;                             // inclusive byte prefix sums
+    const uint32_t inc_hi = s_hi * 0x01010101u + (inc_lo >> 24) * 0x01010101u;
+    const uint32_t m_lo = s_lo * 0xFFu, m_hi = s_hi * 0xFFu;
+    const uint32_t sel_lo = ((inc_lo - s_lo) & m_lo) | (0x0C0C0C0Cu & ~m_lo);
+    const uint32_t sel_hi = ((inc_hi - s_hi) & m_hi) | (0x0C0C0C0Cu & ~m_hi);
+    return perm64(d, (uint64_t)sel_lo | ((uint64_t)sel_hi << 32));
+}
+
 // Per-lane byte stream into a zero-initialised LDS buffer. Every flushed u64 is
 // OR-ed (ds_or_b64) so the partial words a lane shares with its neighbours merge.
 struct LdsByteStream {
@@ -910,6 +922,7 @@ constexpr int kRingRow = kRoundWords * 8 + 16;  // 144 B: 16-B aligned, staggers
 constexpr int kStreamWaves = 2;                 // waves per block
 constexpr int kStreamBlock = kStreamWaves * kWave;
 
+template <uint32_t PF>
 __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8_t* __restrict__ in,
                                                                      const uint64_t* __restrict__ in_off,
                                                                      const uint64_t* __restrict__ in_len,
@@ -918,10 +931,8 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
                                                                      const uint64_t* __restrict__ out_cap,
                                                                      uint64_t* __restrict__ out_len,
                                                                      int32_t* __restrict__ status) {
-    __shared__ uint64_t lut[256];
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kStreamWaves * kWave * kRingRow];
-    for (uint32_t i = threadIdx.x; i < 256; i += kStreamBlock) lut[i] = expand_selector(i);
-    __syncthreads();
+    __shared__ uint32_t pf_sink[kStreamWaves * kWave];  // LDS-DMA prefetch target, never read
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* ring = ring_all + wave * (kWave * kRingRow);
@@ -949,13 +960,26 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
     load_piece(base, npieces, 0, q0, q1);
     load_piece(base, npieces, 1, q2, q3);
     load_piece(base, npieces, 2, n0, n1);
+    uint32_t* sink = pf_sink + wave * kWave;
     auto ensure = [&](uint32_t p) {
         while (p - wb >= 16) {
             q0 = q2; q1 = q3; q2 = n0; q3 = n1;
             wb += 16;
             load_piece(base, npieces, (wb >> 4) + 2, n0, n1);
+            if (PF) {  // pull the line PF bytes ahead into L2 (LDS-DMA into a sink: no VGPR, no wait)
+                const uint32_t pa = wb + PF;
+                if ((pa & 127) == 0 && pa < npieces * 16) {
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + pa),
+                                                     (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
+                }
+            }
         }
     };
+    if (PF) {  // warm the first PF bytes
+        for (uint32_t pa = 128; pa < PF && pa < npieces * 16; pa += 128)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + pa),
+                                             (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
+    }
     uint64_t pos = s;          // next tag
     uint64_t lit = 0;          // next literal word (valid while pend_lit)
     uint32_t pend_zero = 0, pend_lit = 0;
@@ -1001,7 +1025,7 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
                     const uint32_t kk = __popc(t);
                     if (pos + 1 + kk > end64) { st = ST_EOF; have = false; }
                     else {
-                        word = perm64(view_word8(q0, q1, q2, q3, o + 1), lut[t]);
+                        word = expand_word(view_word8(q0, q1, q2, q3, o + 1), t);
                         pos += 1 + kk;
                     }
                 }
@@ -1041,6 +1065,7 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
         wo += nw;
         wave_lds_sync();
     }
+    if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no prefetch may land after the wave exits
     if (!valid) return;
     if (st != ST_OK) {
         out_len[unit] = 0;
@@ -1049,6 +1074,631 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
     }
     out_len[unit] = 8 * wo;
     status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
+}
+
+// ---------------------------------------------------------------------------
+// DECODE, lane per unit, LDS-DMA input ring + lockstep output rounds
+// ---------------------------------------------------------------------------
+// Input side: each lane's packed bytes stream through a per-lane ring of
+// kSlots 64-byte chunks in LDS, filled by LDS-DMA (global_load_lds_dwordx4: no
+// VGPR destination, so nothing forces a wait at issue). Chunks are issued at
+// round ends as soon as the slot they reuse is consumed, so every lane keeps
+// ~3 chunks (~192 B) in flight; one s_waitcnt per round end lands them. Within
+// a DMA instruction, 4 lanes move the 4 x 16 B of one lane's chunk; the 16-B
+// pieces are XOR-swizzled by lane so lanes reading the same logical offset hit
+// different LDS banks (swizzle applied to the DMA source, read with the same
+// swizzle: linear destination).
+// Output side: as decode_stream_kernel (lockstep 16-word rounds, cooperative
+// 128-B line stores).
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+struct DmaCfg {
+    static constexpr uint32_t kPieces = CHUNK / 16;                // 16-B pieces per lane chunk
+    static constexpr uint32_t kTasks = kWave / kPieces;            // lanes whose chunk one DMA moves
+    static constexpr uint32_t kSlotBytes = kWave * CHUNK;          // one slot for every lane
+    static constexpr uint32_t kInRing = SLOTS * kSlotBytes;
+    static constexpr uint32_t kRow = ROUND * 8 + 16;               // output row stride (16-B aligned, staggered)
+    static constexpr uint32_t kOutRing = kWave * kRow;
+    static constexpr uint32_t kLanesPerRow = ROUND / 2;            // 16 B per lane in the store
+    static constexpr uint32_t kRowsPerStep = kWave / kLanesPerRow;
+    static constexpr uint32_t kSteps = kWave / kRowsPerStep;
+    static constexpr uint32_t kBlock = WAVES * kWave;
+    static_assert(CHUNK % 16 == 0 && (SLOTS & (SLOTS - 1)) == 0 && ROUND % 2 == 0, "cfg");
+    __device__ static uint32_t swz(uint32_t l) { return (l >> 2) & (kPieces - 1); }
+};
+
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+__global__ __launch_bounds__(WAVES * 64) void decode_dma_kernel(const uint8_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ in_off,
+                                                                const uint64_t* __restrict__ in_len,
+                                                                uint32_t n, uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint64_t* __restrict__ out_len,
+                                                                int32_t* __restrict__ status) {
+    using C = DmaCfg<CHUNK, SLOTS, ROUND, WAVES>;
+    __shared__ __attribute__((aligned(16))) uint8_t in_all[WAVES * C::kInRing];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[WAVES * C::kOutRing];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* iring = in_all + wave * C::kInRing;
+    uint8_t* oring = ring_all + wave * C::kOutRing;
+    const uint32_t unit = (blockIdx.x * WAVES + wave) * kWave + lane;
+    const bool valid = unit < n;
+
+    const uint8_t* src = in;
+    uint64_t P = 0, capw = 0;
+    uint8_t* dstb = out;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P = in_len[unit];
+        dstb = out + out_off[unit];
+        capw = out_cap[unit] >> 3;
+        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+        if (P > 0xFFFF0000ULL) st = ST_ARG;  // 32-bit stream offsets
+    }
+    bool live = valid && st == ST_OK;
+    if (!live) P = 0;
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint8_t* base = src - s;                    // 16-B aligned
+    const uint32_t end = s + (uint32_t)P;             // logical stream [s, end)
+    const uint32_t npieces = live ? (end + 15) >> 4 : 0;
+    const uint32_t padded = npieces * 16;             // bytes the DMA ever delivers for this lane
+    const uint32_t nchunks = (padded + CHUNK - 1) / CHUNK;
+    uint32_t maxchunks = nchunks;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxchunks = max(maxchunks, (uint32_t)__shfl_xor((int)maxchunks, d, kWave));
+    maxchunks = __builtin_amdgcn_readfirstlane(maxchunks);
+
+    // DMA task descriptors: in pass k, lane L moves source piece kPieces*k + (i ^ swz(r))
+    // of lane r = kTasks*g + L/kPieces into destination piece i = L % kPieces of r's slot k % SLOTS.
+    uint64_t dsrc[C::kPieces];
+    uint32_t dnp[C::kPieces], dpc[C::kPieces];
+#pragma unroll
+    for (uint32_t g = 0; g < C::kPieces; ++g) {
+        const uint32_t r = C::kTasks * g + lane / C::kPieces;
+        const uint32_t sp = (lane % C::kPieces) ^ C::swz(r);
+        dsrc[g] = __shfl(reinterpret_cast<uint64_t>(base), r, kWave) + 16ULL * sp;
+        dnp[g] = __shfl(npieces, r, kWave);
+        dpc[g] = sp;
+    }
+    uint32_t issued = 0;  // wave-uniform: chunks issued for every lane
+    auto dma_pass = [&]() {
+        const uint32_t k = issued;
+        uint8_t* slot = iring + (k & (SLOTS - 1)) * C::kSlotBytes;
+#pragma unroll
+        for (uint32_t g = 0; g < C::kPieces; ++g) {
+            if (C::kPieces * k + dpc[g] < dnp[g]) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[g] + (uint64_t)CHUNK * k),
+                                                 (__attribute__((address_space(3))) void*)(slot + g * C::kTasks * CHUNK),
+                                                 16, 0, 0);
+            }
+        }
+        issued = k + 1;
+    };
+
+    uint32_t pos = s, lit = 0, pend_zero = 0, pend_lit = 0;
+    uint64_t wo = 0;
+    const uint32_t laneb = lane * CHUNK;
+    const uint32_t swz16 = C::swz(lane) << 4;
+    auto u64_at = [&](uint32_t y) -> uint64_t {  // y 8-aligned logical offset
+        const uint32_t a = ((y / CHUNK) & (SLOTS - 1)) * C::kSlotBytes + laneb + ((y & (CHUNK - 1)) ^ swz16);
+        return *reinterpret_cast<const uint64_t*>(iring + a);
+    };
+    // issue a pass while the slowest live lane has freed the slot the pass reuses
+    auto may_issue = [&]() -> bool {
+        const uint32_t mr = (pend_lit ? lit : pos) / CHUNK;  // oldest chunk still needed
+        return issued < maxchunks && __all(!live || issued < mr + SLOTS);
+    };
+
+    for (uint32_t q = 0; q < SLOTS && may_issue(); ++q) dma_pass();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t landed = issued;
+
+    uint64_t* myrow = reinterpret_cast<uint64_t*>(oring + lane * C::kRow);
+    while (__any(live)) {
+        const uint32_t limit = (landed * CHUNK >= padded) ? 0xFFFFFFFFu : landed * CHUNK;
+        uint32_t nw = 0;
+        bool frozen = false;
+        for (uint32_t k = 0; k < ROUND; ++k) {
+            const bool ok = live && !frozen;
+            if (!__any(ok)) break;
+            const bool isZ = pend_zero != 0;
+            const bool isL = !isZ && pend_lit != 0;
+            const bool isR = !isZ && !isL && pos < end;
+            const uint32_t rp = isL ? lit : pos;
+            const uint32_t y = rp & ~7u;
+            const uint64_t a = u64_at(y), b = u64_at(y + 8);
+            const uint32_t o = rp & 7;
+            const uint32_t sh = 8 * o;
+            const uint64_t lw = sh ? ((a >> sh) | (b << (64 - sh))) : a;         // literal word at rp
+            const uint32_t t = (uint32_t)(a >> sh) & 0xFFu;                      // tag at rp
+            const uint64_t pay = (o == 7) ? b : ((a >> (sh + 8)) | (b << (56 - sh)));  // bytes rp+1..rp+8
+            uint32_t cnt = (uint32_t)(b >> (sh + 8)) & 0xFFu;                    // byte rp+9 (o <= 6)
+            bool avail = y + 16 <= limit;
+            const bool ff7 = ok && isR && avail && t == 0xFF && o == 7;
+            if (__any(ff7)) {  // rare: FF count byte in the next 8-byte word
+                if (ff7) {
+                    avail = y + 24 <= limit;
+                    if (avail) cnt = (uint32_t)u64_at(y + 16) & 0xFFu;
+                }
+            }
+            const uint32_t kk = __popc(t);
+            const bool tz = t == 0, tf = t == 0xFF;
+            const uint32_t hdr = tz ? 2u : (tf ? 10u : 1u + kk);                  // bytes needed up front
+            const uint32_t rlen = tf ? 10u + 8u * cnt : hdr;                      // record length
+            const bool eof = (pos + hdr > end) || (pos + rlen > end);             // message.zig:152-191
+            const bool stepZ = ok && isZ;
+            const bool stepL = ok && isL && avail;
+            const bool stepR = ok && isR && avail && !eof;
+            const bool err = ok && isR && avail && eof;
+            const bool fin = ok && !isZ && !isL && !isR;
+            if (ok && (isL || isR) && !avail) frozen = true;
+            if (err) st = ST_EOF;
+            if (err || fin) live = false;
+            const uint64_t rword = tz ? 0 : (tf ? pay : expand_word(pay, t));
+            const uint64_t word = isZ ? 0 : (isL ? lw : rword);
+            myrow[nw] = word;
+            nw += (stepZ || stepL || stepR) ? 1u : 0u;
+            pend_zero = stepZ ? pend_zero - 1 : ((stepR && tz) ? (uint32_t)pay & 0xFFu : pend_zero);
+            pend_lit = stepL ? pend_lit - 1 : ((stepR && tf) ? cnt : pend_lit);
+            lit = stepL ? lit + 8 : ((stepR && tf) ? pos + 10 : lit);
+            pos = stepR ? pos + rlen : pos;
+        }
+        wave_lds_sync();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMAs issued at the last round end have landed
+        landed = issued;
+        // ---- cooperative store of this round's rows: lane L moves 16 B of one row ----------
+        const uint64_t wo_round = wo;
+#pragma unroll
+        for (uint32_t j = 0; j < C::kSteps; ++j) {
+            const uint32_t r = lane / C::kLanesPerRow + C::kRowsPerStep * j;
+            const uint32_t i = lane % C::kLanesPerRow;
+            const uint32_t rnw = __shfl(nw, r, kWave);
+            const uint64_t rwo = __shfl(wo_round, r, kWave);
+            const uint64_t rcap = __shfl(capw, r, kWave);
+            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
+            const uint32_t w0 = 2 * i;
+            if (w0 < rnw) {
+                const uint8_t* rp = oring + r * C::kRow + 16 * i;
+                const uint64_t g = rwo + w0;
+                uint8_t* gp = rdst + 8 * g;
+                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
+                if (g < rcap) {
+                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
+                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rp);
+                    } else {
+                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rp);
+                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rp + 8);
+                    }
+                }
+            }
+        }
+        wo += nw;
+        for (uint32_t q = 0; q < 2 && may_issue(); ++q) dma_pass();
+        wave_lds_sync();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
+    if (!valid) return;
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8 * wo;
+    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
+}
+
+// Two-phase round: (1) WALK — the only serial part: per output word, follow the
+// record chain using tag/count bytes only (ds_read_u8), and record the word's
+// kind and source position in static registers; (2) EXPAND — ROUND independent
+// words (unrolled), each reading its 16-byte window and expanding it, written to
+// static ring offsets. The walk is ~15 instructions per record; the expansion's
+// LDS latency is hidden by ILP across the round's words.
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+__global__ __launch_bounds__(WAVES * 64) void decode_walk_kernel(const uint8_t* __restrict__ in,
+                                                                 const uint64_t* __restrict__ in_off,
+                                                                 const uint64_t* __restrict__ in_len,
+                                                                 uint32_t n, uint8_t* __restrict__ out,
+                                                                 const uint64_t* __restrict__ out_off,
+                                                                 const uint64_t* __restrict__ out_cap,
+                                                                 uint64_t* __restrict__ out_len,
+                                                                 int32_t* __restrict__ status) {
+    using C = DmaCfg<CHUNK, SLOTS, ROUND, WAVES>;
+    __shared__ __attribute__((aligned(16))) uint8_t in_all[WAVES * C::kInRing];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[WAVES * C::kOutRing];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* iring = in_all + wave * C::kInRing;
+    uint8_t* oring = ring_all + wave * C::kOutRing;
+    const uint32_t unit = (blockIdx.x * WAVES + wave) * kWave + lane;
+    const bool valid = unit < n;
+
+    const uint8_t* src = in;
+    uint64_t P = 0, capw = 0;
+    uint8_t* dstb = out;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P = in_len[unit];
+        dstb = out + out_off[unit];
+        capw = out_cap[unit] >> 3;
+        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+        if (P > 0x3FFF0000ULL) st = ST_ARG;  // 30-bit stream offsets
+    }
+    bool live = valid && st == ST_OK;
+    if (!live) P = 0;
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint8_t* base = src - s;
+    const uint32_t end = s + (uint32_t)P;
+    const uint32_t npieces = live ? (end + 15) >> 4 : 0;
+    const uint32_t padded = npieces * 16;
+    const uint32_t nchunks = (padded + CHUNK - 1) / CHUNK;
+    uint32_t maxchunks = nchunks;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxchunks = max(maxchunks, (uint32_t)__shfl_xor((int)maxchunks, d, kWave));
+    maxchunks = __builtin_amdgcn_readfirstlane(maxchunks);
+
+    uint64_t dsrc[C::kPieces];
+    uint32_t dnp[C::kPieces], dpc[C::kPieces];
+#pragma unroll
+    for (uint32_t g = 0; g < C::kPieces; ++g) {
+        const uint32_t r = C::kTasks * g + lane / C::kPieces;
+        const uint32_t sp = (lane % C::kPieces) ^ C::swz(r);
+        dsrc[g] = __shfl(reinterpret_cast<uint64_t>(base), r, kWave) + 16ULL * sp;
+        dnp[g] = __shfl(npieces, r, kWave);
+        dpc[g] = sp;
+    }
+    uint32_t issued = 0;
+    auto dma_pass = [&]() {
+        const uint32_t k = issued;
+        uint8_t* slot = iring + (k & (SLOTS - 1)) * C::kSlotBytes;
+#pragma unroll
+        for (uint32_t g = 0; g < C::kPieces; ++g) {
+            if (C::kPieces * k + dpc[g] < dnp[g]) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[g] + (uint64_t)CHUNK * k),
+                                                 (__attribute__((address_space(3))) void*)(slot + g * C::kTasks * CHUNK),
+                                                 16, 0, 0);
+            }
+        }
+        issued = k + 1;
+    };
+
+    uint32_t pos = s, lit = 0, pend_zero = 0, pend_lit = 0;
+    uint64_t wo = 0;
+    const uint32_t laneb = lane * CHUNK;
+    const uint32_t swz16 = C::swz(lane) << 4;
+    auto ring_addr = [&](uint32_t y) -> uint32_t {  // LDS offset of logical byte y
+        return ((y / CHUNK) & (SLOTS - 1)) * C::kSlotBytes + laneb + ((y & (CHUNK - 1)) ^ swz16);
+    };
+    auto u8_at = [&](uint32_t y) -> uint32_t { return iring[ring_addr(y)]; };
+    auto u64_at = [&](uint32_t y) -> uint64_t {  // y 8-aligned
+        return *reinterpret_cast<const uint64_t*>(iring + ring_addr(y));
+    };
+    auto may_issue = [&]() -> bool {
+        const uint32_t mr = (pend_lit ? lit : pos) / CHUNK;
+        return issued < maxchunks && __all(!live || issued < mr + SLOTS);
+    };
+
+    for (uint32_t q = 0; q < SLOTS && may_issue(); ++q) dma_pass();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t landed = issued;
+
+    uint8_t* myrow = oring + lane * C::kRow;
+    while (__any(live)) {
+        const uint32_t limit = (landed * CHUNK >= padded) ? 0xFFFFFFFFu : landed * CHUNK;
+        // ---- WALK: kinds/positions of this round's words -------------------------------
+        uint32_t srcpos[ROUND];
+        uint32_t mixmask = 0, litmask = 0;  // bit k: word k is a mixed record / a literal word
+        uint32_t nw = 0;
+        bool frozen = false;
+#pragma unroll
+        for (uint32_t k = 0; k < ROUND; ++k) {
+            const bool ok = live && !frozen;
+            const bool isZ = pend_zero != 0;
+            const bool isL = !isZ && pend_lit != 0;
+            const bool isR = !isZ && !isL && pos < end;
+            const uint32_t t = u8_at(pos);          // tag (meaningful when isR)
+            const uint32_t c1 = u8_at(pos + 1);     // zero-run count
+            const uint32_t c9 = u8_at(pos + 9);     // literal-run count
+            const bool avail = isL ? ((lit & ~7u) + 16 <= limit) : (!isR || (pos & ~7u) + 24 <= limit);
+            const bool go = ok && avail && (isZ || isL || isR);
+            const bool tz = t == 0, tf = t == 0xFF;
+            const uint32_t hdr = tz ? 2u : (tf ? 10u : 1u + __popc(t));
+            const uint32_t rlen = tf ? 10u + 8u * c9 : hdr;
+            const bool eof = isR && (pos + hdr > end || pos + rlen > end);  // message.zig:152-191
+            const bool emit = go && !eof;
+            if (ok && !avail) frozen = true;
+            if (go && eof) { st = ST_EOF; live = false; }
+            if (ok && !isZ && !isL && !isR) live = false;  // unit finished
+            srcpos[k] = isL ? lit : (pos + (tf ? 1u : 0u));
+            if (emit && isR && !tz && !tf) mixmask |= 1u << k;
+            if (emit && (isL || (isR && tf))) litmask |= 1u << k;
+            nw += emit ? 1u : 0u;
+            const bool stepR = emit && isR;
+            pend_zero = (emit && isZ) ? pend_zero - 1 : ((stepR && tz) ? c1 : pend_zero);
+            const bool stepL = emit && isL;
+            pend_lit = stepL ? pend_lit - 1 : ((stepR && tf) ? c9 : pend_lit);
+            lit = stepL ? lit + 8 : ((stepR && tf) ? pos + 10 : lit);
+            pos = stepR ? pos + rlen : pos;
+        }
+        // ---- EXPAND: independent words --------------------------------------------------
+#pragma unroll
+        for (uint32_t k = 0; k < ROUND; ++k) {
+            uint64_t word = 0;
+            if ((mixmask | litmask) & (1u << k)) {
+                const uint32_t p = srcpos[k];
+                const uint32_t y = p & ~7u;
+                const uint64_t a = u64_at(y), b = u64_at(y + 8);
+                const uint32_t o = p & 7;
+                if (mixmask & (1u << k)) {
+                    const uint32_t t = (uint32_t)(a >> (8 * o)) & 0xFFu;
+                    const uint64_t pay = (o == 7) ? b : ((a >> (8 * o + 8)) | (b << (56 - 8 * o)));
+                    word = expand_word(pay, t);
+                } else {
+                    word = o ? ((a >> (8 * o)) | (b << (64 - 8 * o))) : a;
+                }
+            }
+            *reinterpret_cast<uint64_t*>(myrow + 8 * k) = word;
+        }
+        wave_lds_sync();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        landed = issued;
+        const uint64_t wo_round = wo;
+#pragma unroll
+        for (uint32_t j = 0; j < C::kSteps; ++j) {
+            const uint32_t r = lane / C::kLanesPerRow + C::kRowsPerStep * j;
+            const uint32_t i = lane % C::kLanesPerRow;
+            const uint32_t rnw = __shfl(nw, r, kWave);
+            const uint64_t rwo = __shfl(wo_round, r, kWave);
+            const uint64_t rcap = __shfl(capw, r, kWave);
+            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
+            const uint32_t w0 = 2 * i;
+            if (w0 < rnw) {
+                const uint8_t* rp = oring + r * C::kRow + 16 * i;
+                const uint64_t g = rwo + w0;
+                uint8_t* gp = rdst + 8 * g;
+                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
+                if (g < rcap) {
+                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
+                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rp);
+                    } else {
+                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rp);
+                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rp + 8);
+                    }
+                }
+            }
+        }
+        wo += nw;
+        for (uint32_t q = 0; q < 2 && may_issue(); ++q) dma_pass();
+        wave_lds_sync();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!valid) return;
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8 * wo;
+    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
+}
+
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+static void launch_walk(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
+                        const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                        hipStream_t stream) {
+    constexpr uint32_t per = WAVES * kWave;
+    decode_walk_kernel<CHUNK, SLOTS, ROUND, WAVES><<<(n + per - 1) / per, per, 0, stream>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+}
+
+// Register window fed from the LDS-DMA ring: the record step reads only
+// registers (a 32-byte view q0..q3); the window advances 16 B at a time from the
+// lane's ring with the next piece (nx0, nx1) read one advance ahead, so LDS
+// latency stays off the record chain and global latency stays behind the DMA ring.
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+__global__ __launch_bounds__(WAVES * 64) void decode_win_kernel(const uint8_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ in_off,
+                                                                const uint64_t* __restrict__ in_len,
+                                                                uint32_t n, uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint64_t* __restrict__ out_len,
+                                                                int32_t* __restrict__ status) {
+    using C = DmaCfg<CHUNK, SLOTS, ROUND, WAVES>;
+    __shared__ __attribute__((aligned(16))) uint8_t in_all[WAVES * C::kInRing];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[WAVES * C::kOutRing];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* iring = in_all + wave * C::kInRing;
+    uint8_t* oring = ring_all + wave * C::kOutRing;
+    const uint32_t unit = (blockIdx.x * WAVES + wave) * kWave + lane;
+    const bool valid = unit < n;
+
+    const uint8_t* src = in;
+    uint64_t P = 0, capw = 0;
+    uint8_t* dstb = out;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P = in_len[unit];
+        dstb = out + out_off[unit];
+        capw = out_cap[unit] >> 3;
+        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+        if (P > 0xFFFF0000ULL) st = ST_ARG;
+    }
+    bool live = valid && st == ST_OK;
+    if (!live) P = 0;
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint8_t* base = src - s;
+    const uint32_t end = s + (uint32_t)P;
+    const uint32_t npieces = live ? (end + 15) >> 4 : 0;
+    const uint32_t padded = npieces * 16;
+    const uint32_t nchunks = (padded + CHUNK - 1) / CHUNK;
+    uint32_t maxchunks = nchunks;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxchunks = max(maxchunks, (uint32_t)__shfl_xor((int)maxchunks, d, kWave));
+    maxchunks = __builtin_amdgcn_readfirstlane(maxchunks);
+
+    uint64_t dsrc[C::kPieces];
+    uint32_t dnp[C::kPieces], dpc[C::kPieces];
+#pragma unroll
+    for (uint32_t g = 0; g < C::kPieces; ++g) {
+        const uint32_t r = C::kTasks * g + lane / C::kPieces;
+        const uint32_t sp = (lane % C::kPieces) ^ C::swz(r);
+        dsrc[g] = __shfl(reinterpret_cast<uint64_t>(base), r, kWave) + 16ULL * sp;
+        dnp[g] = __shfl(npieces, r, kWave);
+        dpc[g] = sp;
+    }
+    uint32_t issued = 0;
+    auto dma_pass = [&]() {
+        const uint32_t k = issued;
+        uint8_t* slot = iring + (k & (SLOTS - 1)) * C::kSlotBytes;
+#pragma unroll
+        for (uint32_t g = 0; g < C::kPieces; ++g) {
+            if (C::kPieces * k + dpc[g] < dnp[g]) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[g] + (uint64_t)CHUNK * k),
+                                                 (__attribute__((address_space(3))) void*)(slot + g * C::kTasks * CHUNK),
+                                                 16, 0, 0);
+            }
+        }
+        issued = k + 1;
+    };
+    const uint32_t laneb = lane * CHUNK;
+    const uint32_t swzp = C::swz(lane);
+    // 16-B piece q (logical piece index) of this lane, from the ring
+    auto piece_at = [&](uint32_t q, uint64_t& lo, uint64_t& hi) {
+        const uint32_t a = ((q / C::kPieces) & (SLOTS - 1)) * C::kSlotBytes + laneb + (((q % C::kPieces) ^ swzp) << 4);
+        const uint4 v = *reinterpret_cast<const uint4*>(iring + a);
+        lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    };
+
+    uint32_t pos = s, lit = 0, pend_zero = 0, pend_lit = 0;
+    uint64_t wo = 0;
+    uint32_t wb = 0;  // logical offset of q0 (piece wb/16); nx = piece wb/16 + 2
+    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nx0 = 0, nx1 = 0;
+    auto may_issue = [&]() -> bool {
+        const uint32_t mr = wb / CHUNK;  // the window's first piece is the oldest byte still needed
+        return issued < maxchunks && __all(!live || issued < mr + SLOTS);
+    };
+
+    for (uint32_t q = 0; q < SLOTS && may_issue(); ++q) dma_pass();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t landed = issued;
+    if (live) {
+        piece_at(0, q0, q1);
+        piece_at(1, q2, q3);
+        piece_at(2, nx0, nx1);
+    }
+
+    uint64_t* myrow = reinterpret_cast<uint64_t*>(oring + lane * C::kRow);
+    while (__any(live)) {
+        const uint32_t limit = (landed * CHUNK >= padded) ? 0xFFFFFFFFu : landed * CHUNK;
+        uint32_t nw = 0;
+        for (uint32_t k = 0; k < ROUND; ++k) {
+            if (!live) break;
+            const uint32_t rp = pend_lit ? lit : pos;
+            if (rp - wb >= 16) {  // advance the window by one piece (never more per word)
+                if (wb + 64 > limit) break;  // piece wb/16 + 3 not landed yet: resume next round
+                q0 = q2; q1 = q3; q2 = nx0; q3 = nx1;
+                wb += 16;
+                piece_at((wb >> 4) + 2, nx0, nx1);
+            }
+            const uint32_t o = rp - wb;  // < 16
+            uint64_t word = 0;
+            if (pend_zero) {
+                --pend_zero;
+            } else if (pend_lit) {
+                word = view_word8(q0, q1, q2, q3, o);
+                lit += 8;
+                --pend_lit;
+            } else if (pos < end) {
+                const uint32_t t = view_byte(q0, q1, q2, q3, o);
+                const uint64_t pay = view_word8(q0, q1, q2, q3, o + 1);
+                if (t == 0x00) {  // message.zig:101-110
+                    if (pos + 2 > end) { st = ST_EOF; live = false; break; }
+                    pend_zero = (uint32_t)pay & 0xFFu;
+                    pos += 2;
+                } else if (t == 0xFF) {  // message.zig:112-128
+                    const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
+                    if (pos + 10 > end || pos + 10 + 8 * c > end) { st = ST_EOF; live = false; break; }
+                    word = pay;
+                    pend_lit = c;
+                    lit = pos + 10;
+                    pos += 10 + 8 * c;
+                } else {  // message.zig:131-141
+                    const uint32_t kk = __popc(t);
+                    if (pos + 1 + kk > end) { st = ST_EOF; live = false; break; }
+                    word = expand_word(pay, t);
+                    pos += 1 + kk;
+                }
+            } else {
+                live = false;  // unit finished
+                break;
+            }
+            myrow[nw++] = word;
+        }
+        wave_lds_sync();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        landed = issued;
+        const uint64_t wo_round = wo;
+#pragma unroll
+        for (uint32_t j = 0; j < C::kSteps; ++j) {
+            const uint32_t r = lane / C::kLanesPerRow + C::kRowsPerStep * j;
+            const uint32_t i = lane % C::kLanesPerRow;
+            const uint32_t rnw = __shfl(nw, r, kWave);
+            const uint64_t rwo = __shfl(wo_round, r, kWave);
+            const uint64_t rcap = __shfl(capw, r, kWave);
+            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
+            const uint32_t w0 = 2 * i;
+            if (w0 < rnw) {
+                const uint8_t* rpp = oring + r * C::kRow + 16 * i;
+                const uint64_t g = rwo + w0;
+                uint8_t* gp = rdst + 8 * g;
+                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
+                if (g < rcap) {
+                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
+                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rpp);
+                    } else {
+                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rpp);
+                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rpp + 8);
+                    }
+                }
+            }
+        }
+        wo += nw;
+        for (uint32_t q = 0; q < 2 && may_issue(); ++q) dma_pass();
+        wave_lds_sync();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!valid) return;
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8 * wo;
+    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
+}
+
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+static void launch_win(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
+                       const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                       hipStream_t stream) {
+    constexpr uint32_t per = WAVES * kWave;
+    decode_win_kernel<CHUNK, SLOTS, ROUND, WAVES><<<(n + per - 1) / per, per, 0, stream>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+}
+
+template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
+static void launch_dma(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
+                       const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                       hipStream_t stream) {
+    constexpr uint32_t per = WAVES * kWave;
+    decode_dma_kernel<CHUNK, SLOTS, ROUND, WAVES><<<(n + per - 1) / per, per, 0, stream>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
 }
 
 // ---------------------------------------------------------------------------
@@ -1180,8 +1830,8 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
 
 static int decode_variant() {
     static int v = [] {
-        const char* e = getenv("CPK_DECODE_VARIANT");
-        return e ? atoi(e) : 1;
+        const char* e = getenv("CPK_DECODE_VARIANT");  // experiment switch; default 2
+        return e ? atoi(e) : 2;
     }();
     return v;
 }
@@ -1190,13 +1840,51 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (decode_variant() == 2 || (decode_variant() == 1 && write)) {
-        if (write) {
-            const uint32_t per = kStreamBlock;
-            decode_stream_kernel<<<(n + per - 1) / per, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                                  out_off, out_cap, out_len, status);
-            return hipGetLastError();
+    if (write) {
+        switch (decode_variant()) {
+            case 1: launch_dma<64, 4, 16, 2>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 3: launch_dma<32, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 4: launch_dma<32, 4, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 5: launch_dma<64, 2, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 6: launch_dma<32, 2, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 7: launch_dma<64, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 12: launch_win<64, 4, 16, 2>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 13: launch_win<32, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 14: launch_win<32, 4, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 15: launch_win<64, 2, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 16: launch_win<64, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 8: launch_walk<64, 4, 16, 2>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 9: launch_walk<64, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 10: launch_walk<32, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            case 11: launch_walk<64, 2, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+                    return hipGetLastError();
+            default: break;
         }
+    }
+    if (write && (decode_variant() == 2 || (decode_variant() >= 20 && decode_variant() <= 23))) {
+        const uint32_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
+        switch (decode_variant()) {
+            case 20: decode_stream_kernel<256><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
+            case 21: decode_stream_kernel<512><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
+            case 22: decode_stream_kernel<1024><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
+            case 23: decode_stream_kernel<128><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
+            default: decode_stream_kernel<0><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
+        }
+        return hipGetLastError();
     }
     if (decode_variant() >= 1) {
         const uint32_t blocks = (n + kBlock - 1) / kBlock;
