@@ -27,6 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import capnp_packed as cp  # noqa: E402
+import sharding  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, 8.0 TB/s (MI355X_MICROARCH.md, chip table)
 META_BYTES_PER_UNIT = 44  # in_off, in_len, out_off, out_cap (4 x 8 B read) + out_len (8 B) + status (4 B)
@@ -44,6 +45,7 @@ def parse():
     ap.add_argument("--sweep", action="store_true", help="also time p = 0.1 / 0.9 (extra fields)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory leg")
     return ap.parse_args()
 
 
@@ -77,7 +79,7 @@ class Workload:
 
 def time_steps(wl, steps, warmup, world, dev):
     stream = torch.cuda.current_stream()
-    gathered = torch.zeros(world, dtype=torch.int64, device=dev)
+    gathered = [torch.zeros(world, dtype=torch.int64, device=dev)]
 
     def step(ev=None):
         if ev is not None:
@@ -88,11 +90,8 @@ def time_steps(wl, steps, warmup, world, dev):
         wl.decode(stream)
         if ev is not None:
             ev[2].record(stream)
-        total = wl.plen.sum()
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, total.view(1))
-        else:
-            gathered[0] = total
+        # per-rank packed total -> RCCL all-gather (the only collective)
+        gathered[0] = sharding.gather_packed_totals(wl.plen.sum())
 
     for _ in range(warmup):
         step()
@@ -112,7 +111,7 @@ def time_steps(wl, steps, warmup, world, dev):
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    return float(elapsed.item()), enc_ms, dec_ms, gathered
+    return float(elapsed.item()), enc_ms, dec_ms, gathered[0]
 
 
 def cpu_baseline(args, budget_s):
@@ -149,6 +148,86 @@ def cpu_baseline(args, budget_s):
     return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{reps} x ({n} units x {ub} B, same generator/seed/density) pack+unpack via "
                       f"oracle/packed_oracle.c (-O3, OpenMP {threads} threads), {t_total:.1f} s"}
+
+
+def host_path(args, dev, n_units=1 << 16):
+    """PCIe-inclusive rates, reported beside the device-resident
+    number and never as `value`. Host buffers are pinned; the batch is cut into 8
+    chunks over 2 streams so H2D, kernels and D2H of different chunks overlap.
+      decode: dense packed stream (P bytes) H2D -> decode -> unpacked D2H
+      encode: unpacked H2D -> sizes -> scan -> dense encode -> packed D2H
+    (the encode leg copies back each chunk's exact packed size, known here from a
+    prior pass; a socket writer would read it from the sizes first)."""
+    ub = args.unit_bytes
+    chunks = 8
+    per = n_units // chunks
+    d_all = cp.generate(n_units, ub, seed=args.seed, zero_thresh=args.zero_thresh, device=dev)
+    in_off, in_len = cp.uniform_layout(n_units, ub, device=dev)
+    lens = torch.empty(n_units, dtype=torch.int64, device=dev)
+    st = torch.empty(n_units, dtype=torch.int32, device=dev)
+    cp.encoded_size_batch(d_all, in_off, in_len, lens, st)
+    off = cp.lengths_to_offsets(lens)
+    dense = torch.empty(int(off[-1].item()) + 16, dtype=torch.uint8, device=dev)
+    cp.encode_batch(d_all, in_off, in_len, dense, off[:-1].contiguous(), lens, lens, st)
+    h_in = d_all.cpu().pin_memory()
+    h_pk = dense.cpu().pin_memory()
+    h_off = off.cpu()
+    h_len = lens.cpu().pin_memory()
+    h_out = torch.empty(n_units * ub, dtype=torch.uint8).pin_memory()
+    h_pk2 = torch.empty_like(h_pk).pin_memory()
+    del d_all, dense
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    cmax = int((h_off[per::per] - h_off[:-1:per]).max().item()) + 16
+    bufs = []
+    for _ in range(2):
+        b = {"un": torch.empty(per * ub, dtype=torch.uint8, device=dev),
+             "pk": torch.empty(cmax, dtype=torch.uint8, device=dev),
+             "len": torch.empty(per, dtype=torch.int64, device=dev),
+             "olen": torch.empty(per, dtype=torch.int64, device=dev),
+             "st": torch.empty(per, dtype=torch.int32, device=dev),
+             "off": torch.empty(per + 1, dtype=torch.int64, device=dev)}
+        b["u_off"], b["u_len"] = cp.uniform_layout(per, ub, device=dev)
+        bufs.append(b)
+
+    def run_decode():
+        for c in range(chunks):
+            sm, b = streams[c % 2], bufs[c % 2]
+            lo, hi = int(h_off[c * per]), int(h_off[(c + 1) * per])
+            with torch.cuda.stream(sm):
+                b["pk"][:hi - lo].copy_(h_pk[lo:hi], non_blocking=True)
+                b["len"].copy_(h_len[c * per:(c + 1) * per], non_blocking=True)
+                cp.lengths_to_offsets(b["len"], out=b["off"], stream=sm)
+                cp.decode_batch(b["pk"], b["off"], b["len"], b["un"], b["u_off"], b["u_len"],
+                                b["olen"], b["st"], stream=sm)
+                h_out[c * per * ub:(c + 1) * per * ub].copy_(b["un"], non_blocking=True)
+
+    def run_encode():
+        for c in range(chunks):
+            sm, b = streams[c % 2], bufs[c % 2]
+            lo, hi = int(h_off[c * per]), int(h_off[(c + 1) * per])
+            with torch.cuda.stream(sm):
+                b["un"].copy_(h_in[c * per * ub:(c + 1) * per * ub], non_blocking=True)
+                cp.encoded_size_batch(b["un"], b["u_off"], b["u_len"], b["len"], b["st"], stream=sm)
+                cp.lengths_to_offsets(b["len"], out=b["off"], stream=sm)
+                cp.encode_batch(b["un"], b["u_off"], b["u_len"], b["pk"], b["off"], b["len"],
+                                b["olen"], b["st"], stream=sm)
+                h_pk2[lo:hi].copy_(b["pk"][:hi - lo], non_blocking=True)
+
+    res = {}
+    for name, fn in (("decode", run_decode), ("encode", run_encode)):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        res[name + "_GiB_s"] = round(3 * n_units * ub / (time.perf_counter() - t0) / 2 ** 30, 2)
+    res.update({"units": n_units, "unit_bytes": ub,
+                "bit_exact_roundtrip": bool(torch.equal(h_out, h_in) and
+                                            torch.equal(h_pk2[:int(h_off[-1])], h_pk[:int(h_off[-1])])),
+                "note": "GiB/s of unpacked bytes; pinned host buffers, 8 chunks over 2 streams, dense "
+                        "packed stream on the host side (PCIe Gen5 x16, 63 GB/s spec)"})
+    return res
 
 
 def load_traffic(config_key):
@@ -204,7 +283,9 @@ def main():
         dom, dom_ms = ("decode_kernel", dec_ms) if dec_ms >= enc_ms else ("encode_kernel", enc_ms)
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
         cfg_key = f"{n}x{ub}_t{args.zero_thresh}"
-        traffic = load_traffic(cfg_key)
+        prof = load_traffic(cfg_key) or {}
+        dom_prof = next((v for k, v in prof.items() if dom.split("_")[0] in k), None)
+        traffic = dom_prof["total_bytes"] if dom_prof else None
         line = {
             "metric": "GiB/s device-resident packed encode+decode, 1M x 4KiB segments",
             "value": round(value, 3),
@@ -227,13 +308,15 @@ def main():
                          "traffic": traffic, "alg_bytes_per_launch": alg_bytes},
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
-            "encode_GiB_s": round(world * 0 + n * ub / (enc_ms * 1e-3) / 2 ** 30, 2),
+            "encode_GiB_s": round(n * ub / (enc_ms * 1e-3) / 2 ** 30, 2),
             "decode_GiB_s": round(n * ub / (dec_ms * 1e-3) / 2 ** 30, 2),
             "packed_ratio": round(packed_all / U_total, 4),
             "packed_total_all_ranks": packed_all,
             "bit_exact_roundtrip": bool(ok_t.item()),
         }
         line.update(extra)
+        if world == 1 and not args.no_host_path:
+            line["host_path"] = host_path(args, dev)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(line), flush=True)

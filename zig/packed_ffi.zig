@@ -1,0 +1,119 @@
+//! Zig binding of include/capnp_packed.h for nullstyle/capnp-zig.
+//!
+//! Drop this file next to src/serialization/message.zig and apply the patch in
+//! INTEGRATION.md. The three wrappers below have exactly the signatures and error
+//! behaviour of the file-private functions they replace:
+//!   packPacked            message.zig:200-271
+//!   unpackPacked          message.zig:88-145
+//!   estimateUnpackedSize  message.zig:152-191
+//! Allocation follows the reference's contract: the returned slice is
+//! allocator-owned with its exact length (the reference returns
+//! `out.toOwnedSlice`, message.zig:144/270), so callers free it unchanged.
+//!
+//! Not compiled in this repo (no Zig toolchain in the build image); the C side
+//! it binds is exercised by tests/test_abi.py and tests/test_gpu_parity.py.
+const std = @import("std");
+
+pub const Status = enum(c_int) {
+    ok = 0,
+    invalid_message_size = 1,
+    unexpected_eof = 2,
+    overflow = 3,
+    out_of_space = 4,
+    invalid_argument = 5,
+    device_error = 6,
+    no_device = 7,
+    _,
+};
+
+// ---- single-buffer host entry points -------------------------------------
+extern "capnp_packed" fn capnp_packed_abi_version() u32;
+extern "capnp_packed" fn capnp_packed_last_error() [*:0]const u8;
+extern "capnp_packed" fn capnp_packed_encode_bound(n: usize) usize;
+extern "capnp_packed" fn capnp_packed_encode(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize) c_int;
+extern "capnp_packed" fn capnp_packed_decoded_size(in: [*]const u8, n: usize, out_size: *usize) c_int;
+extern "capnp_packed" fn capnp_packed_decode(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize) c_int;
+
+// ---- device batch entry points (pointers are device memory) ----------------
+pub extern "capnp_packed" fn capnp_packed_encode_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
+    d_out_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
+pub extern "capnp_packed" fn capnp_packed_encoded_size_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
+pub extern "capnp_packed" fn capnp_packed_decode_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
+    d_out_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
+pub extern "capnp_packed" fn capnp_packed_decoded_size_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
+pub extern "capnp_packed" fn capnp_packed_scan_scratch_bytes(n: u32) usize;
+pub extern "capnp_packed" fn capnp_packed_lengths_to_offsets(
+    d_len: [*]const u64, n: u32, base: u64, d_off: [*]u64,
+    d_scratch: ?*anyopaque, scratch_bytes: usize, stream: ?*anyopaque,
+) c_int;
+
+/// The reference's error names, plus the two the device can add. `NoDevice`
+/// lets the patched message.zig fall back to its own Zig body.
+pub const Error = error{
+    InvalidMessageSize,
+    UnexpectedEof,
+    Overflow,
+    OutOfMemory,
+    PackedDeviceError,
+    NoDevice,
+};
+
+fn check(status: c_int) Error!void {
+    return switch (@as(Status, @enumFromInt(status))) {
+        .ok => {},
+        .invalid_message_size => error.InvalidMessageSize,
+        .unexpected_eof => error.UnexpectedEof,
+        .overflow => error.Overflow,
+        .out_of_space => error.OutOfMemory, // capacity is sized by us; unreachable in practice
+        .no_device => error.NoDevice,
+        else => {
+            std.log.err("capnp_packed: {s}", .{capnp_packed_last_error()});
+            return error.PackedDeviceError;
+        },
+    };
+}
+
+/// message.zig:200 `fn packPacked(allocator, bytes) ![]u8`.
+pub fn packPacked(allocator: std.mem.Allocator, bytes: []const u8) Error![]u8 {
+    if (bytes.len % 8 != 0) return error.InvalidMessageSize; // message.zig:201
+    const buf = try allocator.alloc(u8, capnp_packed_encode_bound(bytes.len));
+    errdefer allocator.free(buf);
+    var len: usize = 0;
+    try check(capnp_packed_encode(bytes.ptr, bytes.len, buf.ptr, buf.len, &len));
+    return allocator.realloc(buf, len);
+}
+
+/// message.zig:152 `fn estimateUnpackedSize(packed) !usize`.
+pub fn estimateUnpackedSize(packed_bytes: []const u8) Error!usize {
+    var size: usize = 0;
+    try check(capnp_packed_decoded_size(packed_bytes.ptr, packed_bytes.len, &size));
+    return size;
+}
+
+/// message.zig:88 `fn unpackPacked(allocator, packed) ![]u8`. Like the reference,
+/// truncated input fails with UnexpectedEof before any output is produced.
+pub fn unpackPacked(allocator: std.mem.Allocator, packed_bytes: []const u8) Error![]u8 {
+    const total = try estimateUnpackedSize(packed_bytes);
+    const out = try allocator.alloc(u8, total);
+    errdefer allocator.free(out);
+    var len: usize = 0;
+    try check(capnp_packed_decode(packed_bytes.ptr, packed_bytes.len, out.ptr, out.len, &len));
+    std.debug.assert(len == total);
+    return out;
+}
+
+pub fn abiVersion() u32 {
+    return capnp_packed_abi_version();
+}
