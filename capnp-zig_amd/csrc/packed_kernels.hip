@@ -4,27 +4,28 @@
 //   encode  nullstyle/capnp-zig src/serialization/message.zig:200-271 (packPacked)
 //   decode  message.zig:88-145 (unpackPacked) with the size pass of :152-191
 //
-// Execution model: one 64-lane wave owns one unit (one packPacked
-// / unpackPacked call). A unit is staged in the wave's private LDS slice with
-// coalesced 16-B global loads, processed with wave-wide scans, assembled in LDS
-// and written back with coalesced 16-B stores. No MFMA: this is byte compaction.
+// Execution model: encode and the wave decoder give one 64-lane
+// wave one unit (one packPacked / unpackPacked call): the unit is staged in the
+// wave's private LDS slice with coalesced 16-B global loads, processed with
+// wave-wide scans and written back with coalesced stores. The stream decoder
+// gives each lane one unit. No MFMA: this is byte compaction.
 //
 //   encode: lane j owns words [8j, 8j+8). Each word's zero-byte tag is formed
 //           with SWAR + a multiply gather; zero/literal runs (greedy, 256-capped)
 //           are resolved with wave max/min scans of break positions; a wave sum
 //           scan gives every lane its output byte offset; each lane appends its
 //           records to a byte stream in LDS (u64 ds_or at 8-B granularity).
-//   decode: the record chain (tag -> record length) is serial. Lanes walk
-//           64-byte chunks of the staged packed bytes speculatively from the
-//           chunk start; a fix-up loop re-walks lanes whose true entry point is
-//           not on their speculative chain (walks couple after a few records,
-//           so 1-2 rounds are typical, 64 worst case). Record starts become one
-//           u64 bitmask per lane; a wave sum scan of words-per-record gives
-//           output word offsets; mixed words are expanded with v_perm_b32 and a
-//           selector LUT; zero runs cost nothing (the LDS window is pre-zeroed).
+//   decode: the record chain (tag -> record length) is serial. Two decoders:
+//           decode_stream_kernel (default) gives each lane one unit and walks its
+//           chain once, emitting 16-word output rounds through an LDS ring that
+//           the wave stores with coalesced 128-B lines; decode_wave_kernel gives
+//           each wave one unit, resolves the chain through 64 lane chunks with
+//           speculative walks + verification rounds, and stores 64 consecutive
+//           words per instruction.
 //
-// Units larger than the fast-path limits run a serial per-wave path (lane 0)
-// that reads and writes global memory directly (correct for any size; slow).
+// Encode units larger than 4 KiB run a serial per-wave path (lane 0) that reads
+// and writes global memory directly (correct for any size; slow). Both decoders
+// handle any unit size on their fast path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -43,12 +44,6 @@ constexpr uint32_t kEncMaxWords = 512;                 // 4 KiB unpacked unit
 constexpr uint32_t kEncRow = 80;                       // 64 B words + 16 B pad per lane row
 constexpr uint32_t kEncLds = 64 * kEncRow;             // 5120 B; reused for the packed output
 // max packed size of 512 words is 9*512+1 = 4609 B; + 16 B align slack + 16 B round-up <= 5120
-
-// ---- decode fast path ------------------------------------------------------
-constexpr uint32_t kDecIn = 4864;                      // staged packed bytes
-constexpr uint32_t kDecPMax = kDecIn - 16 - 32;        // 4816 B of packed input per unit
-constexpr uint32_t kDecWinWords = 512;                 // output window (words)
-constexpr uint32_t kDecOut = kDecWinWords * 8 + 16;    // 4112 B
 
 enum : int32_t {
     ST_OK = CAPNP_PACKED_OK,
@@ -156,22 +151,23 @@ __device__ __forceinline__ uint64_t lds_read_u64_unaligned(const uint8_t* base, 
 }
 
 // Stage nch 16-B chunks from global g[0 .. 16*nch) into lds[0 .. 16*nch):
-// lane l moves chunks l, l+64, ... All K loads are issued before the first LDS
-// store (addresses clamped to the last chunk, guards wave-uniform) so they stay
-// in VGPRs and overlap in flight.
+// lane l moves chunks l, l+64, ... Loads AND stores are unconditional, with the
+// chunk index clamped to nch-1 (a clamped lane re-writes the last chunk with the
+// same bytes), so the compiler cannot sink the loads into guarded blocks: all K
+// loads are in flight together and one vmcnt wait lands them.
 template <int K>
 __device__ __forceinline__ void stage_linear(uint8_t* lds, const uint8_t* g, uint32_t nch, uint32_t lane) {
     if (nch == 0) return;
     uint4 v[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {  // unconditional: clamped lanes re-read the last chunk (same line)
-        uint32_t c = min(lane + 64u * k, nch - 1);
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = min(lane + 64u * k, nch - 1);
         v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        uint32_t c = lane + 64u * k;
-        if ((uint32_t)(64 * k) < nch && c < nch) *reinterpret_cast<uint4*>(lds + 16 * c) = v[k];
+        const uint32_t c = min(lane + 64u * k, nch - 1);
+        *reinterpret_cast<uint4*>(lds + 16 * c) = v[k];
     }
 }
 
@@ -566,215 +562,6 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// DECODE
-// ---------------------------------------------------------------------------
-
-// Walk record starts of one 64-byte chunk [cs, ce) from entry e.
-// Record length: 00 -> 2, FF -> 10 + 8*count, other -> 1 + popc(tag)  (message.zig:152-191)
-__device__ __forceinline__ void walk_chunk(const uint8_t* lds, uint32_t e, uint32_t cs, uint32_t ce,
-                                           uint64_t& mask, uint32_t& exit_pos) {
-    uint32_t pos = e;
-    uint64_t m = 0;
-    while (pos < ce) {
-        m |= 1ULL << (pos - cs);
-        uint32_t t = lds[pos];
-        uint32_t len = (t == 0) ? 2u : (t == 0xFF ? 10u + 8u * (uint32_t)lds[pos + 9] : 1u + __popc(t));
-        pos += len;
-    }
-    mask = m;
-    exit_pos = pos;
-}
-
-template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint64_t* __restrict__ in_len,
-                                                        uint32_t n, uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        const uint64_t* __restrict__ out_cap,
-                                                        uint64_t* __restrict__ out_len,
-                                                        int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[kWavesPerBlock * kDecIn];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[kWavesPerBlock * (WRITE ? kDecOut : 16)];
-    __shared__ uint64_t lut[256];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WRITE) {
-        lut[threadIdx.x] = expand_selector(threadIdx.x);
-        __syncthreads();
-    }
-    const uint32_t unit = blockIdx.x * kWavesPerBlock + wave;
-    if (unit >= n) return;
-    uint8_t* lin = s_in + wave * kDecIn;
-    uint8_t* lout = s_out + wave * (WRITE ? kDecOut : 16);
-
-    const uint64_t b0 = in_off[unit];
-    uint64_t ob = 0, cap = 0;
-    int32_t st = ST_OK;
-    if (WRITE) {
-        ob = out_off[unit];
-        cap = out_cap[unit];
-        if (reinterpret_cast<uintptr_t>(out + ob) & 7) st = ST_ARG;
-    }
-    if (st != ST_OK) {
-        if (lane == 0) { out_len[unit] = 0; status[unit] = st; }
-        return;
-    }
-    const uint64_t P64 = in_len[unit];
-    if (P64 > kDecPMax) {
-        if (lane == 0) {
-            uint64_t U = 0;
-            int32_t s2 = serial_decoded_size(in + b0, P64, &U);
-            if (s2 != ST_OK) U = 0;
-            else if (WRITE) {
-                if (U > cap) s2 = ST_SPACE;
-                else serial_unpack(in + b0, P64, out + ob);
-            }
-            out_len[unit] = U;
-            status[unit] = s2;
-        }
-        return;
-    }
-    const uint32_t P = (uint32_t)P64;
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(in + b0) & 15);
-    const uint32_t end = s + P;
-
-    // ---- stage packed bytes (16-B aligned chunks; bytes outside [s, end) are ignored)
-    stage_linear<5>(lin, in + b0 - s, (end + 15) >> 4, lane);
-    wave_lds_sync();
-
-    // ---- record discovery: speculative chunk walks + fix-up ---------------------------
-    const uint32_t nc = (P + 63) >> 6;  // 64-byte chunks (<= 76)
-    uint64_t m[2] = {0, 0};
-    uint32_t carry = s;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        if ((uint32_t)(64 * r) >= nc) break;
-        const uint32_t c = 64 * r + lane;
-        const bool active = c < nc;
-        const uint32_t cs = s + 64 * c;
-        const uint32_t ce = min(cs + 64, end);
-        uint64_t mask = 0;
-        uint32_t ex = cs;
-        if (active) walk_chunk(lin, lane == 0 ? carry : cs, cs, ce, mask, ex);
-        uint32_t entry = carry;
-        for (int it = 0; it < 66; ++it) {
-            uint32_t prev = __shfl_up(ex, 1, kWave);
-            entry = (lane == 0) ? carry : prev;
-            bool ok = true;
-            if (active) {
-                if (entry >= ce) ok = (mask == 0 && ex == entry);
-                else ok = (entry >= cs) && ((mask >> (entry - cs)) & 1ULL);
-            }
-            if (__all(ok)) break;
-            if (!ok) walk_chunk(lin, entry, cs, ce, mask, ex);
-        }
-        if (active && entry < ce && entry > cs) mask &= ~0ULL << (entry - cs);
-        m[r] = mask;
-        const uint32_t last = min(nc - 64 * r, 64u) - 1;
-        carry = readlane(ex, last);
-    }
-    const bool eof = (carry != end);  // the record chain must end exactly at the last byte
-
-    // ---- words per lane, output word offsets ----------------------------------------
-    uint32_t wc[2] = {0, 0};
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        uint64_t bits = m[r];
-        const uint32_t cs = s + 64 * (64 * r + lane);
-        while (bits) {
-            uint32_t b = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            uint32_t pos = cs + b;
-            uint32_t t = lin[pos];
-            wc[r] += (t == 0) ? 1u + lin[pos + 1] : (t == 0xFF ? 1u + lin[pos + 9] : 1u);
-        }
-    }
-    const uint32_t inc0 = wave_incl_sum(wc[0], lane);
-    const uint32_t tot0 = readlane(inc0, 63);
-    const uint32_t inc1 = wave_incl_sum(wc[1], lane);
-    const uint32_t W = tot0 + readlane(inc1, 63);
-    const uint32_t wbase[2] = {inc0 - wc[0], tot0 + inc1 - wc[1]};
-
-    if (eof) {
-        if (lane == 0) { out_len[unit] = 0; status[unit] = ST_EOF; }
-        return;
-    }
-    const uint64_t U = 8ULL * W;
-    if (!WRITE) {
-        if (lane == 0) { out_len[unit] = U; status[unit] = ST_OK; }
-        return;
-    }
-    if (U > cap) {
-        if (lane == 0) { out_len[unit] = U; status[unit] = ST_SPACE; }
-        return;
-    }
-
-    // ---- expansion, one 512-word output window at a time -------------------------------
-    const uint32_t so = (uint32_t)(reinterpret_cast<uintptr_t>(out + ob) & 15);  // 0 or 8
-    for (uint32_t win = 0; win < W; win += kDecWinWords) {
-        const uint32_t nwin = min(kDecWinWords, W - win);
-        const uint32_t nbytes = so + 8 * nwin;
-        const uint32_t nch = (nbytes + 15) >> 4;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            uint32_t c = lane + 64 * k;
-            if (c < nch) *reinterpret_cast<uint4*>(lout + 16 * c) = make_uint4(0, 0, 0, 0);
-        }
-        wave_lds_sync();
-        const uint32_t wend = win + nwin;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            uint64_t bits = m[r];
-            const uint32_t cs = s + 64 * (64 * r + lane);
-            uint32_t wo = wbase[r];
-            while (bits && wo < wend) {
-                uint32_t b = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                uint32_t pos = cs + b;
-                uint32_t t = lin[pos];
-                if (t == 0) {
-                    wo += 1u + lin[pos + 1];                         // zero run: window is pre-zeroed
-                } else if (t == 0xFF) {
-                    uint32_t c = lin[pos + 9];
-                    uint32_t k0 = wo < win ? win - wo : 0u;
-                    uint32_t k1 = min(c + 1, wend - wo);
-                    for (uint32_t k = k0; k < k1; ++k) {
-                        uint32_t src = k == 0 ? pos + 1 : pos + 10 + 8 * (k - 1);
-                        *reinterpret_cast<uint64_t*>(lout + so + 8 * (wo + k - win)) =
-                            lds_read_u64_unaligned(lin, src);
-                    }
-                    wo += 1 + c;
-                } else {
-                    if (wo >= win) {
-                        uint64_t d = lds_read_u64_unaligned(lin, pos + 1);
-                        *reinterpret_cast<uint64_t*>(lout + so + 8 * (wo - win)) = perm64(d, lut[t]);
-                    }
-                    wo += 1;
-                }
-            }
-        }
-        wave_lds_sync();
-        uint8_t* gdst = out + ob + 8ULL * win - so;  // 16-B aligned
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            uint32_t c = lane + 64 * k;
-            if (c < nch) {
-                uint32_t cb = 16 * c;
-                if (cb >= so && cb + 16 <= nbytes) {
-                    *reinterpret_cast<uint4*>(gdst + cb) = *reinterpret_cast<const uint4*>(lout + cb);
-                } else {  // one valid 8-byte half
-                    uint32_t h = cb < so ? cb + 8 : cb;
-                    *reinterpret_cast<uint64_t*>(gdst + h) = *reinterpret_cast<const uint64_t*>(lout + h);
-                }
-            }
-        }
-        wave_lds_sync();
-    }
-    if (lane == 0) { out_len[unit] = U; status[unit] = ST_OK; }
-}
-
-// ---------------------------------------------------------------------------
 // DECODE, lane per unit
 // ---------------------------------------------------------------------------
 // The record chain (tag -> record length) is inherently serial and speculative
@@ -907,7 +694,7 @@ __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// DECODE, lane per unit, lockstep output rounds (the production decoder)
+// DECODE, lane per unit, lockstep output rounds (the default decoder)
 // ---------------------------------------------------------------------------
 // Lane l of a wave owns unit wave_base + l and walks its record chain exactly
 // once (input side: per-lane register window, as in decode_lane_kernel). The
@@ -922,7 +709,6 @@ constexpr int kRingRow = kRoundWords * 8 + 16;  // 144 B: 16-B aligned, staggers
 constexpr int kStreamWaves = 2;                 // waves per block
 constexpr int kStreamBlock = kStreamWaves * kWave;
 
-template <uint32_t PF>
 __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8_t* __restrict__ in,
                                                                      const uint64_t* __restrict__ in_off,
                                                                      const uint64_t* __restrict__ in_len,
@@ -932,7 +718,6 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
                                                                      uint64_t* __restrict__ out_len,
                                                                      int32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kStreamWaves * kWave * kRingRow];
-    __shared__ uint32_t pf_sink[kStreamWaves * kWave];  // LDS-DMA prefetch target, never read
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* ring = ring_all + wave * (kWave * kRingRow);
@@ -960,26 +745,13 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
     load_piece(base, npieces, 0, q0, q1);
     load_piece(base, npieces, 1, q2, q3);
     load_piece(base, npieces, 2, n0, n1);
-    uint32_t* sink = pf_sink + wave * kWave;
     auto ensure = [&](uint32_t p) {
         while (p - wb >= 16) {
             q0 = q2; q1 = q3; q2 = n0; q3 = n1;
             wb += 16;
             load_piece(base, npieces, (wb >> 4) + 2, n0, n1);
-            if (PF) {  // pull the line PF bytes ahead into L2 (LDS-DMA into a sink: no VGPR, no wait)
-                const uint32_t pa = wb + PF;
-                if ((pa & 127) == 0 && pa < npieces * 16) {
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + pa),
-                                                     (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
-                }
-            }
         }
     };
-    if (PF) {  // warm the first PF bytes
-        for (uint32_t pa = 128; pa < PF && pa < npieces * 16; pa += 128)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + pa),
-                                             (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
-    }
     uint64_t pos = s;          // next tag
     uint64_t lit = 0;          // next literal word (valid while pend_lit)
     uint32_t pend_zero = 0, pend_lit = 0;
@@ -1065,7 +837,6 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
         wo += nw;
         wave_lds_sync();
     }
-    if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no prefetch may land after the wave exits
     if (!valid) return;
     if (st != ST_OK) {
         out_len[unit] = 0;
@@ -1077,628 +848,333 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
 }
 
 // ---------------------------------------------------------------------------
-// DECODE, lane per unit, LDS-DMA input ring + lockstep output rounds
+// DECODE, wave per unit (CPK_DECODE_VARIANT=0; same speed as the stream decoder
+// at p=0.5, exact HBM traffic; see profiles/r01_decode_experiments.md)
 // ---------------------------------------------------------------------------
-// Input side: each lane's packed bytes stream through a per-lane ring of
-// kSlots 64-byte chunks in LDS, filled by LDS-DMA (global_load_lds_dwordx4: no
-// VGPR destination, so nothing forces a wait at issue). Chunks are issued at
-// round ends as soon as the slot they reuse is consumed, so every lane keeps
-// ~3 chunks (~192 B) in flight; one s_waitcnt per round end lands them. Within
-// a DMA instruction, 4 lanes move the 4 x 16 B of one lane's chunk; the 16-B
-// pieces are XOR-swizzled by lane so lanes reading the same logical offset hit
-// different LDS banks (swizzle applied to the DMA source, read with the same
-// swizzle: linear destination).
-// Output side: as decode_stream_kernel (lockstep 16-word rounds, cooperative
-// 128-B line stores).
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-struct DmaCfg {
-    static constexpr uint32_t kPieces = CHUNK / 16;                // 16-B pieces per lane chunk
-    static constexpr uint32_t kTasks = kWave / kPieces;            // lanes whose chunk one DMA moves
-    static constexpr uint32_t kSlotBytes = kWave * CHUNK;          // one slot for every lane
-    static constexpr uint32_t kInRing = SLOTS * kSlotBytes;
-    static constexpr uint32_t kRow = ROUND * 8 + 16;               // output row stride (16-B aligned, staggered)
-    static constexpr uint32_t kOutRing = kWave * kRow;
-    static constexpr uint32_t kLanesPerRow = ROUND / 2;            // 16 B per lane in the store
-    static constexpr uint32_t kRowsPerStep = kWave / kLanesPerRow;
-    static constexpr uint32_t kSteps = kWave / kRowsPerStep;
-    static constexpr uint32_t kBlock = WAVES * kWave;
-    static_assert(CHUNK % 16 == 0 && (SLOTS & (SLOTS - 1)) == 0 && ROUND % 2 == 0, "cfg");
-    __device__ static uint32_t swz(uint32_t l) { return (l >> 2) & (kPieces - 1); }
-};
+// One wave owns one unit. The unit's packed bytes are processed in windows of
+// up to kWvWin bytes (one window for units up to ~4.5 KiB packed), each staged
+// in the wave's LDS slice with coalesced 16-B loads. Lane j owns the chunk
+// [j*C, (j+1)*C) of the window and must find the true record chain through it
+// (tag -> record length -> next tag, message.zig:152-191), which is serial:
+//
+//   walk A   every lane walks its chunk from the chunk start (a guess),
+//            marking the tags it visits in a per-byte mark array (walk id 1);
+//   walk B   every lane walks from the exit of its left neighbour's walk A
+//            (the neighbour's guess of where the chain enters this chunk),
+//            stopping as soon as it reaches a marked tag: from there the
+//            chain is the marked walk's, so its exit is known (walk id 2);
+//   rounds   lane j is verified when its entry equals lane j-1's exit and
+//            lane j-1 is verified (lane 0 enters at 0, the window start is a
+//            tag). Every lane whose entry disagrees re-walks from its
+//            neighbour's exit, again stopping at the first marked tag. Each
+//            round verifies at least the first disagreeing lane, so this ends
+//            in <= 64 rounds; because chains from different entries couple
+//            within a few records, 0-2 rounds are typical.
+//   count    each lane sums the output words of its verified records; a wave
+//            scan gives every lane its output word offset;
+//   expand   each lane expands its records (v_perm_b32 scatter of the nonzero
+//            bytes) and stores the words; zero runs and literal runs longer
+//            than a few words are handed to the whole wave (coalesced).
+//
+// The window's exit (lane 63's verified exit) is the next window's start, so
+// any unit size works; LDS-resident chunks keep every chain step an LDS read.
+constexpr uint32_t kWvWaves = 4;                      // waves (units) per block
+constexpr uint32_t kWvBlock = kWvWaves * kWave;
+constexpr uint32_t kWvWin = 4608;                     // packed bytes per window (64 chunks x 72 B)
+constexpr uint32_t kWvPk = kWvWin + 64;               // + 15 B alignment slack + 16 B overshoot + read slack
+constexpr uint32_t kWvCmin = 32;                      // minimum chunk bytes per lane
+constexpr uint32_t kWvStageK = (kWvPk / 16 + 63) / 64;
+constexpr uint32_t kEOFX = 0xFFFFFFFFu;               // "the chain ran past the end of the input"
+constexpr uint32_t kWvExtLane = 3;                    // longer literal runs are listed by the whole wave
+constexpr uint32_t kWvList = 1024;                    // output words per expand pass (u16 list in the mark array)
+constexpr uint32_t kPosMask = 0x1FFFu;                // list code: window position (< 8192)
+constexpr uint32_t kLit = 0x2000u;                    // list code: literal word (identity selector)
+constexpr uint32_t kZero = 0x8000u;                   // list code: zero word
+constexpr uint32_t kZero2 = kZero | (kZero << 16);
+static_assert(kWvList * 2 <= kWvWin, "list aliases the mark array");
+static_assert(kWvWin + 16 + 2058 < 8192, "list codes hold window positions");
+constexpr uint32_t kWvSlack = 16;                     // plausible entry offset into a chunk (records are <= 9 B)
 
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-__global__ __launch_bounds__(WAVES * 64) void decode_dma_kernel(const uint8_t* __restrict__ in,
-                                                                const uint64_t* __restrict__ in_off,
-                                                                const uint64_t* __restrict__ in_len,
-                                                                uint32_t n, uint8_t* __restrict__ out,
-                                                                const uint64_t* __restrict__ out_off,
-                                                                const uint64_t* __restrict__ out_cap,
-                                                                uint64_t* __restrict__ out_len,
-                                                                int32_t* __restrict__ status) {
-    using C = DmaCfg<CHUNK, SLOTS, ROUND, WAVES>;
-    __shared__ __attribute__((aligned(16))) uint8_t in_all[WAVES * C::kInRing];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[WAVES * C::kOutRing];
+__device__ __forceinline__ uint32_t wv_sel_exit(uint32_t m, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t e4,
+                                                uint32_t e5, uint32_t e6, uint32_t e7) {
+    uint32_t r = e7;
+    r = (m == 6) ? e6 : r;
+    r = (m == 5) ? e5 : r;
+    r = (m == 4) ? e4 : r;
+    r = (m == 3) ? e3 : r;
+    r = (m == 2) ? e2 : r;
+    r = (m == 1) ? e1 : r;
+    return r;
+}
+
+// Walk the chain from window position r to the first tag position >= cend,
+// marking visited tags with id (id 0: no marks). Stops at a tag marked by an
+// earlier walk and reports its id in hit (the caller maps it to that walk's
+// exit). Returns kEOFX if a record runs past the input end (rem bytes).
+__device__ __forceinline__ uint32_t wv_len(uint32_t t, uint32_t c) {  // record length for tag t
+    const uint32_t zf = (t == 0u) | (t == 0xFFu);             // 00 -> 2, FF -> 10 + 8c, else 1 + popc
+    return 1u + __popc(t) + zf + ((t == 0xFFu) ? 8u * c : 0u);
+}
+
+__device__ __forceinline__ uint32_t wv_walk(const uint8_t* pk, uint8_t* mk, uint32_t sh, uint32_t rem, uint32_t r,
+                                            uint32_t cend, uint32_t id, uint32_t& hit) {
+    uint32_t h = 0;
+    bool go = r < cend;
+    while (go) {  // body is branch-free: one loop exit
+        uint32_t m = mk[r];
+        uint32_t t = pk[sh + r];
+        uint32_t c = pk[sh + r + 9];
+        asm volatile("" : "+v"(m), "+v"(t), "+v"(c));  // issue the three LDS reads together, one wait
+        const uint32_t len = wv_len(t, c);
+        const bool coupled = m != 0;
+        mk[r] = (uint8_t)(coupled ? m : id);  // unconditional: rewrites m where coupled or id == 0
+        h = m;
+        const uint32_t nr = (r + len > rem) ? kEOFX : r + len;
+        r = coupled ? r : nr;
+        go = !coupled && r < cend;
+    }
+    hit = h;
+    return r;
+}
+
+// Unaligned 8-byte LDS read as two aligned ds_read_b64 and a branch-free funnel
+// shift (a byte-aligned ds_read_b64 is legal on gfx950 but measured ~2x slower
+// in the expand loop: the LDS splits it).
+__device__ __forceinline__ uint64_t lds_u64_at(const uint8_t* base, uint32_t p) {
+    const uint32_t a = p & ~7u;
+    const uint64_t lo = *reinterpret_cast<const uint64_t*>(base + a);
+    const uint64_t hi = *reinterpret_cast<const uint64_t*>(base + a + 8);
+    const uint32_t s = (p & 7u) * 8u;
+    return (lo >> s) | ((hi << 1) << (63u - s));
+}
+// Unaligned 8-byte global read (gfx950 unaligned-buffer-access: one global_load_dwordx2).
+__device__ __forceinline__ uint64_t gload_u64_unaligned(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+
+#ifdef CPK_WV_PROF
+// Phase probe (tools/wv_probe.hip): per unit, cycle stamps after each phase and counters.
+__device__ uint64_t* cpk_wv_prof;
+#define WV_STAMP(k) do { const uint64_t t_ = __builtin_readcyclecounter(); if (lane == 0) cpk_wv_prof[16ull * unit + (k)] = t_; } while (0)
+#define WV_COUNT(k, v) do { if (lane == 0) cpk_wv_prof[16ull * unit + (k)] += (v); } while (0)
+#else
+#define WV_STAMP(k) do { } while (0)
+#define WV_COUNT(k, v) do { } while (0)
+#endif
+
+__global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __restrict__ in,
+                                                               const uint64_t* __restrict__ in_off,
+                                                               const uint64_t* __restrict__ in_len, uint32_t n,
+                                                               uint8_t* __restrict__ out,
+                                                               const uint64_t* __restrict__ out_off,
+                                                               const uint64_t* __restrict__ out_cap,
+                                                               uint64_t* __restrict__ out_len,
+                                                               int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
+    __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
+    __shared__ uint64_t lut[256];  // tag -> v_perm selector that scatters the packed bytes (FF: identity, 00: zero)
+    lut[threadIdx.x] = expand_selector(threadIdx.x);
+    __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* iring = in_all + wave * C::kInRing;
-    uint8_t* oring = ring_all + wave * C::kOutRing;
-    const uint32_t unit = (blockIdx.x * WAVES + wave) * kWave + lane;
-    const bool valid = unit < n;
+    const uint32_t unit = blockIdx.x * kWvWaves + wave;
+    if (unit >= n) return;  // wave-uniform
+    uint8_t* pk = pk_all + wave * kWvPk;
+    uint8_t* mk = mk_all + wave * kWvWin;
 
-    const uint8_t* src = in;
-    uint64_t P = 0, capw = 0;
-    uint8_t* dstb = out;
-    int32_t st = ST_OK;
-    if (valid) {
-        src = in + in_off[unit];
-        P = in_len[unit];
-        dstb = out + out_off[unit];
-        capw = out_cap[unit] >> 3;
-        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
-        if (P > 0xFFFF0000ULL) st = ST_ARG;  // 32-bit stream offsets
-    }
-    bool live = valid && st == ST_OK;
-    if (!live) P = 0;
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    const uint8_t* base = src - s;                    // 16-B aligned
-    const uint32_t end = s + (uint32_t)P;             // logical stream [s, end)
-    const uint32_t npieces = live ? (end + 15) >> 4 : 0;
-    const uint32_t padded = npieces * 16;             // bytes the DMA ever delivers for this lane
-    const uint32_t nchunks = (padded + CHUNK - 1) / CHUNK;
-    uint32_t maxchunks = nchunks;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxchunks = max(maxchunks, (uint32_t)__shfl_xor((int)maxchunks, d, kWave));
-    maxchunks = __builtin_amdgcn_readfirstlane(maxchunks);
-
-    // DMA task descriptors: in pass k, lane L moves source piece kPieces*k + (i ^ swz(r))
-    // of lane r = kTasks*g + L/kPieces into destination piece i = L % kPieces of r's slot k % SLOTS.
-    uint64_t dsrc[C::kPieces];
-    uint32_t dnp[C::kPieces], dpc[C::kPieces];
-#pragma unroll
-    for (uint32_t g = 0; g < C::kPieces; ++g) {
-        const uint32_t r = C::kTasks * g + lane / C::kPieces;
-        const uint32_t sp = (lane % C::kPieces) ^ C::swz(r);
-        dsrc[g] = __shfl(reinterpret_cast<uint64_t>(base), r, kWave) + 16ULL * sp;
-        dnp[g] = __shfl(npieces, r, kWave);
-        dpc[g] = sp;
-    }
-    uint32_t issued = 0;  // wave-uniform: chunks issued for every lane
-    auto dma_pass = [&]() {
-        const uint32_t k = issued;
-        uint8_t* slot = iring + (k & (SLOTS - 1)) * C::kSlotBytes;
-#pragma unroll
-        for (uint32_t g = 0; g < C::kPieces; ++g) {
-            if (C::kPieces * k + dpc[g] < dnp[g]) {
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[g] + (uint64_t)CHUNK * k),
-                                                 (__attribute__((address_space(3))) void*)(slot + g * C::kTasks * CHUNK),
-                                                 16, 0, 0);
-            }
+    const uint8_t* src = in + in_off[unit];
+    const uint64_t P = in_len[unit];
+    uint8_t* dstb = out + out_off[unit];
+    const uint64_t capw = out_cap[unit] >> 3;
+    if (reinterpret_cast<uintptr_t>(dstb) & 7) {
+        if (lane == 0) {
+            out_len[unit] = 0;
+            status[unit] = ST_ARG;
         }
-        issued = k + 1;
-    };
-
-    uint32_t pos = s, lit = 0, pend_zero = 0, pend_lit = 0;
-    uint64_t wo = 0;
-    const uint32_t laneb = lane * CHUNK;
-    const uint32_t swz16 = C::swz(lane) << 4;
-    auto u64_at = [&](uint32_t y) -> uint64_t {  // y 8-aligned logical offset
-        const uint32_t a = ((y / CHUNK) & (SLOTS - 1)) * C::kSlotBytes + laneb + ((y & (CHUNK - 1)) ^ swz16);
-        return *reinterpret_cast<const uint64_t*>(iring + a);
-    };
-    // issue a pass while the slowest live lane has freed the slot the pass reuses
-    auto may_issue = [&]() -> bool {
-        const uint32_t mr = (pend_lit ? lit : pos) / CHUNK;  // oldest chunk still needed
-        return issued < maxchunks && __all(!live || issued < mr + SLOTS);
-    };
-
-    for (uint32_t q = 0; q < SLOTS && may_issue(); ++q) dma_pass();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t landed = issued;
-
-    uint64_t* myrow = reinterpret_cast<uint64_t*>(oring + lane * C::kRow);
-    while (__any(live)) {
-        const uint32_t limit = (landed * CHUNK >= padded) ? 0xFFFFFFFFu : landed * CHUNK;
-        uint32_t nw = 0;
-        bool frozen = false;
-        for (uint32_t k = 0; k < ROUND; ++k) {
-            const bool ok = live && !frozen;
-            if (!__any(ok)) break;
-            const bool isZ = pend_zero != 0;
-            const bool isL = !isZ && pend_lit != 0;
-            const bool isR = !isZ && !isL && pos < end;
-            const uint32_t rp = isL ? lit : pos;
-            const uint32_t y = rp & ~7u;
-            const uint64_t a = u64_at(y), b = u64_at(y + 8);
-            const uint32_t o = rp & 7;
-            const uint32_t sh = 8 * o;
-            const uint64_t lw = sh ? ((a >> sh) | (b << (64 - sh))) : a;         // literal word at rp
-            const uint32_t t = (uint32_t)(a >> sh) & 0xFFu;                      // tag at rp
-            const uint64_t pay = (o == 7) ? b : ((a >> (sh + 8)) | (b << (56 - sh)));  // bytes rp+1..rp+8
-            uint32_t cnt = (uint32_t)(b >> (sh + 8)) & 0xFFu;                    // byte rp+9 (o <= 6)
-            bool avail = y + 16 <= limit;
-            const bool ff7 = ok && isR && avail && t == 0xFF && o == 7;
-            if (__any(ff7)) {  // rare: FF count byte in the next 8-byte word
-                if (ff7) {
-                    avail = y + 24 <= limit;
-                    if (avail) cnt = (uint32_t)u64_at(y + 16) & 0xFFu;
-                }
-            }
-            const uint32_t kk = __popc(t);
-            const bool tz = t == 0, tf = t == 0xFF;
-            const uint32_t hdr = tz ? 2u : (tf ? 10u : 1u + kk);                  // bytes needed up front
-            const uint32_t rlen = tf ? 10u + 8u * cnt : hdr;                      // record length
-            const bool eof = (pos + hdr > end) || (pos + rlen > end);             // message.zig:152-191
-            const bool stepZ = ok && isZ;
-            const bool stepL = ok && isL && avail;
-            const bool stepR = ok && isR && avail && !eof;
-            const bool err = ok && isR && avail && eof;
-            const bool fin = ok && !isZ && !isL && !isR;
-            if (ok && (isL || isR) && !avail) frozen = true;
-            if (err) st = ST_EOF;
-            if (err || fin) live = false;
-            const uint64_t rword = tz ? 0 : (tf ? pay : expand_word(pay, t));
-            const uint64_t word = isZ ? 0 : (isL ? lw : rword);
-            myrow[nw] = word;
-            nw += (stepZ || stepL || stepR) ? 1u : 0u;
-            pend_zero = stepZ ? pend_zero - 1 : ((stepR && tz) ? (uint32_t)pay & 0xFFu : pend_zero);
-            pend_lit = stepL ? pend_lit - 1 : ((stepR && tf) ? cnt : pend_lit);
-            lit = stepL ? lit + 8 : ((stepR && tf) ? pos + 10 : lit);
-            pos = stepR ? pos + rlen : pos;
-        }
-        wave_lds_sync();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMAs issued at the last round end have landed
-        landed = issued;
-        // ---- cooperative store of this round's rows: lane L moves 16 B of one row ----------
-        const uint64_t wo_round = wo;
-#pragma unroll
-        for (uint32_t j = 0; j < C::kSteps; ++j) {
-            const uint32_t r = lane / C::kLanesPerRow + C::kRowsPerStep * j;
-            const uint32_t i = lane % C::kLanesPerRow;
-            const uint32_t rnw = __shfl(nw, r, kWave);
-            const uint64_t rwo = __shfl(wo_round, r, kWave);
-            const uint64_t rcap = __shfl(capw, r, kWave);
-            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
-            const uint32_t w0 = 2 * i;
-            if (w0 < rnw) {
-                const uint8_t* rp = oring + r * C::kRow + 16 * i;
-                const uint64_t g = rwo + w0;
-                uint8_t* gp = rdst + 8 * g;
-                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
-                if (g < rcap) {
-                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
-                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rp);
-                    } else {
-                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rp);
-                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rp + 8);
-                    }
-                }
-            }
-        }
-        wo += nw;
-        for (uint32_t q = 0; q < 2 && may_issue(); ++q) dma_pass();
-        wave_lds_sync();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
-    if (!valid) return;
-    if (st != ST_OK) {
-        out_len[unit] = 0;
-        status[unit] = st;
         return;
     }
-    out_len[unit] = 8 * wo;
-    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
-}
+    uint64_t* const dst = reinterpret_cast<uint64_t*>(dstb);
 
-// Two-phase round: (1) WALK — the only serial part: per output word, follow the
-// record chain using tag/count bytes only (ds_read_u8), and record the word's
-// kind and source position in static registers; (2) EXPAND — ROUND independent
-// words (unrolled), each reading its 16-byte window and expanding it, written to
-// static ring offsets. The walk is ~15 instructions per record; the expansion's
-// LDS latency is hidden by ILP across the round's words.
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-__global__ __launch_bounds__(WAVES * 64) void decode_walk_kernel(const uint8_t* __restrict__ in,
-                                                                 const uint64_t* __restrict__ in_off,
-                                                                 const uint64_t* __restrict__ in_len,
-                                                                 uint32_t n, uint8_t* __restrict__ out,
-                                                                 const uint64_t* __restrict__ out_off,
-                                                                 const uint64_t* __restrict__ out_cap,
-                                                                 uint64_t* __restrict__ out_len,
-                                                                 int32_t* __restrict__ status) {
-    using C = DmaCfg<CHUNK, SLOTS, ROUND, WAVES>;
-    __shared__ __attribute__((aligned(16))) uint8_t in_all[WAVES * C::kInRing];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[WAVES * C::kOutRing];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* iring = in_all + wave * C::kInRing;
-    uint8_t* oring = ring_all + wave * C::kOutRing;
-    const uint32_t unit = (blockIdx.x * WAVES + wave) * kWave + lane;
-    const bool valid = unit < n;
-
-    const uint8_t* src = in;
-    uint64_t P = 0, capw = 0;
-    uint8_t* dstb = out;
+    WV_STAMP(0);
+    uint64_t X = 0;   // packed position of the current window (always a tag)
+    uint64_t Wb = 0;  // output words before the current window
     int32_t st = ST_OK;
-    if (valid) {
-        src = in + in_off[unit];
-        P = in_len[unit];
-        dstb = out + out_off[unit];
-        capw = out_cap[unit] >> 3;
-        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
-        if (P > 0x3FFF0000ULL) st = ST_ARG;  // 30-bit stream offsets
-    }
-    bool live = valid && st == ST_OK;
-    if (!live) P = 0;
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    const uint8_t* base = src - s;
-    const uint32_t end = s + (uint32_t)P;
-    const uint32_t npieces = live ? (end + 15) >> 4 : 0;
-    const uint32_t padded = npieces * 16;
-    const uint32_t nchunks = (padded + CHUNK - 1) / CHUNK;
-    uint32_t maxchunks = nchunks;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxchunks = max(maxchunks, (uint32_t)__shfl_xor((int)maxchunks, d, kWave));
-    maxchunks = __builtin_amdgcn_readfirstlane(maxchunks);
+    bool fits = true;
+    while (X < P) {
+        const uint64_t rem64 = P - X;
+        const uint32_t rem = rem64 > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)rem64;
+        const uint32_t Pw = min(rem, kWvWin);
+        const uint32_t nload = min(rem, Pw + 16);  // records starting in the window end <= 9 B past it
+        const uint8_t* g = src + X;
+        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15);
 
-    uint64_t dsrc[C::kPieces];
-    uint32_t dnp[C::kPieces], dpc[C::kPieces];
-#pragma unroll
-    for (uint32_t g = 0; g < C::kPieces; ++g) {
-        const uint32_t r = C::kTasks * g + lane / C::kPieces;
-        const uint32_t sp = (lane % C::kPieces) ^ C::swz(r);
-        dsrc[g] = __shfl(reinterpret_cast<uint64_t>(base), r, kWave) + 16ULL * sp;
-        dnp[g] = __shfl(npieces, r, kWave);
-        dpc[g] = sp;
-    }
-    uint32_t issued = 0;
-    auto dma_pass = [&]() {
-        const uint32_t k = issued;
-        uint8_t* slot = iring + (k & (SLOTS - 1)) * C::kSlotBytes;
-#pragma unroll
-        for (uint32_t g = 0; g < C::kPieces; ++g) {
-            if (C::kPieces * k + dpc[g] < dnp[g]) {
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[g] + (uint64_t)CHUNK * k),
-                                                 (__attribute__((address_space(3))) void*)(slot + g * C::kTasks * CHUNK),
-                                                 16, 0, 0);
-            }
-        }
-        issued = k + 1;
-    };
-
-    uint32_t pos = s, lit = 0, pend_zero = 0, pend_lit = 0;
-    uint64_t wo = 0;
-    const uint32_t laneb = lane * CHUNK;
-    const uint32_t swz16 = C::swz(lane) << 4;
-    auto ring_addr = [&](uint32_t y) -> uint32_t {  // LDS offset of logical byte y
-        return ((y / CHUNK) & (SLOTS - 1)) * C::kSlotBytes + laneb + ((y & (CHUNK - 1)) ^ swz16);
-    };
-    auto u8_at = [&](uint32_t y) -> uint32_t { return iring[ring_addr(y)]; };
-    auto u64_at = [&](uint32_t y) -> uint64_t {  // y 8-aligned
-        return *reinterpret_cast<const uint64_t*>(iring + ring_addr(y));
-    };
-    auto may_issue = [&]() -> bool {
-        const uint32_t mr = (pend_lit ? lit : pos) / CHUNK;
-        return issued < maxchunks && __all(!live || issued < mr + SLOTS);
-    };
-
-    for (uint32_t q = 0; q < SLOTS && may_issue(); ++q) dma_pass();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t landed = issued;
-
-    uint8_t* myrow = oring + lane * C::kRow;
-    while (__any(live)) {
-        const uint32_t limit = (landed * CHUNK >= padded) ? 0xFFFFFFFFu : landed * CHUNK;
-        // ---- WALK: kinds/positions of this round's words -------------------------------
-        uint32_t srcpos[ROUND];
-        uint32_t mixmask = 0, litmask = 0;  // bit k: word k is a mixed record / a literal word
-        uint32_t nw = 0;
-        bool frozen = false;
-#pragma unroll
-        for (uint32_t k = 0; k < ROUND; ++k) {
-            const bool ok = live && !frozen;
-            const bool isZ = pend_zero != 0;
-            const bool isL = !isZ && pend_lit != 0;
-            const bool isR = !isZ && !isL && pos < end;
-            const uint32_t t = u8_at(pos);          // tag (meaningful when isR)
-            const uint32_t c1 = u8_at(pos + 1);     // zero-run count
-            const uint32_t c9 = u8_at(pos + 9);     // literal-run count
-            const bool avail = isL ? ((lit & ~7u) + 16 <= limit) : (!isR || (pos & ~7u) + 24 <= limit);
-            const bool go = ok && avail && (isZ || isL || isR);
-            const bool tz = t == 0, tf = t == 0xFF;
-            const uint32_t hdr = tz ? 2u : (tf ? 10u : 1u + __popc(t));
-            const uint32_t rlen = tf ? 10u + 8u * c9 : hdr;
-            const bool eof = isR && (pos + hdr > end || pos + rlen > end);  // message.zig:152-191
-            const bool emit = go && !eof;
-            if (ok && !avail) frozen = true;
-            if (go && eof) { st = ST_EOF; live = false; }
-            if (ok && !isZ && !isL && !isR) live = false;  // unit finished
-            srcpos[k] = isL ? lit : (pos + (tf ? 1u : 0u));
-            if (emit && isR && !tz && !tf) mixmask |= 1u << k;
-            if (emit && (isL || (isR && tf))) litmask |= 1u << k;
-            nw += emit ? 1u : 0u;
-            const bool stepR = emit && isR;
-            pend_zero = (emit && isZ) ? pend_zero - 1 : ((stepR && tz) ? c1 : pend_zero);
-            const bool stepL = emit && isL;
-            pend_lit = stepL ? pend_lit - 1 : ((stepR && tf) ? c9 : pend_lit);
-            lit = stepL ? lit + 8 : ((stepR && tf) ? pos + 10 : lit);
-            pos = stepR ? pos + rlen : pos;
-        }
-        // ---- EXPAND: independent words --------------------------------------------------
-#pragma unroll
-        for (uint32_t k = 0; k < ROUND; ++k) {
-            uint64_t word = 0;
-            if ((mixmask | litmask) & (1u << k)) {
-                const uint32_t p = srcpos[k];
-                const uint32_t y = p & ~7u;
-                const uint64_t a = u64_at(y), b = u64_at(y + 8);
-                const uint32_t o = p & 7;
-                if (mixmask & (1u << k)) {
-                    const uint32_t t = (uint32_t)(a >> (8 * o)) & 0xFFu;
-                    const uint64_t pay = (o == 7) ? b : ((a >> (8 * o + 8)) | (b << (56 - 8 * o)));
-                    word = expand_word(pay, t);
-                } else {
-                    word = o ? ((a >> (8 * o)) | (b << (64 - 8 * o))) : a;
-                }
-            }
-            *reinterpret_cast<uint64_t*>(myrow + 8 * k) = word;
-        }
+        // ---- stage the window (pk[sh + r] = byte r) and clear the marks ------------
         wave_lds_sync();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        landed = issued;
-        const uint64_t wo_round = wo;
-#pragma unroll
-        for (uint32_t j = 0; j < C::kSteps; ++j) {
-            const uint32_t r = lane / C::kLanesPerRow + C::kRowsPerStep * j;
-            const uint32_t i = lane % C::kLanesPerRow;
-            const uint32_t rnw = __shfl(nw, r, kWave);
-            const uint64_t rwo = __shfl(wo_round, r, kWave);
-            const uint64_t rcap = __shfl(capw, r, kWave);
-            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
-            const uint32_t w0 = 2 * i;
-            if (w0 < rnw) {
-                const uint8_t* rp = oring + r * C::kRow + 16 * i;
-                const uint64_t g = rwo + w0;
-                uint8_t* gp = rdst + 8 * g;
-                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
-                if (g < rcap) {
-                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
-                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rp);
-                    } else {
-                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rp);
-                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rp + 8);
+        stage_linear<kWvStageK>(pk, g - sh, (sh + nload + 15) >> 4, lane);
+        for (uint32_t i = lane * 16; i < Pw; i += 16 * kWave) *reinterpret_cast<uint4*>(mk + i) = make_uint4(0, 0, 0, 0);
+        wave_lds_sync();
+        WV_STAMP(1);
+
+        const uint32_t C = max(kWvCmin, (Pw + 63) >> 6);
+        const uint32_t cs = min(lane * C, Pw);
+        const uint32_t ce = min(cs + C, Pw);
+
+        // ---- walk A: guess "the chain enters at the chunk start" --------------------
+        uint32_t hit;
+        const uint32_t e1 = wv_walk(pk, mk, sh, rem, cs, ce, 1, hit);
+        uint32_t e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0, e7 = 0;
+        WV_STAMP(2);
+
+        // ---- walk B: enter where the left neighbour's walk A left off ---------------
+        // An entry far past the chunk start (a misread FF run, or a misread record
+        // running past the input end) would only pass through; keep walk A's guess.
+        uint32_t ent = __shfl_up(e1, 1, kWave);
+        if (lane == 0) ent = 0;
+        if (ent > cs + kWvSlack) ent = cs;
+        uint32_t ex = e1;
+        if (ent != cs) {
+            ex = wv_walk(pk, mk, sh, rem, ent, ce, 2, hit);
+            if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
+            e2 = ex;
+        }
+        WV_STAMP(3);
+
+        // ---- verification rounds ------------------------------------------------------
+        // Lanes before the first disagreeing lane f are verified. A disagreeing lane
+        // re-walks from its neighbour's exit when that neighbour is verified (lane f),
+        // or when the neighbour agrees with ITS neighbour this round and the exit is a
+        // plausible entry (<= kWvSlack into the chunk): far or EOF exits adopted from
+        // an unverified neighbour would otherwise ripple one lane per round.
+        uint32_t nid = 3;
+        for (;;) {
+            uint32_t prev = __shfl_up(ex, 1, kWave);
+            if (lane == 0) prev = 0;
+            const bool bad = ent != prev;
+            const uint64_t bm = __ballot(bad);
+            if (!bm) break;
+            WV_COUNT(8, 1);
+            const uint32_t f = (uint32_t)__builtin_ctzll(bm);
+            const bool left_bad = lane > 0 && ((bm >> (lane - 1)) & 1);
+            if (bad && (lane == f || (!left_bad && prev <= cs + kWvSlack))) {
+                ent = prev;
+                const uint32_t id = nid <= 7 ? nid : 0;
+                ex = wv_walk(pk, mk, sh, rem, ent, ce, id, hit);
+                if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
+                e3 = (id == 3) ? ex : e3;
+                e4 = (id == 4) ? ex : e4;
+                e5 = (id == 5) ? ex : e5;
+                e6 = (id == 6) ? ex : e6;
+                e7 = (id == 7) ? ex : e7;
+                ++nid;
+            }
+        }
+        WV_STAMP(4);
+        const uint32_t xw = readlane(ex, kWave - 1);  // window exit = next window start
+        if (xw == kEOFX) {
+            st = ST_EOF;
+            break;
+        }
+
+        // ---- count output words of the verified records ------------------------------
+        uint32_t words = 0;
+        for (uint32_t r = ent; r < ce;) {
+            uint32_t t = pk[sh + r];
+            uint32_t b1 = pk[sh + r + 1];
+            uint32_t c9 = pk[sh + r + 9];
+            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+            words += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+            r += wv_len(t, c9);
+        }
+        const uint32_t incl = wave_incl_sum(words, lane);
+        const uint32_t total = readlane(incl, kWave - 1);
+        if (Wb + total > capw) fits = false;
+        WV_STAMP(5);
+
+        // ---- expand, by output word ---------------------------------------------------
+        // Output words are produced in passes of kWvList words [W0, W0 + kWvList).
+        // fill:   each lane walks its verified records once more and writes, for
+        //         every output word of the pass that its records produce, a 16-bit
+        //         source code into a list in LDS (the mark array, dead by now):
+        //         code = q (window position of a tag; word = perm(bytes q+1..q+8,
+        //         lut[byte q])) or kLit | (s - 1) (literal word at bytes s..s+7);
+        //         zero-run words keep the kZero code the list is reset to.
+        // expand: lane i turns list entry i into its word and stores it, so every
+        //         store instruction writes 64 consecutive output words (512 B).
+        if (fits) {
+            uint16_t* const list = reinterpret_cast<uint16_t*>(mk);
+            uint64_t* const o = dst + Wb;
+            const uint32_t wbeg = incl - words, wend = incl;  // this lane's output words
+            for (uint32_t W0 = 0; W0 < total; W0 += kWvList) {
+                const uint32_t W1 = min(total, W0 + kWvList);
+                wave_lds_sync();
+                for (uint32_t i = lane * 8; i < kWvList; i += 8 * kWave)
+                    *reinterpret_cast<uint4*>(list + i) = make_uint4(kZero2, kZero2, kZero2, kZero2);
+                wave_lds_sync();
+                uint32_t pn = 0, ps = 0, pw = 0;  // long literal run handed to the wave
+                if (wbeg < W1 && wend > W0) {
+                    uint32_t w = wbeg;
+                    for (uint32_t r = ent; r < ce && w < W1;) {
+                        uint32_t t = pk[sh + r];
+                        uint32_t b1 = pk[sh + r + 1];
+                        uint32_t c9 = pk[sh + r + 9];
+                        asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                        const bool z = t == 0, f = t == 0xFFu;
+                        if (!z && w >= W0) list[w - W0] = (uint16_t)r;
+                        if (f && c9) {  // literal words r+10 .. r+10+8c
+                            if (c9 <= kWvExtLane || pn != 0) {  // one long run per lane goes to the wave
+                                for (uint32_t i = 0; i < c9; ++i) {
+                                    const uint32_t wi = w + 1 + i;
+                                    if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (r + 9 + 8 * i));
+                                }
+                            } else {
+                                pn = c9;
+                                ps = r + 9;
+                                pw = w + 1;
+                            }
+                        }
+                        w += 1u + (z ? b1 : 0u) + (f ? c9 : 0u);
+                        r += wv_len(t, c9);
                     }
                 }
-            }
-        }
-        wo += nw;
-        for (uint32_t q = 0; q < 2 && may_issue(); ++q) dma_pass();
-        wave_lds_sync();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!valid) return;
-    if (st != ST_OK) {
-        out_len[unit] = 0;
-        status[unit] = st;
-        return;
-    }
-    out_len[unit] = 8 * wo;
-    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
-}
-
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-static void launch_walk(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
-                        const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
-                        hipStream_t stream) {
-    constexpr uint32_t per = WAVES * kWave;
-    decode_walk_kernel<CHUNK, SLOTS, ROUND, WAVES><<<(n + per - 1) / per, per, 0, stream>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
-}
-
-// Register window fed from the LDS-DMA ring: the record step reads only
-// registers (a 32-byte view q0..q3); the window advances 16 B at a time from the
-// lane's ring with the next piece (nx0, nx1) read one advance ahead, so LDS
-// latency stays off the record chain and global latency stays behind the DMA ring.
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-__global__ __launch_bounds__(WAVES * 64) void decode_win_kernel(const uint8_t* __restrict__ in,
-                                                                const uint64_t* __restrict__ in_off,
-                                                                const uint64_t* __restrict__ in_len,
-                                                                uint32_t n, uint8_t* __restrict__ out,
-                                                                const uint64_t* __restrict__ out_off,
-                                                                const uint64_t* __restrict__ out_cap,
-                                                                uint64_t* __restrict__ out_len,
-                                                                int32_t* __restrict__ status) {
-    using C = DmaCfg<CHUNK, SLOTS, ROUND, WAVES>;
-    __shared__ __attribute__((aligned(16))) uint8_t in_all[WAVES * C::kInRing];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[WAVES * C::kOutRing];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* iring = in_all + wave * C::kInRing;
-    uint8_t* oring = ring_all + wave * C::kOutRing;
-    const uint32_t unit = (blockIdx.x * WAVES + wave) * kWave + lane;
-    const bool valid = unit < n;
-
-    const uint8_t* src = in;
-    uint64_t P = 0, capw = 0;
-    uint8_t* dstb = out;
-    int32_t st = ST_OK;
-    if (valid) {
-        src = in + in_off[unit];
-        P = in_len[unit];
-        dstb = out + out_off[unit];
-        capw = out_cap[unit] >> 3;
-        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
-        if (P > 0xFFFF0000ULL) st = ST_ARG;
-    }
-    bool live = valid && st == ST_OK;
-    if (!live) P = 0;
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    const uint8_t* base = src - s;
-    const uint32_t end = s + (uint32_t)P;
-    const uint32_t npieces = live ? (end + 15) >> 4 : 0;
-    const uint32_t padded = npieces * 16;
-    const uint32_t nchunks = (padded + CHUNK - 1) / CHUNK;
-    uint32_t maxchunks = nchunks;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxchunks = max(maxchunks, (uint32_t)__shfl_xor((int)maxchunks, d, kWave));
-    maxchunks = __builtin_amdgcn_readfirstlane(maxchunks);
-
-    uint64_t dsrc[C::kPieces];
-    uint32_t dnp[C::kPieces], dpc[C::kPieces];
-#pragma unroll
-    for (uint32_t g = 0; g < C::kPieces; ++g) {
-        const uint32_t r = C::kTasks * g + lane / C::kPieces;
-        const uint32_t sp = (lane % C::kPieces) ^ C::swz(r);
-        dsrc[g] = __shfl(reinterpret_cast<uint64_t>(base), r, kWave) + 16ULL * sp;
-        dnp[g] = __shfl(npieces, r, kWave);
-        dpc[g] = sp;
-    }
-    uint32_t issued = 0;
-    auto dma_pass = [&]() {
-        const uint32_t k = issued;
-        uint8_t* slot = iring + (k & (SLOTS - 1)) * C::kSlotBytes;
-#pragma unroll
-        for (uint32_t g = 0; g < C::kPieces; ++g) {
-            if (C::kPieces * k + dpc[g] < dnp[g]) {
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[g] + (uint64_t)CHUNK * k),
-                                                 (__attribute__((address_space(3))) void*)(slot + g * C::kTasks * CHUNK),
-                                                 16, 0, 0);
-            }
-        }
-        issued = k + 1;
-    };
-    const uint32_t laneb = lane * CHUNK;
-    const uint32_t swzp = C::swz(lane);
-    // 16-B piece q (logical piece index) of this lane, from the ring
-    auto piece_at = [&](uint32_t q, uint64_t& lo, uint64_t& hi) {
-        const uint32_t a = ((q / C::kPieces) & (SLOTS - 1)) * C::kSlotBytes + laneb + (((q % C::kPieces) ^ swzp) << 4);
-        const uint4 v = *reinterpret_cast<const uint4*>(iring + a);
-        lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
-    };
-
-    uint32_t pos = s, lit = 0, pend_zero = 0, pend_lit = 0;
-    uint64_t wo = 0;
-    uint32_t wb = 0;  // logical offset of q0 (piece wb/16); nx = piece wb/16 + 2
-    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nx0 = 0, nx1 = 0;
-    auto may_issue = [&]() -> bool {
-        const uint32_t mr = wb / CHUNK;  // the window's first piece is the oldest byte still needed
-        return issued < maxchunks && __all(!live || issued < mr + SLOTS);
-    };
-
-    for (uint32_t q = 0; q < SLOTS && may_issue(); ++q) dma_pass();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t landed = issued;
-    if (live) {
-        piece_at(0, q0, q1);
-        piece_at(1, q2, q3);
-        piece_at(2, nx0, nx1);
-    }
-
-    uint64_t* myrow = reinterpret_cast<uint64_t*>(oring + lane * C::kRow);
-    while (__any(live)) {
-        const uint32_t limit = (landed * CHUNK >= padded) ? 0xFFFFFFFFu : landed * CHUNK;
-        uint32_t nw = 0;
-        for (uint32_t k = 0; k < ROUND; ++k) {
-            if (!live) break;
-            const uint32_t rp = pend_lit ? lit : pos;
-            if (rp - wb >= 16) {  // advance the window by one piece (never more per word)
-                if (wb + 64 > limit) break;  // piece wb/16 + 3 not landed yet: resume next round
-                q0 = q2; q1 = q3; q2 = nx0; q3 = nx1;
-                wb += 16;
-                piece_at((wb >> 4) + 2, nx0, nx1);
-            }
-            const uint32_t o = rp - wb;  // < 16
-            uint64_t word = 0;
-            if (pend_zero) {
-                --pend_zero;
-            } else if (pend_lit) {
-                word = view_word8(q0, q1, q2, q3, o);
-                lit += 8;
-                --pend_lit;
-            } else if (pos < end) {
-                const uint32_t t = view_byte(q0, q1, q2, q3, o);
-                const uint64_t pay = view_word8(q0, q1, q2, q3, o + 1);
-                if (t == 0x00) {  // message.zig:101-110
-                    if (pos + 2 > end) { st = ST_EOF; live = false; break; }
-                    pend_zero = (uint32_t)pay & 0xFFu;
-                    pos += 2;
-                } else if (t == 0xFF) {  // message.zig:112-128
-                    const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
-                    if (pos + 10 > end || pos + 10 + 8 * c > end) { st = ST_EOF; live = false; break; }
-                    word = pay;
-                    pend_lit = c;
-                    lit = pos + 10;
-                    pos += 10 + 8 * c;
-                } else {  // message.zig:131-141
-                    const uint32_t kk = __popc(t);
-                    if (pos + 1 + kk > end) { st = ST_EOF; live = false; break; }
-                    word = expand_word(pay, t);
-                    pos += 1 + kk;
-                }
-            } else {
-                live = false;  // unit finished
-                break;
-            }
-            myrow[nw++] = word;
-        }
-        wave_lds_sync();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        landed = issued;
-        const uint64_t wo_round = wo;
-#pragma unroll
-        for (uint32_t j = 0; j < C::kSteps; ++j) {
-            const uint32_t r = lane / C::kLanesPerRow + C::kRowsPerStep * j;
-            const uint32_t i = lane % C::kLanesPerRow;
-            const uint32_t rnw = __shfl(nw, r, kWave);
-            const uint64_t rwo = __shfl(wo_round, r, kWave);
-            const uint64_t rcap = __shfl(capw, r, kWave);
-            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
-            const uint32_t w0 = 2 * i;
-            if (w0 < rnw) {
-                const uint8_t* rpp = oring + r * C::kRow + 16 * i;
-                const uint64_t g = rwo + w0;
-                uint8_t* gp = rdst + 8 * g;
-                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
-                if (g < rcap) {
-                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
-                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rpp);
-                    } else {
-                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rpp);
-                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rpp + 8);
+                uint64_t pm = __ballot(pn != 0);
+                while (pm) {  // long literal runs: the whole wave fills their entries
+                    const uint32_t l = (uint32_t)__builtin_ctzll(pm);
+                    pm &= pm - 1;
+                    const uint32_t nn = readlane(pn, l), ss = readlane(ps, l), ww = readlane(pw, l);
+                    for (uint32_t i = lane; i < nn; i += kWave) {
+                        const uint32_t wi = ww + i;
+                        if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (ss + 8 * i));
                     }
                 }
+                wave_lds_sync();
+                for (uint32_t i = W0 + lane; i < W1; i += kWave) {
+                    const uint32_t code = list[i - W0];
+                    const uint32_t q = code & kPosMask;
+                    const bool lit = (code & kLit) != 0;
+                    uint64_t word = 0;
+                    if (!(code & kZero)) {
+                        if (!lit || q + 9 <= nload) {  // a tag's bytes are always staged
+                            const uint32_t t = lit ? 0xFFu : pk[sh + q];
+                            word = perm64(lds_u64_at(pk, sh + q + 1), lut[t]);
+                        } else {  // literal word past the staged bytes (long FF run), inside the input
+                            word = gload_u64_unaligned(g + q + 1);
+                        }
+                    }
+                    o[i] = word;
+                }
             }
         }
-        wo += nw;
-        for (uint32_t q = 0; q < 2 && may_issue(); ++q) dma_pass();
-        wave_lds_sync();
+        WV_STAMP(6);
+        WV_COUNT(10, 1);
+        Wb += total;
+        X += xw;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!valid) return;
-    if (st != ST_OK) {
-        out_len[unit] = 0;
-        status[unit] = st;
-        return;
+    if (lane == 0) {
+        out_len[unit] = (st == ST_OK) ? 8 * Wb : 0;
+        status[unit] = (st != ST_OK) ? st : (fits ? ST_OK : ST_SPACE);
     }
-    out_len[unit] = 8 * wo;
-    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
-}
-
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-static void launch_win(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
-                       const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
-                       hipStream_t stream) {
-    constexpr uint32_t per = WAVES * kWave;
-    decode_win_kernel<CHUNK, SLOTS, ROUND, WAVES><<<(n + per - 1) / per, per, 0, stream>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
-}
-
-template <uint32_t CHUNK, uint32_t SLOTS, uint32_t ROUND, uint32_t WAVES>
-static void launch_dma(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
-                       const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
-                       hipStream_t stream) {
-    constexpr uint32_t per = WAVES * kWave;
-    decode_dma_kernel<CHUNK, SLOTS, ROUND, WAVES><<<(n + per - 1) / per, per, 0, stream>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
 }
 
 // ---------------------------------------------------------------------------
@@ -1828,80 +1304,33 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     return hipGetLastError();
 }
 
+// Decoder selection: CPK_DECODE_VARIANT=0 selects the wave-per-unit
+// decoder; anything else (default) the lane-per-unit stream decoder. Read per
+// launch so tests can exercise both in one process.
 static int decode_variant() {
-    static int v = [] {
-        const char* e = getenv("CPK_DECODE_VARIANT");  // experiment switch; default 2
-        return e ? atoi(e) : 2;
-    }();
-    return v;
+    const char* e = getenv("CPK_DECODE_VARIANT");
+    return e ? atoi(e) : 2;
 }
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (write) {
-        switch (decode_variant()) {
-            case 1: launch_dma<64, 4, 16, 2>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 3: launch_dma<32, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 4: launch_dma<32, 4, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 5: launch_dma<64, 2, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 6: launch_dma<32, 2, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 7: launch_dma<64, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 12: launch_win<64, 4, 16, 2>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 13: launch_win<32, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 14: launch_win<32, 4, 8, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 15: launch_win<64, 2, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 16: launch_win<64, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 8: launch_walk<64, 4, 16, 2>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 9: launch_walk<64, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 10: launch_walk<32, 4, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            case 11: launch_walk<64, 2, 16, 1>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-                    return hipGetLastError();
-            default: break;
-        }
-    }
-    if (write && (decode_variant() == 2 || (decode_variant() >= 20 && decode_variant() <= 23))) {
-        const uint32_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
-        switch (decode_variant()) {
-            case 20: decode_stream_kernel<256><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
-            case 21: decode_stream_kernel<512><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
-            case 22: decode_stream_kernel<1024><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
-            case 23: decode_stream_kernel<128><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
-            default: decode_stream_kernel<0><<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status); break;
-        }
-        return hipGetLastError();
-    }
-    if (decode_variant() >= 1) {
+    if (!write) {  // size pass: lane walk without stores
         const uint32_t blocks = (n + kBlock - 1) / kBlock;
-        if (write)
-            decode_lane_kernel<true><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                     out_len, status);
-        else
-            decode_lane_kernel<false><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                      out_len, status);
+        decode_lane_kernel<false><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                  out_len, status);
         return hipGetLastError();
     }
-    if (write)
-        decode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                   out_len, status);
-    else
-        decode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                    out_len, status);
+    if (decode_variant() != 0) {
+        const uint32_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
+        decode_stream_kernel<<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                     out_len, status);
+        return hipGetLastError();
+    }
+    const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
+    decode_wave_kernel<<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
+                                                        status);
     return hipGetLastError();
 }
 

@@ -139,14 +139,22 @@ PAIRS = [("binary", "packed"), ("segmented", "segmented-packed"),
          ("fixture_single.bin", "fixture_single_packed.bin"), ("fixture_far.bin", "fixture_far_packed.bin")]
 
 
+@pytest.fixture(params=["2", "0"], ids=["stream", "wave"])
+def decoder(request, monkeypatch):
+    """Run a decode test against both decoders (capnp_packed reads
+    CPK_DECODE_VARIANT per launch: 2 = lane stream (default), 0 = wave per unit)."""
+    monkeypatch.setenv("CPK_DECODE_VARIANT", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("unpacked,packed", PAIRS)
-def test_single_fixture_pairs(unpacked, packed):
+def test_single_fixture_pairs(unpacked, packed, decoder):
     assert cp.unpack_packed(fx(packed)) == fx(unpacked)
     assert cp.estimate_unpacked_size(fx(packed)) == len(fx(unpacked))
     assert cp.pack_packed(fx(unpacked)) == oracle.pack(fx(unpacked))[1]
 
 
-def test_single_kats():
+def test_single_kats(decoder):
     p = bytes([0x00, 0x01, 0xFF, 1, 2, 3, 4, 5, 6, 7, 8, 0x00])
     assert cp.estimate_unpacked_size(p) == 24
     assert cp.unpack_packed(p) == bytes(16) + bytes(range(1, 9))
@@ -160,7 +168,7 @@ def test_single_kats():
     assert cp.unpack_packed(b"") == b""
 
 
-def test_single_golden_vectors():
+def test_single_golden_vectors(decoder):
     import json
     gold = json.load(open(os.path.join(HERE, "golden", "zig_vectors.json")))
     for v in gold["vectors"]:
@@ -169,7 +177,7 @@ def test_single_golden_vectors():
         assert cp.unpack_packed(bytes.fromhex(v["packed_hex"])) == data, v["name"]
 
 
-def test_message_init_packed_roundtrip():
+def test_message_init_packed_roundtrip(decoder):
     b = cp.MessageBuilder()
     b.create_segment(bytes(range(1, 25)))
     b.create_segment(bytes(64))
@@ -244,7 +252,7 @@ def test_batch_encode_dense_unaligned_output():
     assert host[:3] == b"\xee" * 3 and host[3 + len(expect):3 + len(expect) + 8] == b"\xee" * 8
 
 
-def test_batch_decode_adversarial_and_fuzz():
+def test_batch_decode_adversarial_and_fuzz(decoder):
     units = [bytes.fromhex(h) for h in (
         "", "01", "00", "0000", "00ff", "ff", "ff01020304", "ff0102030405060708",
         "ff010203040506070800", "ff010203040506070801", "ff010203040506070801aabb",
@@ -255,20 +263,20 @@ def test_batch_decode_adversarial_and_fuzz():
     check_decode_parity(units)
 
 
-def test_batch_decode_roundtrips_random():
+def test_batch_decode_roundtrips_random(decoder):
     rng = random.Random(21)
     raw = rand_units(rng, 400, 512)
     packed = [oracle.pack(u)[1] for u in raw]
     check_decode_parity(packed)
 
 
-def test_batch_decode_unaligned_packed_bases():
+def test_batch_decode_unaligned_packed_bases(decoder):
     rng = random.Random(22)
     packed = [oracle.pack(u)[1] for u in rand_units(rng, 200, 300)]
     check_decode_parity(packed, pad_front=5)
 
 
-def test_batch_decode_windows_and_slow_path():
+def test_batch_decode_windows_and_slow_path(decoder):
     full = bytes(range(1, 9))
     units = [b"\x00\xff" * 3,                              # 6144 zero bytes, 3 windows
              oracle.pack(full * 700)[1],                   # literal runs across windows, P > fast limit
@@ -279,7 +287,7 @@ def test_batch_decode_windows_and_slow_path():
     check_decode_parity(units)
 
 
-def test_batch_decode_out_of_space_and_misaligned_output():
+def test_batch_decode_out_of_space_and_misaligned_output(decoder):
     units = [b"\x00\x03", b"\x00\x00"]
     got = gpu_decode(units, caps=[16, 8])
     assert got[0] == (cp.OUT_OF_SPACE, 32)
@@ -293,7 +301,7 @@ def test_batch_decode_out_of_space_and_misaligned_output():
     assert int(st.item()) == cp.INVALID_ARGUMENT
 
 
-def test_size_batches_match_oracle():
+def test_size_batches_match_oracle(decoder):
     rng = random.Random(31)
     raw = rand_units(rng, 300, 600)
     d_in, in_off, in_len = device_units(raw, align=8)
@@ -368,7 +376,7 @@ def check_sample_vs_oracle(d_in, d_pk, plen, slot, unit_bytes, n_sample):
         assert rows_pk[k][:len(p)].tobytes() == p, i
 
 
-def test_config2_64k_x_1KiB_p50_bit_exact():
+def test_config2_64k_x_1KiB_p50_bit_exact(decoder):
     """BASELINE configs[1]: 64K x 1 KiB, p = 0.5, pack+unpack bit-exact vs the oracle (every unit)."""
     n, ub = 65536, 1024
     d_in, d_pk, plen, slot = roundtrip_uniform(n, ub, 0xC0DE0002, 128)
@@ -386,13 +394,13 @@ def test_config2_64k_x_1KiB_p50_bit_exact():
 
 
 @pytest.mark.parametrize("thr", [26, 128, 230])  # p = 0.1 / 0.5 / 0.9 (x/256)
-def test_config3_4KiB_units_density_sweep(thr):
+def test_config3_4KiB_units_density_sweep(thr, decoder):
     """BASELINE configs[2] shape at 16K units; every 8th unit byte-compared with the oracle."""
     d_in, d_pk, plen, slot = roundtrip_uniform(16384, 4096, 0xC0DE0003, thr)
     check_sample_vs_oracle(d_in, d_pk, plen, slot, 4096, 2048)
 
 
-def test_config3_full_size_roundtrip_property():
+def test_config3_full_size_roundtrip_property(decoder):
     """1M x 4 KiB, p = 0.5 (headline size): decode(encode(x)) == x on device,
     and 1024 strided units byte-compared with the oracle."""
     d_in, d_pk, plen, slot = roundtrip_uniform(1 << 20, 4096, 0xC0DE0003, 128)
