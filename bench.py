@@ -231,7 +231,8 @@ def host_path(args, dev, n_units=1 << 16):
 
 
 def load_traffic(config_key):
-    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    """PMC HBM bytes per launch for this config (scripts/pmc_traffic.py output)."""
+    path = os.environ.get("CPK_TRAFFIC_JSON") or os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -280,12 +281,12 @@ def main():
         value = U_total / (elapsed / steps) / 2 ** 30
         P = packed_local
         alg_bytes = n * ub + P + META_BYTES_PER_UNIT * n  # per launch on one GPU, same for enc and dec
-        dom, dom_ms = ("decode_kernel", dec_ms) if dec_ms >= enc_ms else ("encode_kernel", enc_ms)
+        role, dom_ms = ("decode", dec_ms) if dec_ms >= enc_ms else ("encode", enc_ms)
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
         cfg_key = f"{n}x{ub}_t{args.zero_thresh}"
-        prof = load_traffic(cfg_key) or {}
-        dom_prof = next((v for k, v in prof.items() if dom.split("_")[0] in k), None)
-        traffic = dom_prof["total_bytes"] if dom_prof else None
+        prof = (load_traffic(cfg_key) or {}).get(role) or {}
+        traffic = prof.get("total_bytes")
+        dom = ", ".join(prof.get("kernels", [])) or role
         line = {
             "metric": "GiB/s device-resident packed encode+decode, 1M x 4KiB segments",
             "value": round(value, 3),

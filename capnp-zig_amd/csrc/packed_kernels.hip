@@ -183,44 +183,6 @@ __device__ __forceinline__ uint64_t expand_word(uint64_t d, uint32_t t) {
     return perm64(d, (uint64_t)sel_lo | ((uint64_t)sel_hi << 32));
 }
 
-// Per-lane byte stream into a zero-initialised LDS buffer. Every flushed u64 is
-// OR-ed (ds_or_b64) so the partial words a lane shares with its neighbours merge.
-struct LdsByteStream {
-    uint8_t* lds;
-    uint32_t addr;  // 8-aligned byte address of acc
-    uint32_t fill;  // bytes already in acc (0..7)
-    uint64_t acc;
-
-    __device__ __forceinline__ void init(uint8_t* base, uint32_t start) {
-        lds = base;
-        addr = start & ~7u;
-        fill = start & 7u;
-        acc = 0;
-    }
-    __device__ __forceinline__ void flush(uint64_t v) {
-        atomicOr(reinterpret_cast<unsigned long long*>(lds + addr), (unsigned long long)v);
-    }
-    // append k (<= 8) bytes held in the low bytes of v (bytes >= k must be zero)
-    __device__ __forceinline__ void put(uint64_t v, uint32_t k) {
-        if (k == 0) return;
-        uint32_t sh = fill * 8u;
-        uint64_t a = fill ? (acc | (v << sh)) : v;
-        uint32_t nf = fill + k;
-        if (nf >= 8) {
-            flush(a);
-            addr += 8;
-            acc = fill ? (v >> (64u - sh)) : 0;
-            fill = nf - 8;
-        } else {
-            acc = a;
-            fill = nf;
-        }
-    }
-    __device__ __forceinline__ void finish() {
-        if (fill) flush(acc);
-    }
-};
-
 // ---------------------------------------------------------------------------
 // Serial per-wave fallback (lane 0), any unit size. Restates message.zig
 // directly over global memory. Used for units beyond the fast-path limits.
@@ -452,15 +414,23 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     }
     fbz = min(fbz, words);
     fbf = min(fbf, words);
-    // run start carried into this lane = last break before it (+1); run end = first break after it
-    uint32_t cz = __shfl_up(wave_incl_max(lbz, lane), 1, kWave);
-    uint32_t cf = __shfl_up(wave_incl_max(lbf, lane), 1, kWave);
-    uint32_t ez = __shfl_down(wave_incl_suffix_min(fbz, lane), 1, kWave);
-    uint32_t ef = __shfl_down(wave_incl_suffix_min(fbf, lane), 1, kWave);
-    if (lane == 0) { cz = 0; cf = 0; }
-    if (lane == 63) { ez = words; ef = words; }
-    ez = min(ez, words);
-    ef = min(ef, words);
+    // run start carried into this lane = last break before it (+1); run end = first break after it.
+    // When no zero run and no literal run crosses a lane boundary (the common case
+    // away from very sparse or very dense data) the carries are the lane's own
+    // bounds and the four wave scans are skipped.
+    const uint64_t bz0 = __ballot(zmask & 1u), bz7 = __ballot((zmask >> 7) & 1u);
+    const uint64_t bf0 = __ballot(fmask & 1u), bf7 = __ballot((fmask >> 7) & 1u);
+    uint32_t cz = base, cf = base, ez = min(base + 8, words), ef = ez;
+    if ((bz0 & (bz7 << 1)) | (bf0 & (bf7 << 1))) {
+        cz = __shfl_up(wave_incl_max(lbz, lane), 1, kWave);
+        cf = __shfl_up(wave_incl_max(lbf, lane), 1, kWave);
+        ez = __shfl_down(wave_incl_suffix_min(fbz, lane), 1, kWave);
+        ef = __shfl_down(wave_incl_suffix_min(fbf, lane), 1, kWave);
+        if (lane == 0) { cz = 0; cf = 0; }
+        if (lane == 63) { ez = words; ef = words; }
+        ez = min(ez, words);
+        ef = min(ef, words);
+    }
 
     uint32_t rs[8];  // run start of word t's class run (Z or F)
 #pragma unroll
@@ -517,26 +487,31 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     }
     wave_lds_sync();
     {
-        LdsByteStream bs;
-        bs.init(lds, so + o);
+        // Each record (<= 10 bytes) is OR-ed into the zeroed buffer as two (FF heads:
+        // three) aligned u64 pieces: no per-byte shifting state, no branches.
+        uint32_t x = so + o;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            if (sz[t] == 0) continue;
+            uint64_t lo, hi = 0;
             if ((zmask >> t) & 1u) {
-                bs.put((uint64_t)cnt[t] << 8, 2);                       // 00 <count>
+                lo = (uint64_t)cnt[t] << 8;                                  // 00 <count>
             } else if ((fmask >> t) & 1u) {
-                if (sz[t] == 10) {                                       // FF w0..w7 <count>
-                    bs.put(0xFFULL | (w[t] << 8), 8);
-                    bs.put((w[t] >> 56) | ((uint64_t)cnt[t] << 8), 2);
-                } else {
-                    bs.put(w[t], 8);                                     // literal run body
-                }
-            } else {                                                     // tag + nonzero bytes
-                uint64_t comp = perm64(w[t], lut[tag[t]]);
-                bs.put((uint64_t)tag[t] | (comp << 8), sz[t]);
+                const bool head = sz[t] == 10;                               // FF w0..w7 <count>
+                lo = head ? (0xFFULL | (w[t] << 8)) : w[t];                  // or literal run body
+                hi = head ? ((w[t] >> 56) | ((uint64_t)cnt[t] << 8)) : 0;
+            } else {
+                lo = (uint64_t)tag[t] | (perm64(w[t], lut[tag[t]]) << 8);    // tag + nonzero bytes
             }
+            if (sz[t]) {
+                const uint32_t a = x & ~7u, sh = (x & 7u) * 8u;
+                atomicOr(reinterpret_cast<unsigned long long*>(lds + a), (unsigned long long)(lo << sh));
+                atomicOr(reinterpret_cast<unsigned long long*>(lds + a + 8),
+                         (unsigned long long)(((lo >> 1) >> (63u - sh)) | (hi << sh)));
+                if (sh == 56 && (hi >> 8))
+                    atomicOr(reinterpret_cast<unsigned long long*>(lds + a + 16), (unsigned long long)(hi >> 8));
+            }
+            x += sz[t];
         }
-        bs.finish();
     }
     wave_lds_sync();
 
@@ -704,12 +679,11 @@ __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __re
 // each round the wave stores the ring cooperatively: 8 lanes per 128-B line,
 // 8 lines per store instruction (fully coalesced), instead of 64 scattered
 // 8-byte stores per instruction.
-constexpr int kRoundWords = 16;                 // 128 B of output per lane per round
-constexpr int kRingRow = kRoundWords * 8 + 16;  // 144 B: 16-B aligned, staggers LDS banks
-constexpr int kStreamWaves = 2;                 // waves per block
-constexpr int kStreamBlock = kStreamWaves * kWave;
+// ROUND words of output per lane per round (ROUND = 16: one 128-B line); ring rows
+// are ROUND*8 + 16 B (16-B aligned, staggers LDS banks); WAVES waves per block.
 
-__global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8_t* __restrict__ in,
+template <int ROUND, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(const uint8_t* __restrict__ in,
                                                                      const uint64_t* __restrict__ in_off,
                                                                      const uint64_t* __restrict__ in_len,
                                                                      uint32_t n, uint8_t* __restrict__ out,
@@ -717,6 +691,12 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
                                                                      const uint64_t* __restrict__ out_cap,
                                                                      uint64_t* __restrict__ out_len,
                                                                      int32_t* __restrict__ status) {
+    constexpr int kRoundWords = ROUND;
+    constexpr int kRingRow = ROUND * 8 + 16;
+    constexpr int kStreamWaves = WAVES;
+    constexpr int kLanesPerRow = ROUND / 2;              // 16 B per lane in the cooperative store
+    constexpr int kRowsPerStep = kWave / kLanesPerRow;
+    constexpr int kSteps = kWave / kRowsPerStep;
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kStreamWaves * kWave * kRingRow];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -811,9 +791,9 @@ __global__ __launch_bounds__(kStreamBlock) void decode_stream_kernel(const uint8
         // ---- cooperative store: lane L moves 16 B of unit row (L>>3)+8j ---------------
         const uint64_t wo_round = wo;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t r = (lane >> 3) + 8 * j;  // ring row (= lane of the owning unit)
-            const uint32_t i = lane & 7;             // 16-B piece within the row
+        for (int j = 0; j < kSteps; ++j) {
+            const uint32_t r = lane / kLanesPerRow + kRowsPerStep * j;  // ring row (= lane of the owning unit)
+            const uint32_t i = lane % kLanesPerRow;                     // 16-B piece within the row
             const uint32_t rnw = __shfl(nw, r, kWave);
             const uint64_t rwo = __shfl(wo_round, r, kWave);
             const uint64_t rcap = __shfl(capw, r, kWave);
@@ -954,6 +934,149 @@ __device__ __forceinline__ uint64_t gload_u64_unaligned(const uint8_t* p) {
     return v;
 }
 
+// ---------------------------------------------------------------------------
+// DECODE, checkpoint pass (first half of the two-pass decoder, CPK_DECODE_VARIANT=5)
+// ---------------------------------------------------------------------------
+// Lane l of a wave walks the record chain of unit l (message.zig:152-191) and, for
+// every 64-byte block b of the packed unit, records a checkpoint
+//   ck[b] = (words produced by records whose tag lies before 64b) << 7 | off,
+// off = offset of the first tag in block b (64 = no tag starts in the block).
+// The walk is lockstep by input: in step k every lane consumes the records whose
+// tag lies in its block k, so the wave stages block k+3 of all 64 units with four
+// LDS-DMA instructions per step (16 units x 64 B each) into a 4-slot ring and
+// waits with a fixed vmcnt: the chain reads LDS only, never global memory.
+// Checkpoints are written to the first 4*nblk bytes of the unit's output slot
+// (decode_wave_kernel reads them before it writes a byte of output). The pass
+// also yields the decoded size, EOF and out-of-space statuses. Units it does not
+// take (packed start not 16-B aligned, more than kWvWin packed bytes) get
+// kStNeedFull and are decoded by the wave kernel's full path.
+constexpr int32_t kStNeedFull = 0x7FFF0001;    // internal: wave kernel resolves the chain itself
+constexpr uint32_t kCkWaves = 2;
+constexpr uint32_t kCkBlock = kCkWaves * kWave;
+constexpr uint32_t kCkSlot = kWave * 64;        // one 64-B block for every lane of the wave
+constexpr uint32_t kCkNone = 64;
+
+__global__ __launch_bounds__(kCkBlock) void decode_ckpt_kernel(const uint8_t* __restrict__ in,
+                                                               const uint64_t* __restrict__ in_off,
+                                                               const uint64_t* __restrict__ in_len, uint32_t n,
+                                                               uint8_t* __restrict__ out,
+                                                               const uint64_t* __restrict__ out_off,
+                                                               const uint64_t* __restrict__ out_cap,
+                                                               uint64_t* __restrict__ out_len,
+                                                               int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kCkWaves * 4 * kCkSlot];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const ring = ring_all + wave * 4 * kCkSlot;
+    const uint32_t unit = (blockIdx.x * kCkWaves + wave) * kWave + lane;
+    const bool valid = unit < n;
+
+    const uint8_t* src = in;
+    uint32_t P = 0;
+    uint8_t* dstb = out;
+    uint64_t cap = 0;
+    bool fast = false;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        const uint64_t P64 = in_len[unit];
+        dstb = out + out_off[unit];
+        cap = out_cap[unit];
+        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+        fast = st == ST_OK && !(reinterpret_cast<uintptr_t>(src) & 15) && P64 <= kWvWin &&
+               cap >= 4 * ((P64 + 63) / 64);
+        P = fast ? (uint32_t)P64 : 0u;
+        if (st == ST_OK && !fast) st = kStNeedFull;
+    }
+    const uint32_t nblk = (P + 63) >> 6;
+    uint32_t maxblk = nblk;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxblk = max(maxblk, (uint32_t)__shfl_xor((int)maxblk, d, kWave));
+    maxblk = __builtin_amdgcn_readfirstlane(maxblk);
+
+    // DMA descriptors: instruction q moves piece (lane & 3) of the block of unit 16q + lane/4
+    const uint8_t* dsrc[4];
+    uint32_t dlast[4];  // last valid 16-B piece of that unit
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t r = 16 * q + lane / 4;
+        const uint32_t rp = __shfl(P, r, kWave);
+        const uint64_t rs = __shfl(reinterpret_cast<uint64_t>(src), r, kWave);
+        // a unit with nothing to stage re-reads 16 B at the start of the in_len array
+        dsrc[q] = rp ? reinterpret_cast<const uint8_t*>(rs) : reinterpret_cast<const uint8_t*>(in_len);
+        dlast[q] = rp ? (rp - 1) >> 4 : 0u;
+    }
+    auto dma = [&](uint32_t k) {  // stage block k of every unit into slot k & 3
+        uint8_t* slot = ring + (k & 3) * kCkSlot;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t piece = min(4 * k + (lane & 3), dlast[q]);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[q] + 16ull * piece),
+                                             (__attribute__((address_space(3))) void*)(slot + q * 1024), 16, 0, 0);
+        }
+    };
+    auto rb = [&](uint32_t p) -> uint32_t {  // byte p of this lane's unit (its block must be staged)
+        return ring[((p >> 6) & 3) * kCkSlot + lane * 64 + (p & 63)];
+    };
+
+    uint32_t pos = 0;         // next tag
+    uint32_t words = 0;       // words of the records before pos (saturates the checkpoint field)
+    uint32_t total = 0;       // decoded words (<= 4608 / 2 * 256)
+    bool live = fast;
+    uint32_t ck[4];
+    if (maxblk) {
+        dma(0);
+        if (maxblk > 1) dma(1);
+        if (maxblk > 2) dma(2);
+    }
+    for (uint32_t k = 0; k < maxblk; ++k) {
+        // blocks k and k+1 must have landed. Each step ends with [checkpoint stores]
+        // [DMA of block k+3] (when there is one), so the 4 youngest vector-memory
+        // operations are block k+2's DMA; near the end there is none: drain.
+        if (k + 3 <= maxblk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_lds_sync();
+        const uint32_t bend = 64 * (k + 1);
+        ck[k & 3] = ((pos < bend) ? (pos & 63) : kCkNone) | (words << 7);
+        for (;;) {  // one record per lane per pass; branch-free body, uniform exit
+            const bool act = live && pos < bend && pos < P;
+            if (!__any(act)) break;
+            uint32_t t = rb(pos);  // any position maps into the ring: inactive lanes read harmlessly
+            uint32_t b1 = rb(pos + 1);
+            uint32_t c9 = rb(pos + 9);
+            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per record
+            const uint32_t len = wv_len(t, c9);
+            const bool eof = act && pos + len > P;  // message.zig:152-191: record runs past the input
+            const bool ok = act && !eof;
+            st = eof ? ST_EOF : st;
+            live = live && !eof;
+            const uint32_t wd = 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+            total += ok ? wd : 0u;
+            words = ok ? min(words + wd, 0x1FFFFFFu) : words;
+            pos = ok ? pos + len : pos;
+        }
+        if (k < nblk && ((k & 3) == 3 || k + 1 == nblk)) {  // flush up to four checkpoints (16 B)
+            if (fast && st == ST_OK) {
+                uint32_t* cp = reinterpret_cast<uint32_t*>(dstb) + (k & ~3u);
+                const uint32_t nv = min(4u, nblk - (k & ~3u));
+                if (nv == 4 && !(reinterpret_cast<uintptr_t>(cp) & 15)) {
+                    *reinterpret_cast<uint4*>(cp) = make_uint4(ck[0], ck[1], ck[2], ck[3]);
+                } else {
+                    for (uint32_t i = 0; i < nv; ++i) cp[i] = ck[i];
+                }
+            }
+        }
+        wave_lds_sync();
+        if (k + 3 < maxblk) dma(k + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
+    if (!valid) return;
+    if (st == ST_OK && words >= 0x1FFFFFFu) st = kStNeedFull;  // checkpoint word field overflow
+    if (st == ST_OK && 8ull * total > cap) st = ST_SPACE;
+    out_len[unit] = (st == ST_OK || st == ST_SPACE) ? 8ull * total : 0;
+    status[unit] = st;
+}
+
 #ifdef CPK_WV_PROF
 // Phase probe (tools/wv_probe.hip): per unit, cycle stamps after each phase and counters.
 __device__ uint64_t* cpk_wv_prof;
@@ -964,6 +1087,7 @@ __device__ uint64_t* cpk_wv_prof;
 #define WV_COUNT(k, v) do { } while (0)
 #endif
 
+template <bool CK>
 __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __restrict__ in,
                                                                const uint64_t* __restrict__ in_off,
                                                                const uint64_t* __restrict__ in_len, uint32_t n,
@@ -984,6 +1108,9 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     uint8_t* pk = pk_all + wave * kWvPk;
     uint8_t* mk = mk_all + wave * kWvWin;
 
+    // CK: decode_ckpt_kernel ran first; this kernel then takes only the units it
+    // marked kStNeedFull (every other status is final or decode_expand_kernel's).
+    if (CK && status[unit] != kStNeedFull) return;  // decode_expand_kernel takes ST_OK units
     const uint8_t* src = in + in_off[unit];
     const uint64_t P = in_len[unit];
     uint8_t* dstb = out + out_off[unit];
@@ -1017,9 +1144,12 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         wave_lds_sync();
         WV_STAMP(1);
 
+        uint32_t cs, ce, ent, wbeg, wend, total, xw;
+        {
+
         const uint32_t C = max(kWvCmin, (Pw + 63) >> 6);
-        const uint32_t cs = min(lane * C, Pw);
-        const uint32_t ce = min(cs + C, Pw);
+        cs = min(lane * C, Pw);
+        ce = min(cs + C, Pw);
 
         // ---- walk A: guess "the chain enters at the chunk start" --------------------
         uint32_t hit;
@@ -1030,7 +1160,7 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         // ---- walk B: enter where the left neighbour's walk A left off ---------------
         // An entry far past the chunk start (a misread FF run, or a misread record
         // running past the input end) would only pass through; keep walk A's guess.
-        uint32_t ent = __shfl_up(e1, 1, kWave);
+        ent = __shfl_up(e1, 1, kWave);
         if (lane == 0) ent = 0;
         if (ent > cs + kWvSlack) ent = cs;
         uint32_t ex = e1;
@@ -1071,7 +1201,7 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
             }
         }
         WV_STAMP(4);
-        const uint32_t xw = readlane(ex, kWave - 1);  // window exit = next window start
+        xw = readlane(ex, kWave - 1);  // window exit = next window start
         if (xw == kEOFX) {
             st = ST_EOF;
             break;
@@ -1088,8 +1218,11 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
             r += wv_len(t, c9);
         }
         const uint32_t incl = wave_incl_sum(words, lane);
-        const uint32_t total = readlane(incl, kWave - 1);
+        total = readlane(incl, kWave - 1);
         if (Wb + total > capw) fits = false;
+        wbeg = incl - words;
+        wend = incl;
+        }
         WV_STAMP(5);
 
         // ---- expand, by output word ---------------------------------------------------
@@ -1105,7 +1238,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         if (fits) {
             uint16_t* const list = reinterpret_cast<uint16_t*>(mk);
             uint64_t* const o = dst + Wb;
-            const uint32_t wbeg = incl - words, wend = incl;  // this lane's output words
             for (uint32_t W0 = 0; W0 < total; W0 += kWvList) {
                 const uint32_t W1 = min(total, W0 + kWvList);
                 wave_lds_sync();
@@ -1174,6 +1306,136 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     if (lane == 0) {
         out_len[unit] = (st == ST_OK) ? 8 * Wb : 0;
         status[unit] = (st != ST_OK) ? st : (fits ? ST_OK : ST_SPACE);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// DECODE, expansion pass (second half of the two-pass decoder, CPK_DECODE_VARIANT=5)
+// ---------------------------------------------------------------------------
+// One wave per unit that decode_ckpt_kernel left at ST_OK (16-B aligned, <= kWvWin
+// packed bytes). Lane j owns 64-B blocks [bpl*j, bpl*(j+1)); their checkpoints give
+// its first tag and output word directly, so there is no chain resolution: one
+// fill walk lists the source of each output word (as in decode_wave_kernel) and
+// the wave expands the list with 64 consecutive words per store instruction.
+// The checkpoint loads are issued with the staging loads and all are consumed
+// before the first output store (they live in the output slot).
+constexpr uint32_t kExWaves = 4;
+constexpr uint32_t kExBlock = kExWaves * kWave;
+constexpr uint32_t kExList = 512;  // output words per expand pass
+
+__global__ __launch_bounds__(kExBlock) void decode_expand_kernel(const uint8_t* __restrict__ in,
+                                                                 const uint64_t* __restrict__ in_off,
+                                                                 const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                 uint8_t* __restrict__ out,
+                                                                 const uint64_t* __restrict__ out_off,
+                                                                 const uint64_t* __restrict__ out_len,
+                                                                 const int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kExWaves * kWvPk];
+    __shared__ __attribute__((aligned(16))) uint16_t list_all[kExWaves * kExList];
+    __shared__ uint64_t lut[256];
+    lut[threadIdx.x] = expand_selector(threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t unit = blockIdx.x * kExWaves + wave;
+    if (unit >= n || status[unit] != ST_OK) return;  // wave-uniform
+    uint8_t* const pk = pk_all + wave * kWvPk;
+    uint16_t* const list = list_all + wave * kExList;
+
+    const uint8_t* const src = in + in_off[unit];  // 16-B aligned (decode_ckpt_kernel)
+    const uint32_t P = (uint32_t)in_len[unit];     // <= kWvWin
+    uint64_t* const dst = reinterpret_cast<uint64_t*>(out + out_off[unit]);
+    const uint32_t total = (uint32_t)(out_len[unit] >> 3);
+    if (P == 0) return;
+    const uint32_t nblk = (P + 63) >> 6;
+    const uint32_t bpl = (nblk + kWave - 1) / kWave;
+    const uint32_t b0 = min(bpl * lane, nblk), b1 = min(b0 + bpl, nblk);
+
+    // ---- checkpoint loads + staging loads in flight together -----------------------
+    const uint32_t* ckp = reinterpret_cast<const uint32_t*>(dst);
+    uint32_t c0 = ckp[min(b0, nblk - 1)];
+    uint32_t c1 = ckp[min(b0 + 1, nblk - 1)];
+    uint32_t cn = ckp[min(b1, nblk - 1)];
+    stage_linear<kWvStageK>(pk, src, (P + 15) >> 4, lane);
+    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(cn));  // all checkpoints read before any store
+    wave_lds_sync();
+
+    const uint32_t cs = 64 * b0, ce = min(64 * b1, P);
+    uint32_t ent = ce;  // no tag starts in this lane's blocks
+    uint32_t wbeg = (b1 < nblk) ? (cn >> 7) : total;
+    if (b0 < nblk && (c0 & 127) != kCkNone) {
+        ent = cs + (c0 & 127);
+        wbeg = c0 >> 7;
+    } else if (bpl > 1 && b0 + 1 < nblk && (c1 & 127) != kCkNone) {
+        ent = cs + 64 + (c1 & 127);
+        wbeg = c1 >> 7;
+    }
+    const uint32_t wend = (b1 < nblk) ? (cn >> 7) : total;
+
+    for (uint32_t W0 = 0; W0 < total; W0 += kExList) {
+        const uint32_t W1 = min(total, W0 + kExList);
+        wave_lds_sync();
+        for (uint32_t i = lane * 8; i < kExList; i += 8 * kWave)
+            *reinterpret_cast<uint4*>(list + i) = make_uint4(kZero2, kZero2, kZero2, kZero2);
+        wave_lds_sync();
+        // ---- fill: one record per lane per pass, uniform exit ------------------------
+        uint32_t r = ent, w = wbeg;
+        const bool mine = wbeg < W1 && wend > W0;
+        uint32_t pn = 0, ps = 0, pw = 0;  // one long literal run per lane goes to the wave
+        for (;;) {
+            const bool act = mine && r < ce && w < W1;
+            if (!__any(act)) break;
+            const uint32_t rr = act ? r : 0u;
+            uint32_t t = pk[rr];
+            uint32_t b1v = pk[rr + 1];
+            uint32_t c9 = pk[rr + 9];
+            asm volatile("" : "+v"(t), "+v"(b1v), "+v"(c9));
+            const bool z = t == 0, f = t == 0xFFu;
+            if (act) {
+                if (!z && w >= W0) list[w - W0] = (uint16_t)rr;
+                if (f && c9) {  // literal words rr+10 .. rr+10+8c
+                    if (c9 <= kWvExtLane || pn != 0) {
+                        for (uint32_t i = 0; i < c9; ++i) {
+                            const uint32_t wi = w + 1 + i;
+                            if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (rr + 9 + 8 * i));
+                        }
+                    } else {
+                        pn = c9;
+                        ps = rr + 9;
+                        pw = w + 1;
+                    }
+                }
+            }
+            w = act ? w + 1u + (z ? b1v : 0u) + (f ? c9 : 0u) : w;
+            r = act ? r + wv_len(t, c9) : r;
+        }
+        uint64_t pm = __ballot(pn != 0);
+        while (pm) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t nn = readlane(pn, l), ss = readlane(ps, l), ww = readlane(pw, l);
+            for (uint32_t i = lane; i < nn; i += kWave) {
+                const uint32_t wi = ww + i;
+                if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (ss + 8 * i));
+            }
+        }
+        wave_lds_sync();
+        // ---- expand: lane i -> output word W0 + i (+64k) ---------------------------------
+        for (uint32_t i = W0 + lane; i < W1; i += kWave) {
+            const uint32_t code = list[i - W0];
+            const uint32_t q = code & kPosMask;
+            const bool lit = (code & kLit) != 0;
+            uint64_t word = 0;
+            if (!(code & kZero)) {
+                if (!lit || q + 9 <= P) {
+                    const uint32_t t = lit ? 0xFFu : pk[q];
+                    word = perm64(lds_u64_at(pk, q + 1), lut[t]);
+                } else {
+                    word = gload_u64_unaligned(src + q + 1);
+                }
+            }
+            dst[i] = word;
+        }
     }
 }
 
@@ -1304,12 +1566,13 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     return hipGetLastError();
 }
 
-// Decoder selection: CPK_DECODE_VARIANT=0 selects the wave-per-unit
-// decoder; anything else (default) the lane-per-unit stream decoder. Read per
-// launch so tests can exercise both in one process.
+// Decoder selection, read per launch so tests can exercise every
+// decoder in one process: CPK_DECODE_VARIANT unset = lane-per-unit stream decoder
+// (one wave per block), 2 = the same with two waves per block, 3 = 8-word rounds,
+// 0 = wave per unit, 5 = checkpoint pass + expansion pass.
 static int decode_variant() {
     const char* e = getenv("CPK_DECODE_VARIANT");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 4;
 }
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
@@ -1322,15 +1585,39 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                   out_len, status);
         return hipGetLastError();
     }
-    if (decode_variant() != 0) {
-        const uint32_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
-        decode_stream_kernel<<<blocks, kStreamBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+    switch (decode_variant()) {
+        case 0: break;  // wave per unit, below
+        case 5: {       // checkpoint pass, expansion pass, full path for what the first pass declined
+            decode_ckpt_kernel<<<(n + kCkBlock - 1) / kCkBlock, kCkBlock, 0, stream>>>(
+                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+            decode_expand_kernel<<<(n + kExWaves - 1) / kExWaves, kExBlock, 0, stream>>>(
+                in, in_off, in_len, n, out, out_off, out_len, status);
+            decode_wave_kernel<true><<<(n + kWvWaves - 1) / kWvWaves, kWvBlock, 0, stream>>>(
+                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+            return hipGetLastError();
+        }
+        case 3: {
+            const uint32_t blocks = (n + 2 * kWave - 1) / (2 * kWave);
+            decode_stream_kernel<8, 2><<<blocks, 2 * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                        out_len, status);
+            return hipGetLastError();
+        }
+        case 2: {       // stream, two waves per block (round 1 default)
+            const uint32_t blocks = (n + 2 * kWave - 1) / (2 * kWave);
+            decode_stream_kernel<16, 2><<<blocks, 2 * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                         out_len, status);
+            return hipGetLastError();
+        }
+        default: {      // stream, one wave per block (default)
+            const uint32_t blocks = (n + kWave - 1) / kWave;
+            decode_stream_kernel<16, 1><<<blocks, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status);
-        return hipGetLastError();
+            return hipGetLastError();
+        }
     }
     const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
-    decode_wave_kernel<<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
-                                                        status);
+    decode_wave_kernel<false><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                               out_len, status);
     return hipGetLastError();
 }
 

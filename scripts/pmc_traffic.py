@@ -4,8 +4,11 @@
 FETCH_SIZE and WRITE_SIZE are in KB. On gfx950 FETCH_SIZE counts 128-B wide
 streaming reads as 64 B (MI355X_MICROARCH.md §HBM), so read bytes = 2 x FETCH_SIZE
 x 1024 for 16-B-per-lane streaming loads; writes are counted exactly.
-Usage: pmc_traffic.py gpurun_out/TAG CONFIG_KEY > profiles/pmc_traffic.json (merged)
+Usage: pmc_traffic.py gpurun_out/TAG CONFIG_KEY [existing.json] > pmc_traffic.json
+Output per config: per-kernel bytes, plus "encode" / "decode" role totals (a
+decoder may be several kernels) that bench.py reports as roofline.traffic.
 """
+import os
 import collections
 import csv
 import glob
@@ -26,16 +29,25 @@ def per_kernel(path, counter):
 def main():
     path, key = sys.argv[1], sys.argv[2]
     fetch, write = per_kernel(path, "FETCH_SIZE"), per_kernel(path, "WRITE_SIZE")
-    out = {}
+    kernels = {}
     for k in sorted(set(fetch) | set(write)):
         if "generate" in k:
             continue
         rd = 2 * fetch.get(k, 0.0) * 1024
         wr = write.get(k, 0.0) * 1024
-        out[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr,
-                  "raw_FETCH_SIZE_KB": fetch.get(k), "raw_WRITE_SIZE_KB": write.get(k)}
+        kernels[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr,
+                      "raw_FETCH_SIZE_KB": fetch.get(k), "raw_WRITE_SIZE_KB": write.get(k)}
+    out = {"kernels": kernels}
+    for role in ("encode", "decode"):
+        ks = [k for k in kernels if (("encode" in k) if role == "encode" else ("decode" in k and "size" not in k))]
+        if ks:
+            out[role] = {"kernels": ks,
+                         "read_bytes": sum(kernels[k]["read_bytes"] for k in ks),
+                         "write_bytes": sum(kernels[k]["write_bytes"] for k in ks),
+                         "total_bytes": sum(kernels[k]["total_bytes"] for k in ks)}
+    prev = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
     try:
-        cur = json.load(open("profiles/pmc_traffic.json"))
+        cur = json.load(open(prev)) if os.path.exists(prev) else {}
     except Exception:
         cur = {}
     cur[key] = out

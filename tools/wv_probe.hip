@@ -16,6 +16,8 @@ int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 262144;
     const uint32_t thr = argc > 2 ? atoi(argv[2]) : 128;
     const uint64_t ub = argc > 3 ? atoll(argv[3]) : 4096;
+    const int mode = argc > 4 ? atoi(argv[4]) : 0;  // 0 wave, 1 checkpoint pass + fast path, 2 stream
+    const bool ck = mode == 1;
     const uint64_t slot = 10 * (ub / 8);
     std::vector<uint64_t> h_uoff(n), h_ulen(n, ub), h_poff(n), h_pcap(n, slot);
     for (uint32_t i = 0; i < n; ++i) { h_uoff[i] = i * ub; h_poff[i] = i * slot; }
@@ -40,7 +42,15 @@ int main(int argc, char** argv) {
         CK(hipMemset(prof, 0, 16 * 8 * (size_t)n));
         CK(hipEventRecord(a, 0));
         const uint32_t blocks = (n + cpk::kWvWaves - 1) / cpk::kWvWaves;
-        cpk::decode_wave_kernel<<<blocks, cpk::kWvBlock, 0, 0>>>(d_p, poff, plen, n, d_o, uoff, ulen, olen, st);
+        if (mode == 2) {
+            cpk::decode_stream_kernel<16, 2><<<(n + 127) / 128, 128, 0, 0>>>(d_p, poff, plen, n, d_o, uoff, ulen, olen, st);
+        } else if (ck) {
+            cpk::decode_ckpt_kernel<<<(n + cpk::kCkBlock - 1) / cpk::kCkBlock, cpk::kCkBlock, 0, 0>>>(
+                d_p, poff, plen, n, d_o, uoff, ulen, olen, st);
+            cpk::decode_wave_kernel<true><<<blocks, cpk::kWvBlock, 0, 0>>>(d_p, poff, plen, n, d_o, uoff, ulen, olen, st);
+        } else {
+            cpk::decode_wave_kernel<false><<<blocks, cpk::kWvBlock, 0, 0>>>(d_p, poff, plen, n, d_o, uoff, ulen, olen, st);
+        }
         CK(hipGetLastError());
         CK(hipEventRecord(b, 0));
         CK(hipEventSynchronize(b));
@@ -56,7 +66,10 @@ int main(int argc, char** argv) {
     printf("{\"units\": %u, \"thr\": %u, \"ms\": %.4f, \"roundtrip_ok\": %s", n, thr, ms, ok ? "true" : "false");
     for (int k = 0; k < 6; ++k) {
         std::vector<double> v(n);
-        for (uint32_t i = 0; i < n; ++i) v[i] = (double)(int64_t)(hp[16ull * i + k + 1] - hp[16ull * i + k]);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint64_t a = hp[16ull * i + k], b = hp[16ull * i + k + 1];
+            v[i] = (a && b) ? (double)(int64_t)(b - a) : 0.0;
+        }
         std::sort(v.begin(), v.end());
         double s = 0; for (double x : v) s += x;
         printf(", \"%s\": [%.0f, %.0f, %.0f]", names[k], s / n, v[n / 2], v[(size_t)(n * 0.99)]);
