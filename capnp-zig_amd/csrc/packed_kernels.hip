@@ -52,6 +52,8 @@ enum : int32_t {
     ST_SPACE = CAPNP_PACKED_OUT_OF_SPACE,
     ST_ARG = CAPNP_PACKED_INVALID_ARGUMENT,
 };
+// internal status between decode passes: the unit goes to a full (fallback) decoder
+constexpr int32_t kStNeedFull = 0x7FFF0001;
 
 // ---------------------------------------------------------------------------
 // small device helpers
@@ -575,7 +577,7 @@ __device__ __forceinline__ void load_piece(const uint8_t* base, uint32_t npieces
     }
 }
 
-template <bool WRITE>
+template <bool WRITE, bool CK = false>
 __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __restrict__ in,
                                                              const uint64_t* __restrict__ in_off,
                                                              const uint64_t* __restrict__ in_len,
@@ -591,6 +593,7 @@ __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __re
     }
     const uint32_t unit = blockIdx.x * kBlock + threadIdx.x;
     if (unit >= n) return;
+    if (CK && status[unit] != kStNeedFull) return;  // size-only fallback after decode_index_kernel<true>
     const uint8_t* src = in + in_off[unit];
     const uint64_t P = in_len[unit];
     uint64_t* dst = nullptr;
@@ -950,7 +953,6 @@ __device__ __forceinline__ uint64_t gload_u64_unaligned(const uint8_t* p) {
 // also yields the decoded size, EOF and out-of-space statuses. Units it does not
 // take (packed start not 16-B aligned, more than kWvWin packed bytes) get
 // kStNeedFull and are decoded by the wave kernel's full path.
-constexpr int32_t kStNeedFull = 0x7FFF0001;    // internal: wave kernel resolves the chain itself
 constexpr uint32_t kCkWaves = 2;
 constexpr uint32_t kCkBlock = kCkWaves * kWave;
 constexpr uint32_t kCkSlot = kWave * 64;        // one 64-B block for every lane of the wave
@@ -1103,14 +1105,23 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t unit = blockIdx.x * kWvWaves + wave;
-    if (unit >= n) return;  // wave-uniform
     uint8_t* pk = pk_all + wave * kWvPk;
     uint8_t* mk = mk_all + wave * kWvWin;
-
-    // CK: decode_ckpt_kernel ran first; this kernel then takes only the units it
-    // marked kStNeedFull (every other status is final or decode_expand_kernel's).
-    if (CK && status[unit] != kStNeedFull) return;  // decode_expand_kernel takes ST_OK units
+    // CK: a first pass (decode_index_kernel / decode_ckpt_kernel) ran; this kernel
+    // then takes only the units it marked kStNeedFull, with a small grid striding
+    // over the batch (every other status is final or the fill pass's).
+    // The wave tests 64 statuses per load (CK) and walks the marked units in order.
+    const uint32_t stride = CK ? gridDim.x * kWvWaves * kWave : gridDim.x * kWvWaves;
+    for (uint32_t ubase = CK ? (blockIdx.x * kWvWaves + wave) * kWave : blockIdx.x * kWvWaves + wave; ubase < n;
+         ubase += stride) {
+    uint64_t todo = 1;
+    if (CK) {
+        const uint32_t u = ubase + lane;
+        todo = __ballot(u < n && status[u] == kStNeedFull);
+    }
+    while (todo) {  // wave-uniform
+    const uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : ubase;
+    todo &= todo - 1;
     const uint8_t* src = in + in_off[unit];
     const uint64_t P = in_len[unit];
     uint8_t* dstb = out + out_off[unit];
@@ -1120,7 +1131,7 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
             out_len[unit] = 0;
             status[unit] = ST_ARG;
         }
-        return;
+        continue;
     }
     uint64_t* const dst = reinterpret_cast<uint64_t*>(dstb);
 
@@ -1307,6 +1318,8 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         out_len[unit] = (st == ST_OK) ? 8 * Wb : 0;
         status[unit] = (st != ST_OK) ? st : (fits ? ST_OK : ST_SPACE);
     }
+    }  // marked units
+    }  // unit loop
 }
 
 // ---------------------------------------------------------------------------
@@ -1440,6 +1453,434 @@ __global__ __launch_bounds__(kExBlock) void decode_expand_kernel(const uint8_t* 
 }
 
 // ---------------------------------------------------------------------------
+// DECODE, indexed two-pass decoder (the default)
+// ---------------------------------------------------------------------------
+// Pass 1, decode_index_kernel: lane l of a wave owns unit l and walks its record
+// chain once (message.zig:152-191), lockstep by 64-B input block: in round k
+// every lane consumes the records whose tag lies in block k of its unit. Blocks
+// reach LDS by LDS-DMA — five 1-KiB instructions per round stage 64 rows of
+// (64-B block + 16-B look-ahead), so a record's tag, count byte and FF count
+// byte are three reads off one row address — two rounds ahead, in a 3-slot
+// ring, with fixed vmcnt waits (every round issues the same instructions). The
+// walk yields the decoded size and the EOF status, and for every 16-B piece of
+// the unit (16-B aligned address space) the offset of the first tag that starts
+// in it (16: none): the entry index, one byte per piece, written to the start of
+// the unit's own output slot (pass 2 reads it before it writes any output).
+//
+// Pass 2, decode_fill_kernel: one wave per unit. The unit's pieces and its entry
+// index are staged in LDS; lane j takes pieces [jL, jL + L), L = ceil(pieces/64),
+// and starts at their first entry, so no chain is resolved: a count walk over
+// its own records, a wave scan for output word offsets, an expand walk into a
+// zeroed LDS staging area (zero runs cost nothing), and coalesced stores.
+//
+// Units pass 2 cannot stage (> kFlPieces pieces) or whose slot cannot hold the
+// index get kStNeedFull from pass 1 and go to decode_wave_kernel<true>.
+constexpr uint32_t kIxWaves = 2;
+constexpr uint32_t kIxRow = 80;                   // 64-B block + 16-B look-ahead per unit
+constexpr uint32_t kIxSlot = kWave * kIxRow;      // one round of 64 units
+constexpr uint32_t kIxRing = 3;                   // round k in use, k+1 and k+2 in flight
+constexpr uint32_t kIxNone = 16;                  // entry byte: no tag starts in the piece
+constexpr uint32_t kIxDead = 0xFFFFFFFFu;         // walk position of a lane with nothing (more) to walk
+constexpr uint32_t kFlPieces = 320;               // pass-2 window: 64 lanes x 5 pieces
+constexpr uint64_t kIxSizeMax = 1ull << 31;       // size-only walk: longer units use decode_lane_kernel
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16 readable bytes for DMA lanes that have nothing to stage, and 16 writable
+// bytes for the entry-index stores of lanes without a unit.
+__device__ __attribute__((aligned(16))) uint8_t cpk_dummy16[16];
+__device__ __attribute__((aligned(16))) uint8_t cpk_sink16[16];
+
+template <bool SIZE_ONLY>
+__global__ __launch_bounds__(kIxWaves * kWave) void decode_index_kernel(const uint8_t* __restrict__ in,
+                                                                        const uint64_t* __restrict__ in_off,
+                                                                        const uint64_t* __restrict__ in_len,
+                                                                        uint32_t n, uint8_t* __restrict__ out,
+                                                                        const uint64_t* __restrict__ out_off,
+                                                                        const uint64_t* __restrict__ out_cap,
+                                                                        uint64_t* __restrict__ out_len,
+                                                                        int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kIxWaves * kIxRing * kIxSlot];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const ring = ring_all + wave * (kIxRing * kIxSlot);
+    const uint32_t unit = (blockIdx.x * kIxWaves + wave) * kWave + lane;
+    const bool valid = unit < n;
+
+    // ---- per-lane unit ---------------------------------------------------------------
+    const uint8_t* src = cpk_dummy16;
+    uint64_t P64 = 0, cap = 0;
+    uint8_t* dstb = nullptr;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P64 = in_len[unit];
+        if (!SIZE_ONLY) {
+            dstb = out + out_off[unit];
+            cap = out_cap[unit];
+            if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+        }
+    }
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    bool take = valid && st == ST_OK && P64 > 0;
+    if (take) {
+        const uint64_t np = (s + P64 + 15) >> 4;
+        const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && cap >= ((np + 15) & ~15ull));
+        if (!fits) {
+            take = false;
+            st = kStNeedFull;
+        }
+    }
+    const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
+    const uint32_t npieces = (end + 15) >> 4;
+    uint32_t maxr = (end + 63) >> 6;                     // rounds this lane needs
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
+    maxr = __builtin_amdgcn_readfirstlane(maxr);
+
+    // ---- DMA descriptors: instruction m, lane l moves piece (64m+l)%5 of row (64m+l)/5 ---
+    const uint8_t* dsrc[5];
+    uint32_t dpi[5], dlast[5];
+#pragma unroll
+    for (uint32_t m = 0; m < 5; ++m) {
+        const uint32_t r = (64 * m + lane) / 5;
+        const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
+        const uint32_t rn = __shfl(npieces, r, kWave);
+        dsrc[m] = rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16;
+        dlast[m] = rn ? rn - 1 : 0u;
+        dpi[m] = (64 * m + lane) % 5;
+    }
+    auto dma = [&](uint32_t k) {  // stage round k (block k + look-ahead of every row) into slot k % 3
+        uint8_t* slot = ring + (k % kIxRing) * kIxSlot;
+#pragma unroll
+        for (uint32_t m = 0; m < 5; ++m) {
+            const uint32_t piece = min(4 * k + dpi[m], dlast[m]);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[m] + 16ull * piece),
+                                             (__attribute__((address_space(3))) void*)(slot + 1024 * m), 16, 0,
+                                             0);
+        }
+    };
+
+    uint32_t pos = take ? s : kIxDead;  // next tag (aligned space)
+    uint64_t words = 0;                 // decoded words so far
+    uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0;  // entry bytes of the last four rounds
+    uint64_t* const ixp = reinterpret_cast<uint64_t*>((!SIZE_ONLY && take) ? dstb : cpk_sink16);
+    const uint32_t ngroups = (npieces + 15) >> 4;  // 16-B groups of entry bytes in the slot
+    if (maxr > 0) dma(0);
+    if (maxr > 1) dma(1);
+    for (uint32_t k = 0; k < maxr; ++k) {
+        // Round k's DMA must have landed. Younger than it: round k+1's DMA (5, when
+        // there is one) and, if round k-1 flushed entry bytes, that 1 store.
+        if (k + 1 < maxr) {
+            if (!SIZE_ONLY && (k & 3) == 0 && k > 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        wave_lds_sync();
+        const uint8_t* const row = ring + (k % kIxRing) * kIxSlot + lane * kIxRow;
+        const uint32_t b0 = 64 * k;
+        const uint32_t lim = min(b0 + 64, end);
+        uint64_t bits = 0;       // tags that start in block k (bit = offset)
+        uint32_t rw = 0;         // words of this round
+        for (;;) {  // one record per lane per pass; branch-free body, uniform exit
+            const bool act = pos < lim;  // a finished or failed lane has pos = kIxDead
+            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+            const uint32_t o = act ? pos - b0 : 0u;  // inactive lanes read their row harmlessly
+            uint32_t t = row[o];
+            uint32_t b1 = row[o + 1];
+            uint32_t c9 = row[o + 9];
+            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per record
+            const bool z = t == 0u, f = t == 0xFFu;
+            const uint32_t len = 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u);
+            const bool eof = act && pos + len > end;  // message.zig:152-191: record runs past the input
+            const bool ok = act && !eof;
+            st = eof ? ST_EOF : st;
+            bits |= ok ? (1ull << o) : 0ull;
+            rw += ok ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
+            pos = eof ? kIxDead : (ok ? pos + len : pos);
+        }
+        words += rw;
+        if (!SIZE_ONLY) {
+            const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
+            const uint32_t e = __builtin_ctz((lo & 0xFFFFu) | 0x10000u) |
+                               (__builtin_ctz((lo >> 16) | 0x10000u) << 8) |
+                               (__builtin_ctz((hi & 0xFFFFu) | 0x10000u) << 16) |
+                               (__builtin_ctz((hi >> 16) | 0x10000u) << 24);
+            g0 = g1; g1 = g2; g2 = g3; g3 = e;
+            if ((k & 3) == 3 || k + 1 == maxr) {  // flush 16 entry bytes (pieces 16*(k/4) ..)
+                for (uint32_t r = k & 3; r < 3; ++r) { g0 = g1; g1 = g2; g2 = g3; g3 = 0x10101010u; }
+                // every lane stores (lanes without a unit into cpk_dummy16), so the vmcnt count is fixed
+                uint64_t* const q = (take && (k >> 2) < ngroups) ? ixp + 2 * (k >> 2)
+                                                                 : reinterpret_cast<uint64_t*>(cpk_sink16);
+                // exactly one store instruction (the vmcnt waits above count it); the
+                // slot is 8-B aligned, which gfx950 global stores accept
+                u32x4 v = {g0, g1, g2, g3};
+                asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(q), "v"(v) : "memory");
+            }
+        }
+        if (k + 2 < maxr) dma(k + 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
+    if (!valid) return;
+    if (st == kStNeedFull) {
+        status[unit] = st;
+        return;
+    }
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8 * words;
+    status[unit] = (!SIZE_ONLY && 8 * words > cap) ? ST_SPACE : ST_OK;
+}
+
+constexpr uint32_t kFlWaves = 4;
+constexpr uint32_t kFlPk = kFlPieces * 16 + 16;   // staged pieces + room for 16-B reads at the last tag
+constexpr uint32_t kFlOut = 512;                  // output words per staging pass
+
+// s_waitcnt needs an immediate: wait until at most min(c, 8) vector-memory
+// operations are outstanding (a smaller count than the true number of younger
+// operations only waits longer).
+__device__ __forceinline__ void vmcnt_at_most(uint32_t c) {
+    switch (c) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+// Per-unit values the fill pass needs. A wave loads them for 64 of its units at
+// once (lane i: the wave's unit k0 + i), so one vector load per array serves 64
+// units and each unit reads its values from registers (readlane).
+struct FillMeta {
+    int32_t st;
+    uint32_t P;
+    const uint8_t* src;
+    uint8_t* dst;
+    uint32_t T;  // output words
+};
+
+__global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uint8_t* __restrict__ in,
+                                                                       const uint64_t* __restrict__ in_off,
+                                                                       const uint64_t* __restrict__ in_len,
+                                                                       uint32_t n, uint8_t* __restrict__ out,
+                                                                       const uint64_t* __restrict__ out_off,
+                                                                       const uint64_t* __restrict__ out_len,
+                                                                       const int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFlWaves * kFlPk];
+    __shared__ __attribute__((aligned(16))) uint64_t stg_all[kFlWaves * (kFlOut + 2)];  // + a dummy word
+    __shared__ __attribute__((aligned(16))) uint8_t ent_all[kFlWaves * kFlPieces];
+    __shared__ uint64_t lut[256];  // tag -> v_perm selector scattering popc(tag) packed bytes
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    lut[threadIdx.x] = expand_selector(threadIdx.x);
+    __syncthreads();
+    uint8_t* const pk = pk_all + wave * kFlPk;
+    uint64_t* const stg = stg_all + wave * (kFlOut + 2);
+    uint8_t* const ent = ent_all + wave * kFlPieces;
+    const uint32_t G = gridDim.x * kFlWaves;  // persistent: the wave takes units u0, u0+G, u0+2G, ...
+    const uint32_t u0 = blockIdx.x * kFlWaves + wave;
+    if (u0 >= n) return;
+
+    uint64_t m_in = 0, m_out = 0;
+    uint32_t m_P = 0, m_T = 0;
+    int32_t m_st = -1;
+    auto load_batch = [&](uint32_t k0) {  // meta of the wave's units k0 .. k0+63
+        const uint64_t uu = (uint64_t)u0 + (uint64_t)(k0 + lane) * G;
+        m_st = -1;
+        if (uu < n) {
+            m_in = in_off[uu];
+            m_P = (uint32_t)in_len[uu];
+            m_out = out_off[uu];
+            m_T = (uint32_t)(out_len[uu] >> 3);
+            m_st = status[uu];
+        }
+    };
+    auto meta = [&](uint32_t j) {  // the batch's unit j (wave-uniform j)
+        FillMeta m;
+        m.st = (int32_t)readlane((uint32_t)m_st, j);
+        m.P = readlane(m_P, j);
+        m.src = in + ((uint64_t)readlane((uint32_t)m_in, j) | ((uint64_t)readlane((uint32_t)(m_in >> 32), j) << 32));
+        m.dst = out + ((uint64_t)readlane((uint32_t)m_out, j) | ((uint64_t)readlane((uint32_t)(m_out >> 32), j) << 32));
+        m.T = readlane(m_T, j);
+        return m;
+    };
+
+    // Registers of the prefetched unit: its pieces (lane l: pieces l + 64m) and its
+    // entry index (lane l: bytes 8l .. 8l+7). Unit k+1 is loaded while unit k is decoded.
+    uint4 v0, v1, v2, v3, v4;
+    uint64_t ev = 0;
+    auto load_unit = [&](const FillMeta& m) {
+        const bool go = m.st == ST_OK && m.P > 0;  // wave-uniform
+        if (!go) return;
+        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(m.src) & 15);
+        const uint4* const b = reinterpret_cast<const uint4*>(m.src - s);
+        const uint32_t np = (s + m.P + 15) >> 4;
+        const uint32_t last = np - 1;
+        v0 = b[min(lane, last)];
+        if (np > 64) v1 = b[min(lane + 64, last)];
+        if (np > 128) v2 = b[min(lane + 128, last)];
+        if (np > 192) v3 = b[min(lane + 192, last)];
+        if (np > 256) v4 = b[min(lane + 256, last)];
+        const uint32_t ne8 = (np + 7) >> 3;
+        ev = reinterpret_cast<const uint64_t*>(m.dst)[min(lane, ne8 - 1)];
+    };
+
+    load_batch(0);
+    FillMeta cur = meta(0);
+    load_unit(cur);
+    uint32_t younger = 0;  // vector-memory ops issued after cur's loads (its predecessor's stores)
+    for (uint32_t k = 0; (uint64_t)u0 + (uint64_t)k * G < n; ++k) {
+        const bool go = cur.st == ST_OK && cur.P > 0;
+        vmcnt_at_most(younger);  // cur's pieces and entry index are in registers
+        younger = 0;
+        uint32_t np = 0, s = 0, end = 0;
+        if (go) {
+            s = (uint32_t)(reinterpret_cast<uintptr_t>(cur.src) & 15);
+            end = s + cur.P;
+            np = (end + 15) >> 4;  // <= kFlPieces (decode_index_kernel)
+            wave_lds_sync();       // the previous unit's LDS reads are done
+            uint4* const pk4 = reinterpret_cast<uint4*>(pk);
+            pk4[lane] = v0;
+            if (np > 64) pk4[lane + 64] = v1;
+            if (np > 128) pk4[lane + 128] = v2;
+            if (np > 192) pk4[lane + 192] = v3;
+            if (np > 256) pk4[lane + 256] = v4;
+            if (lane < ((np + 7) >> 3)) reinterpret_cast<uint64_t*>(ent)[lane] = ev;
+#pragma unroll
+            for (uint32_t i = 0; i < kFlOut / 128; ++i)
+                reinterpret_cast<uint4*>(stg)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+            wave_lds_sync();
+        }
+        // the next unit's loads go out before any store of this unit
+        const uint32_t k1 = k + 1;
+        if ((k1 & 63) == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of cur in flight but its loads (landed)
+            load_batch(k1);
+        }
+        const FillMeta nxt = meta(k1 & 63);  // st = -1 past the batch end
+        load_unit(nxt);
+        if (go) {
+            // ---- lane range and first tag -------------------------------------------------
+            const uint32_t L = (np + 63) >> 6;
+            const uint32_t q0 = min(lane * L, np), q1 = min(q0 + L, np);
+            const uint32_t jend = min(16 * q1, end);
+            uint32_t pos = jend;
+            for (uint32_t q = q1; q > q0;) {
+                --q;
+                const uint32_t e = ent[q];
+                if (e < kIxNone) pos = 16 * q + e;
+            }
+            // ---- count walk + scan ----------------------------------------------------------
+            uint32_t words = 0;
+            for (uint32_t p = pos;;) {
+                const bool act = p < jend;
+                if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                const uint32_t pp = act ? p : 0u;
+                uint32_t t = pk[pp];
+                uint32_t b1 = pk[pp + 1];
+                uint32_t c9 = pk[pp + 9];
+                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                const bool z = t == 0u, f = t == 0xFFu;
+                words += act ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
+                p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u) : p;
+            }
+            const uint32_t incl = wave_incl_sum(words, lane);
+            const uint32_t wbase = incl - words;
+            // ---- expand walk into the zeroed staging area, coalesced stores, 512 words a pass
+            const bool a16 = !(reinterpret_cast<uintptr_t>(cur.dst) & 15);
+            uint64_t* const dst = reinterpret_cast<uint64_t*>(cur.dst);
+            const uint32_t T = cur.T;
+            for (uint32_t W0 = 0; W0 < T; W0 += kFlOut) {
+                const uint32_t W1 = min(T, W0 + kFlOut);
+                if (W0 > 0) {
+                    wave_lds_sync();
+#pragma unroll
+                    for (uint32_t i = 0; i < kFlOut / 128; ++i)
+                        reinterpret_cast<uint4*>(stg)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+                    wave_lds_sync();
+                }
+                const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
+                uint32_t p = pos, w = wbase;
+                if (T <= kFlOut) {
+                    // one staging pass holds every word: no window tests; inactive lanes
+                    // write the dummy word, so the store needs no exec change
+                    for (;;) {
+                        const bool act = p < jend;
+                        if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                        const uint32_t pp = act ? p : 0u;
+                        const uint32_t a = pp & ~7u, sh = 8u * (pp & 7u);
+                        uint64_t lo = *reinterpret_cast<const uint64_t*>(pk + a);
+                        uint64_t hi = *reinterpret_cast<const uint64_t*>(pk + a + 8);
+                        uint32_t c9 = pk[pp + 9];
+                        asm volatile("" : "+v"(lo), "+v"(hi), "+v"(c9));
+                        const uint32_t t = (uint32_t)(lo >> sh) & 0xFFu;
+                        const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));  // bytes p+1 .. p+8
+                        const bool z = t == 0u, f = t == 0xFFu;
+                        // message.zig:101-141: 00 -> zero word(s) (lut[0] selects nothing), FF ->
+                        // literal word (lut[FF] is the identity) + c literal words, other tags ->
+                        // scatter of popc(t) bytes
+                        stg[act ? w : kFlOut] = perm64(pay, lut[t]);
+                        const uint32_t c = f ? c9 : 0u;
+                        if (act && c) {  // FF run body: literal words p+10 .. p+10+8c
+                            for (uint32_t i = 1; i <= c; ++i) stg[w + i] = lds_u64_at(pk, pp + 2 + 8 * i);
+                        }
+                        w = act ? w + 1u + (z ? (uint32_t)(pay & 0xFFu) : 0u) + c : w;
+                        p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
+                    }
+                } else {
+                    for (;;) {  // one record per lane per pass; predicated body, uniform exit
+                        const bool act = mine && p < jend && w < W1;
+                        if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                        const uint32_t pp = act ? p : 0u;
+                        const uint32_t a = pp & ~7u, sh = 8u * (pp & 7u);
+                        uint64_t lo = *reinterpret_cast<const uint64_t*>(pk + a);
+                        uint64_t hi = *reinterpret_cast<const uint64_t*>(pk + a + 8);
+                        uint32_t c9 = pk[pp + 9];
+                        asm volatile("" : "+v"(lo), "+v"(hi), "+v"(c9));
+                        const uint32_t t = (uint32_t)(lo >> sh) & 0xFFu;
+                        const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));
+                        const bool z = t == 0u, f = t == 0xFFu;
+                        stg[(act && w >= W0) ? w - W0 : kFlOut] = perm64(pay, lut[t]);
+                        const uint32_t c = f ? c9 : 0u;
+                        if (act && c) {
+                            for (uint32_t i = 1; i <= c; ++i) {
+                                const uint32_t wi = w + i;
+                                if (wi >= W0 && wi < W1) stg[wi - W0] = lds_u64_at(pk, pp + 2 + 8 * i);
+                            }
+                        }
+                        w = act ? w + 1u + (z ? (uint32_t)(pay & 0xFFu) : 0u) + c : w;
+                        p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
+                    }
+                }
+                wave_lds_sync();
+                const uint32_t nw = W1 - W0;
+                if (a16) {
+                    for (uint32_t i = 2 * lane; i < nw; i += 2 * kWave) {
+                        if (i + 1 < nw) *reinterpret_cast<uint4*>(dst + W0 + i) = *reinterpret_cast<const uint4*>(stg + i);
+                        else dst[W0 + i] = stg[i];
+                    }
+                    younger += (nw + 2 * kWave - 1) / (2 * kWave);
+                } else {
+                    for (uint32_t i = lane; i < nw; i += kWave) dst[W0 + i] = stg[i];
+                    younger += (nw + kWave - 1) / kWave;
+                }
+            }
+        }
+        cur = nxt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
 // synthetic generator and offset scan
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t seed, uint64_t unit, uint64_t word) {
@@ -1567,33 +2008,76 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
 }
 
 // Decoder selection, read per launch so tests can exercise every
-// decoder in one process: CPK_DECODE_VARIANT unset = lane-per-unit stream decoder
-// (one wave per block), 2 = the same with two waves per block, 3 = 8-word rounds,
-// 0 = wave per unit, 5 = checkpoint pass + expansion pass.
+// decoder in one process: CPK_DECODE_VARIANT unset = indexed two-pass decoder
+// (decode_index_kernel + decode_fill_kernel), 4 = lane-per-unit stream decoder,
+// 2 = the same with two waves per block, 3 = 8-word rounds, 0 = wave per unit,
+// 5 = checkpoint pass + expansion pass.
 static int decode_variant() {
     const char* e = getenv("CPK_DECODE_VARIANT");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 6;
+}
+
+// Persistent grid of the fill pass: 4 resident blocks per CU (LDS-bound), each
+// wave striding over the batch with one unit in flight ahead.
+static uint32_t fill_blocks(uint32_t n) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        cus = c;
+    }
+    const uint32_t full = (n + kFlWaves - 1) / kFlWaves;
+    const uint32_t cap = 4u * (uint32_t)cus;
+    return full < cap ? full : cap;
+}
+
+// Grid of the fallback pass for units a first pass declined: it strides over the
+// batch reading statuses, so it stays cheap when (as usual) there are none.
+static uint32_t fallback_blocks(uint32_t n) {
+    const uint32_t full = (n + kWvWaves * kWave - 1) / (kWvWaves * kWave);
+    return full < 2048u ? full : 2048u;
 }
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (!write) {  // size pass: lane walk without stores
+    const int variant = decode_variant();
+    if (!write) {  // size pass
+        if (variant == 6) {
+            const uint32_t per = kIxWaves * kWave;
+            decode_index_kernel<true><<<(n + per - 1) / per, per, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                out_cap, out_len, status);
+            decode_lane_kernel<false, true><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(
+                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+            return hipGetLastError();
+        }
         const uint32_t blocks = (n + kBlock - 1) / kBlock;
         decode_lane_kernel<false><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                   out_len, status);
         return hipGetLastError();
     }
-    switch (decode_variant()) {
+    switch (variant) {
         case 0: break;  // wave per unit, below
+        case 6: {       // index pass, fill pass, full path for what the first pass declined
+            const uint32_t per = kIxWaves * kWave;
+            decode_index_kernel<false><<<(n + per - 1) / per, per, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                 out_cap, out_len, status);
+            decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
+                                                                               out_off, out_len, status);
+            decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                out_cap, out_len, status);
+            return hipGetLastError();
+        }
         case 5: {       // checkpoint pass, expansion pass, full path for what the first pass declined
             decode_ckpt_kernel<<<(n + kCkBlock - 1) / kCkBlock, kCkBlock, 0, stream>>>(
                 in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
             decode_expand_kernel<<<(n + kExWaves - 1) / kExWaves, kExBlock, 0, stream>>>(
                 in, in_off, in_len, n, out, out_off, out_len, status);
-            decode_wave_kernel<true><<<(n + kWvWaves - 1) / kWvWaves, kWvBlock, 0, stream>>>(
-                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+            decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                out_cap, out_len, status);
             return hipGetLastError();
         }
         case 3: {
@@ -1602,13 +2086,13 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                         out_len, status);
             return hipGetLastError();
         }
-        case 2: {       // stream, two waves per block (round 1 default)
+        case 2: {       // stream, two waves per block
             const uint32_t blocks = (n + 2 * kWave - 1) / (2 * kWave);
             decode_stream_kernel<16, 2><<<blocks, 2 * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                          out_len, status);
             return hipGetLastError();
         }
-        default: {      // stream, one wave per block (default)
+        default: {      // stream, one wave per block
             const uint32_t blocks = (n + kWave - 1) / kWave;
             decode_stream_kernel<16, 1><<<blocks, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status);
