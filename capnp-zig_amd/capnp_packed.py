@@ -26,7 +26,8 @@ except ImportError:  # pragma: no cover - the ABI still loads for symbol checks
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libcapnp_packed.so")
+# CPK_LIB selects an experimental build of the same library (scripts/ diagnostics only)
+LIB_PATH = os.environ.get("CPK_LIB") or os.path.join(HERE, "lib", "libcapnp_packed.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "capnp_packed.h")
 
 OK = 0

@@ -276,3 +276,4 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
 }
 
 }  // extern "C"
+

@@ -28,6 +28,7 @@
 // handle any unit size on their fast path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "capnp_packed.h"
@@ -1455,56 +1456,52 @@ __global__ __launch_bounds__(kExBlock) void decode_expand_kernel(const uint8_t* 
 // ---------------------------------------------------------------------------
 // DECODE, indexed two-pass decoder (the default)
 // ---------------------------------------------------------------------------
-// Pass 1, decode_index_kernel: lane l of a wave owns unit l and walks its record
-// chain once (message.zig:152-191), lockstep by 64-B input block: in round k
-// every lane consumes the records whose tag lies in block k of its unit. Blocks
-// reach LDS by LDS-DMA — five 1-KiB instructions per round stage 64 rows of
-// (64-B block + 16-B look-ahead), so a record's tag, count byte and FF count
-// byte are three reads off one row address — two rounds ahead, in a 3-slot
-// ring, with fixed vmcnt waits (every round issues the same instructions). The
-// walk yields the decoded size and the EOF status, and for every 16-B piece of
-// the unit (16-B aligned address space) the offset of the first tag that starts
-// in it (16: none): the entry index, one byte per piece, written to the start of
-// the unit's own output slot (pass 2 reads it before it writes any output).
-//
-// Pass 2, decode_fill_kernel: one wave per unit. The unit's pieces and its entry
-// index are staged in LDS; lane j takes pieces [jL, jL + L), L = ceil(pieces/64),
-// and starts at their first entry, so no chain is resolved: a count walk over
-// its own records, a wave scan for output word offsets, an expand walk into a
-// zeroed LDS staging area (zero runs cost nothing), and coalesced stores.
-//
+// The record chain (tag -> record length -> next tag) is serial within a unit, so
+// the decoder splits it from the byte work:
+//   pass 1 (decode_index_kernel) walks every unit's chain once, lane per unit, and
+//          leaves a u16 record per 16-B piece (first tag offset, words produced);
+//   pass 2 (decode_fill_kernel) gives each unit a wave whose lanes start at their
+//          own pieces' first tags (no chain to resolve), take their output word
+//          offsets from a scan of the records' word counts, expand into LDS and
+//          store coalesced.
 // Units pass 2 cannot stage (> kFlPieces pieces) or whose slot cannot hold the
-// index get kStNeedFull from pass 1 and go to decode_wave_kernel<true>.
-constexpr uint32_t kIxWaves = 2;
-constexpr uint32_t kIxRow = 80;                   // 64-B block + 16-B look-ahead per unit
-constexpr uint32_t kIxSlot = kWave * kIxRow;      // one round of 64 units
-constexpr uint32_t kIxRing = 3;                   // round k in use, k+1 and k+2 in flight
-constexpr uint32_t kIxNone = 16;                  // entry byte: no tag starts in the piece
+// records get kStNeedFull from pass 1 and go to decode_wave_kernel<true>.
 constexpr uint32_t kIxDead = 0xFFFFFFFFu;         // walk position of a lane with nothing (more) to walk
 constexpr uint32_t kFlPieces = 320;               // pass-2 window: 64 lanes x 5 pieces
 constexpr uint64_t kIxSizeMax = 1ull << 31;       // size-only walk: longer units use decode_lane_kernel
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// 16 readable bytes for DMA lanes that have nothing to stage, and 16 writable
-// bytes for the entry-index stores of lanes without a unit.
+// 16 readable bytes for load lanes that have nothing to stage, and 16 writable
+// bytes for the piece-record stores of lanes without a unit.
 __device__ __attribute__((aligned(16))) uint8_t cpk_dummy16[16];
 __device__ __attribute__((aligned(16))) uint8_t cpk_sink16[16];
+__device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 
+// Pass 1, decode_index_kernel: lane l of a wave owns unit l and walks its record
+// chain once (message.zig:152-191), lockstep by 64-B input block. Every byte is
+// fetched from HBM once: round k's loads are quad-coalesced (4 lanes x 16 B = one
+// unit's 64-B block, 16 units per instruction), issued one round ahead into
+// registers, and written to the lane-major LDS ring: unit u keeps blocks k-1 and
+// k at ring_u + (k & 1) * 64 (plus a mirror of the even block's first 16 B at
+// +128, for reads that wrap). Round k walks the tags in [64k - 16, 64k + 48), i.e.
+// pieces 4k-1 .. 4k+2, whose count bytes (+1, +9) are all resident; a final round
+// (k = rounds) walks the last piece.
+//
+// Per piece p the walk yields a u16 record — the offset of the first tag that
+// starts in p (4 bits) | the words its records produce << 4 (0: no tag) — kept at
+// index p + 1 of the record array at the start of the unit's output slot (so a
+// round's four records and a 16-B store stay aligned). Pass 2 reads them before it
+// writes any output. The walk also yields the decoded size and the EOF status.
 template <bool SIZE_ONLY>
-__global__ __launch_bounds__(kIxWaves * kWave) void decode_index_kernel(const uint8_t* __restrict__ in,
-                                                                        const uint64_t* __restrict__ in_off,
-                                                                        const uint64_t* __restrict__ in_len,
-                                                                        uint32_t n, uint8_t* __restrict__ out,
-                                                                        const uint64_t* __restrict__ out_off,
-                                                                        const uint64_t* __restrict__ out_cap,
-                                                                        uint64_t* __restrict__ out_len,
-                                                                        int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kIxWaves * kIxRing * kIxSlot];
+__global__ __launch_bounds__(kWave) void decode_index_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
+    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
+    constexpr uint32_t kRing = 144;  // two 64-B blocks + 16-B mirror
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWave * kRing];
     const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* const ring = ring_all + wave * (kIxRing * kIxSlot);
-    const uint32_t unit = (blockIdx.x * kIxWaves + wave) * kWave + lane;
+    const uint32_t unit = blockIdx.x * kWave + lane;
     const bool valid = unit < n;
 
     // ---- per-lane unit ---------------------------------------------------------------
@@ -1525,7 +1522,8 @@ __global__ __launch_bounds__(kIxWaves * kWave) void decode_index_kernel(const ui
     bool take = valid && st == ST_OK && P64 > 0;
     if (take) {
         const uint64_t np = (s + P64 + 15) >> 4;
-        const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && cap >= ((np + 15) & ~15ull));
+        const uint64_t nr = (s + P64 + 63) >> 6;  // rounds; records take 16 B per two rounds (+1)
+        const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && cap >= 64 * ((nr + 8) / 8));
         if (!fits) {
             take = false;
             st = kStNeedFull;
@@ -1533,95 +1531,122 @@ __global__ __launch_bounds__(kIxWaves * kWave) void decode_index_kernel(const ui
     }
     const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
     const uint32_t npieces = (end + 15) >> 4;
-    uint32_t maxr = (end + 63) >> 6;                     // rounds this lane needs
+    const uint32_t nr = (end + 63) >> 6;                 // rounds with data for this lane
+    uint32_t maxr = nr;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
     maxr = __builtin_amdgcn_readfirstlane(maxr);
 
-    // ---- DMA descriptors: instruction m, lane l moves piece (64m+l)%5 of row (64m+l)/5 ---
-    const uint8_t* dsrc[5];
-    uint32_t dpi[5], dlast[5];
+    // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block -------------
+    const uint4* qsrc[4];
+    uint32_t qlast[4];
 #pragma unroll
-    for (uint32_t m = 0; m < 5; ++m) {
-        const uint32_t r = (64 * m + lane) / 5;
+    for (uint32_t m = 0; m < 4; ++m) {
+        const uint32_t r = 16 * m + lane / 4;
         const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
         const uint32_t rn = __shfl(npieces, r, kWave);
-        dsrc[m] = rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16;
-        dlast[m] = rn ? rn - 1 : 0u;
-        dpi[m] = (64 * m + lane) % 5;
+        qsrc[m] = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16);
+        qlast[m] = rn ? rn - 1 : 0u;
     }
-    auto dma = [&](uint32_t k) {  // stage round k (block k + look-ahead of every row) into slot k % 3
-        uint8_t* slot = ring + (k % kIxRing) * kIxSlot;
-#pragma unroll
-        for (uint32_t m = 0; m < 5; ++m) {
-            const uint32_t piece = min(4 * k + dpi[m], dlast[m]);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[m] + 16ull * piece),
-                                             (__attribute__((address_space(3))) void*)(slot + 1024 * m), 16, 0,
-                                             0);
-        }
+    const uint32_t qp = lane & 3;
+    uint4 d0, d1, d2, d3;
+    auto load = [&](uint32_t k) {
+        d0 = qsrc[0][min(4 * k + qp, qlast[0])];
+        d1 = qsrc[1][min(4 * k + qp, qlast[1])];
+        d2 = qsrc[2][min(4 * k + qp, qlast[2])];
+        d3 = qsrc[3][min(4 * k + qp, qlast[3])];
     };
+    uint8_t* const wq = ring_all + (lane / 4) * kRing + 16 * qp;  // unit 16m + l/4: + 16 * kRing * m
+    const uint8_t* const ring = ring_all + lane * kRing;
 
     uint32_t pos = take ? s : kIxDead;  // next tag (aligned space)
     uint64_t words = 0;                 // decoded words so far
-    uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0;  // entry bytes of the last four rounds
-    uint64_t* const ixp = reinterpret_cast<uint64_t*>((!SIZE_ONLY && take) ? dstb : cpk_sink16);
-    const uint32_t ngroups = (npieces + 15) >> 4;  // 16-B groups of entry bytes in the slot
-    if (maxr > 0) dma(0);
-    if (maxr > 1) dma(1);
-    for (uint32_t k = 0; k < maxr; ++k) {
-        // Round k's DMA must have landed. Younger than it: round k+1's DMA (5, when
-        // there is one) and, if round k-1 flushed entry bytes, that 1 store.
-        if (k + 1 < maxr) {
-            if (!SIZE_ONLY && (k & 3) == 0 && k > 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint64_t rec0 = 0;                  // records of the previous (even) round
+    u32x4 rq0 = {0, 0, 0, 0}, rq1 = rq0, rq2 = rq0, rq3 = rq0;  // 64 B of records waiting for their store
+    uint8_t* const ixp = (!SIZE_ONLY && take) ? dstb : cpk_sink64;
+    const uint32_t nflush = (nr + 8) / 8;  // 64-B record stores of this unit
+    if (maxr > 0) load(0);
+    for (uint32_t k = 0; k <= maxr; ++k) {
+        if (k < maxr) {
+            // round k's loads are the oldest in flight; younger: the 4 record stores of round
+            // k-1 when it flushed (k-1 = 7 mod 8)
+            if (!SIZE_ONLY && (k & 7) == 0 && k > 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_lds_sync();  // every lane is done with block k-2's half of the ring
+            uint8_t* const w = wq + (k & 1) * 64;
+            *reinterpret_cast<uint4*>(w) = d0;
+            *reinterpret_cast<uint4*>(w + 16 * kRing) = d1;
+            *reinterpret_cast<uint4*>(w + 32 * kRing) = d2;
+            *reinterpret_cast<uint4*>(w + 48 * kRing) = d3;
+            if (!(k & 1) && qp == 0) {  // mirror of the even block's first piece
+                *reinterpret_cast<uint4*>(w + 128) = d0;
+                *reinterpret_cast<uint4*>(w + 128 + 16 * kRing) = d1;
+                *reinterpret_cast<uint4*>(w + 128 + 32 * kRing) = d2;
+                *reinterpret_cast<uint4*>(w + 128 + 48 * kRing) = d3;
+            }
+            if (k + 1 < maxr) load(k + 1);
+            wave_lds_sync();
         }
-        wave_lds_sync();
-        const uint8_t* const row = ring + (k % kIxRing) * kIxSlot + lane * kIxRow;
-        const uint32_t b0 = 64 * k;
-        const uint32_t lim = min(b0 + 64, end);
-        uint64_t bits = 0;       // tags that start in block k (bit = offset)
-        uint32_t rw = 0;         // words of this round
+        const uint32_t ob = 64 * k;                 // offset o = pos + 16 - ob in [0, 64)
+        const uint32_t lim = min(ob + 48, end);     // tags of pieces 4k-1 .. 4k+2
+        uint64_t bits = 0;  // tags that start in pieces 4k-1 .. 4k+2 (bit = offset o)
+        uint64_t cnt = 0;   // words of the records of piece 4k-1+i (16-bit field i)
         for (;;) {  // one record per lane per pass; branch-free body, uniform exit
             const bool act = pos < lim;  // a finished or failed lane has pos = kIxDead
             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-            const uint32_t o = act ? pos - b0 : 0u;  // inactive lanes read their row harmlessly
-            uint32_t t = row[o];
-            uint32_t b1 = row[o + 1];
-            uint32_t c9 = row[o + 9];
+            const uint8_t* const a = ring + ((act ? pos : 0u) & 127u);
+            uint32_t t = a[0];
+            uint32_t b1 = a[1];
+            uint32_t c9 = a[9];
             asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per record
             const bool z = t == 0u, f = t == 0xFFu;
             const uint32_t len = 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u);
             const bool eof = act && pos + len > end;  // message.zig:152-191: record runs past the input
             const bool ok = act && !eof;
             st = eof ? ST_EOF : st;
+            const uint32_t o = (pos + 16u - ob) & 63u;
             bits |= ok ? (1ull << o) : 0ull;
-            rw += ok ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
+            const uint32_t wd = 1u + (z ? b1 : 0u) + (f ? c9 : 0u);  // <= 256: a piece sums to <= 2048
+            cnt += ok ? ((uint64_t)wd << (16u * (o >> 4))) : 0ull;
             pos = eof ? kIxDead : (ok ? pos + len : pos);
         }
-        words += rw;
+        words += (cnt & 0xFFFFu) + ((cnt >> 16) & 0xFFFFu) + ((cnt >> 32) & 0xFFFFu) + (cnt >> 48);
         if (!SIZE_ONLY) {
             const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
-            const uint32_t e = __builtin_ctz((lo & 0xFFFFu) | 0x10000u) |
-                               (__builtin_ctz((lo >> 16) | 0x10000u) << 8) |
-                               (__builtin_ctz((hi & 0xFFFFu) | 0x10000u) << 16) |
-                               (__builtin_ctz((hi >> 16) | 0x10000u) << 24);
-            g0 = g1; g1 = g2; g2 = g3; g3 = e;
-            if ((k & 3) == 3 || k + 1 == maxr) {  // flush 16 entry bytes (pieces 16*(k/4) ..)
-                for (uint32_t r = k & 3; r < 3; ++r) { g0 = g1; g1 = g2; g2 = g3; g3 = 0x10101010u; }
-                // every lane stores (lanes without a unit into cpk_dummy16), so the vmcnt count is fixed
-                uint64_t* const q = (take && (k >> 2) < ngroups) ? ixp + 2 * (k >> 2)
-                                                                 : reinterpret_cast<uint64_t*>(cpk_sink16);
-                // exactly one store instruction (the vmcnt waits above count it); the
-                // slot is 8-B aligned, which gfx950 global stores accept
-                u32x4 v = {g0, g1, g2, g3};
-                asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(q), "v"(v) : "memory");
+            const uint64_t e = (uint64_t)(__builtin_ctz(lo | 0x10000u) & 15u) |
+                               ((uint64_t)(__builtin_ctz((lo >> 16) | 0x10000u) & 15u) << 16) |
+                               ((uint64_t)(__builtin_ctz(hi | 0x10000u) & 15u) << 32) |
+                               ((uint64_t)(__builtin_ctz((hi >> 16) | 0x10000u) & 15u) << 48);
+            const uint64_t rec = e | (cnt << 4);  // records 4k .. 4k+3 (pieces 4k-1 .. 4k+2)
+            if ((k & 1) || k == maxr) {
+                // records 8g .. 8g+7 (16 B) go to queue entry g % 4 (a uniform switch: no
+                // register indexing); every 8 rounds, and after the last, the queue is stored
+                // as 64 contiguous bytes per lane (4 store instructions, which the vmcnt waits
+                // above count; lanes without a unit store into cpk_sink64; the slot is 8-B
+                // aligned, which gfx950 global stores accept)
+                const uint32_t g = k >> 1;
+                const uint64_t r0 = (k & 1) ? rec0 : rec, r1 = (k & 1) ? rec : 0ull;
+                const u32x4 v = {(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+                switch (g & 3) {
+                    case 0: rq0 = v; break;
+                    case 1: rq1 = v; break;
+                    case 2: rq2 = v; break;
+                    default: rq3 = v; break;
+                }
+                if ((g & 3) == 3 || k == maxr) {
+                    const uint32_t fb = g >> 2;
+                    uint8_t* const q = (take && fb < nflush) ? ixp + 64 * fb : cpk_sink64;
+                    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(q), "v"(rq0) : "memory");
+                    asm volatile("global_store_dwordx4 %0, %1, off offset:16" ::"v"(q), "v"(rq1) : "memory");
+                    asm volatile("global_store_dwordx4 %0, %1, off offset:32" ::"v"(q), "v"(rq2) : "memory");
+                    asm volatile("global_store_dwordx4 %0, %1, off offset:48" ::"v"(q), "v"(rq3) : "memory");
+                }
+            } else {
+                rec0 = rec;
             }
         }
-        if (k + 2 < maxr) dma(k + 2);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!valid) return;
     if (st == kStNeedFull) {
         status[unit] = st;
@@ -1636,9 +1661,28 @@ __global__ __launch_bounds__(kIxWaves * kWave) void decode_index_kernel(const ui
     status[unit] = (!SIZE_ONLY && 8 * words > cap) ? ST_SPACE : ST_OK;
 }
 
+#ifdef CPK_FILL_PROF
+// Diagnostic build: cycles per fill-kernel phase, summed over waves (s_memtime).
+__device__ unsigned long long cpk_fill_prof[8];
+#define FL_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define FL_ACC(i, d) prof[i] += (d)
+#else
+#define FL_T(v) do { } while (0)
+#define FL_ACC(i, d) do { } while (0)
+#endif
+
 constexpr uint32_t kFlWaves = 4;
-constexpr uint32_t kFlPk = kFlPieces * 16 + 16;   // staged pieces + room for 16-B reads at the last tag
-constexpr uint32_t kFlOut = 512;                  // output words per staging pass
+constexpr uint32_t kFlPk = kFlPieces * 16 + 8;    // staged pieces + room for the 16-B read at the last tag
+constexpr uint32_t kFlOut = 512;                  // output words per code pass
+constexpr uint32_t kFlMaxL = 5;                   // pieces per lane (kFlPieces / 64)
+// Output word codes (u16): a window position q whose byte q is the word's tag and
+// bytes q+1 .. q+8 its packed bytes (a mixed record, or an FF record's first word,
+// whose tag 0xFF selects all 8 bytes), kFlLit | q for a literal word at q+1 .. q+8
+// (an FF run's body), or kFlZero.
+constexpr uint32_t kFlLit = 0x2000u;
+constexpr uint32_t kFlZero = 0xFFFFu;
+constexpr uint32_t kFlPos = 0x1FFFu;
+static_assert(kFlPk < kFlPos, "codes hold window positions");
 
 // s_waitcnt needs an immediate: wait until at most min(c, 8) vector-memory
 // operations are outstanding (a smaller count than the true number of younger
@@ -1668,6 +1712,19 @@ struct FillMeta {
     uint32_t T;  // output words
 };
 
+// Word of a code (see kFlLit): 16 bytes around its position from the staged
+// pieces, then the tag's v_perm selector (literal words: the identity).
+__device__ __forceinline__ uint64_t fill_word(const uint8_t* pk, const uint64_t* lut, uint32_t code) {
+    const uint32_t q = code & kFlPos;
+    const uint32_t a = q & ~7u, sh = 8u * (q & 7u);
+    const uint64_t lo = *reinterpret_cast<const uint64_t*>(pk + a);
+    const uint64_t hi = *reinterpret_cast<const uint64_t*>(pk + a + 8);
+    const uint32_t t = (code & kFlLit) ? 0xFFu : (uint32_t)(lo >> sh) & 0xFFu;
+    const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));  // bytes q+1 .. q+8
+    const uint64_t w = perm64(pay, lut[t]);
+    return code == kFlZero ? 0ull : w;
+}
+
 __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uint8_t* __restrict__ in,
                                                                        const uint64_t* __restrict__ in_off,
                                                                        const uint64_t* __restrict__ in_len,
@@ -1676,16 +1733,14 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                                                                        const uint64_t* __restrict__ out_len,
                                                                        const int32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFlWaves * kFlPk];
-    __shared__ __attribute__((aligned(16))) uint64_t stg_all[kFlWaves * (kFlOut + 2)];  // + a dummy word
-    __shared__ __attribute__((aligned(16))) uint8_t ent_all[kFlWaves * kFlPieces];
+    __shared__ __attribute__((aligned(16))) uint16_t code_all[kFlWaves * (kFlOut + 8)];  // + a dummy slot
     __shared__ uint64_t lut[256];  // tag -> v_perm selector scattering popc(tag) packed bytes
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     lut[threadIdx.x] = expand_selector(threadIdx.x);
     __syncthreads();
     uint8_t* const pk = pk_all + wave * kFlPk;
-    uint64_t* const stg = stg_all + wave * (kFlOut + 2);
-    uint8_t* const ent = ent_all + wave * kFlPieces;
+    uint16_t* const code = code_all + wave * (kFlOut + 8);
     const uint32_t G = gridDim.x * kFlWaves;  // persistent: the wave takes units u0, u0+G, u0+2G, ...
     const uint32_t u0 = blockIdx.x * kFlWaves + wave;
     if (u0 >= n) return;
@@ -1714,10 +1769,11 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
         return m;
     };
 
-    // Registers of the prefetched unit: its pieces (lane l: pieces l + 64m) and its
-    // entry index (lane l: bytes 8l .. 8l+7). Unit k+1 is loaded while unit k is decoded.
+    // Registers of the prefetched unit: its pieces (lane l: pieces l + 64m) and the
+    // records of the lane's own pieces [lL, lL + L) (decode_index_kernel). Unit k+1 is
+    // loaded while unit k is decoded.
     uint4 v0, v1, v2, v3, v4;
-    uint64_t ev = 0;
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
     auto load_unit = [&](const FillMeta& m) {
         const bool go = m.st == ST_OK && m.P > 0;  // wave-uniform
         if (!go) return;
@@ -1730,21 +1786,33 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
         if (np > 128) v2 = b[min(lane + 128, last)];
         if (np > 192) v3 = b[min(lane + 192, last)];
         if (np > 256) v4 = b[min(lane + 256, last)];
-        const uint32_t ne8 = (np + 7) >> 3;
-        ev = reinterpret_cast<const uint64_t*>(m.dst)[min(lane, ne8 - 1)];
+        const uint32_t L = (np + 63) >> 6;
+        const uint16_t* const rec = reinterpret_cast<const uint16_t*>(m.dst);
+        const uint32_t q = lane * L + 1;  // record of piece p: index p + 1 (decode_index_kernel)
+        r0 = rec[min(q, np)];             // lanes past the last piece read the last record (unused)
+        if (L > 1) r1 = rec[min(q + 1, np)];
+        if (L > 2) r2 = rec[min(q + 2, np)];
+        if (L > 3) r3 = rec[min(q + 3, np)];
+        if (L > 4) r4 = rec[min(q + 4, np)];
     };
 
     load_batch(0);
     FillMeta cur = meta(0);
     load_unit(cur);
     uint32_t younger = 0;  // vector-memory ops issued after cur's loads (its predecessor's stores)
+#ifdef CPK_FILL_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     for (uint32_t k = 0; (uint64_t)u0 + (uint64_t)k * G < n; ++k) {
         const bool go = cur.st == ST_OK && cur.P > 0;
-        vmcnt_at_most(younger);  // cur's pieces and entry index are in registers
+        FL_T(t0);
+        vmcnt_at_most(younger);  // cur's pieces and records are in registers
+        FL_T(t1);
+        FL_ACC(0, t1 - t0);
         younger = 0;
-        uint32_t np = 0, s = 0, end = 0;
+        uint32_t np = 0, end = 0, pos = 0, words = 0, jend = 0;
         if (go) {
-            s = (uint32_t)(reinterpret_cast<uintptr_t>(cur.src) & 15);
+            const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(cur.src) & 15);
             end = s + cur.P;
             np = (end + 15) >> 4;  // <= kFlPieces (decode_index_kernel)
             wave_lds_sync();       // the previous unit's LDS reads are done
@@ -1754,11 +1822,20 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
             if (np > 128) pk4[lane + 128] = v2;
             if (np > 192) pk4[lane + 192] = v3;
             if (np > 256) pk4[lane + 256] = v4;
-            if (lane < ((np + 7) >> 3)) reinterpret_cast<uint64_t*>(ent)[lane] = ev;
+            // ---- lane range [q0, q1): first tag and output words, from the piece records ----
+            const uint32_t L = (np + 63) >> 6;
+            const uint32_t q0 = min(lane * L, np), q1 = min(q0 + L, np);
+            const uint32_t nq = q1 - q0;
+            jend = min(16 * q1, end);
+            pos = jend;
+            const uint32_t rr[kFlMaxL] = {r0, r1, r2, r3, r4};
 #pragma unroll
-            for (uint32_t i = 0; i < kFlOut / 128; ++i)
-                reinterpret_cast<uint4*>(stg)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-            wave_lds_sync();
+            for (int i = kFlMaxL - 1; i >= 0; --i) {
+                const uint32_t r = rr[i];
+                const bool has = (uint32_t)i < nq && (r >> 4) != 0;
+                words += has ? (r >> 4) : 0u;
+                pos = has ? 16 * (q0 + i) + (r & 15u) : pos;
+            }
         }
         // the next unit's loads go out before any store of this unit
         const uint32_t k1 = k + 1;
@@ -1767,116 +1844,78 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
             load_batch(k1);
         }
         const FillMeta nxt = meta(k1 & 63);  // st = -1 past the batch end
+        FL_T(t2);
+        FL_ACC(1, t2 - t1);
         load_unit(nxt);
+        FL_T(t3);
+        FL_ACC(2, t3 - t2);
         if (go) {
-            // ---- lane range and first tag -------------------------------------------------
-            const uint32_t L = (np + 63) >> 6;
-            const uint32_t q0 = min(lane * L, np), q1 = min(q0 + L, np);
-            const uint32_t jend = min(16 * q1, end);
-            uint32_t pos = jend;
-            for (uint32_t q = q1; q > q0;) {
-                --q;
-                const uint32_t e = ent[q];
-                if (e < kIxNone) pos = 16 * q + e;
-            }
-            // ---- count walk + scan ----------------------------------------------------------
-            uint32_t words = 0;
-            for (uint32_t p = pos;;) {
-                const bool act = p < jend;
-                if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                const uint32_t pp = act ? p : 0u;
-                uint32_t t = pk[pp];
-                uint32_t b1 = pk[pp + 1];
-                uint32_t c9 = pk[pp + 9];
-                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                const bool z = t == 0u, f = t == 0xFFu;
-                words += act ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
-                p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u) : p;
-            }
             const uint32_t incl = wave_incl_sum(words, lane);
             const uint32_t wbase = incl - words;
-            // ---- expand walk into the zeroed staging area, coalesced stores, 512 words a pass
             const bool a16 = !(reinterpret_cast<uintptr_t>(cur.dst) & 15);
             uint64_t* const dst = reinterpret_cast<uint64_t*>(cur.dst);
             const uint32_t T = cur.T;
             for (uint32_t W0 = 0; W0 < T; W0 += kFlOut) {
+                // ---- code walk: every lane lists the source of each of its words in [W0, W1)
                 const uint32_t W1 = min(T, W0 + kFlOut);
-                if (W0 > 0) {
-                    wave_lds_sync();
-#pragma unroll
-                    for (uint32_t i = 0; i < kFlOut / 128; ++i)
-                        reinterpret_cast<uint4*>(stg)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-                    wave_lds_sync();
-                }
-                const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
-                uint32_t p = pos, w = wbase;
-                if (T <= kFlOut) {
-                    // one staging pass holds every word: no window tests; inactive lanes
-                    // write the dummy word, so the store needs no exec change
-                    for (;;) {
-                        const bool act = p < jend;
-                        if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                        const uint32_t pp = act ? p : 0u;
-                        const uint32_t a = pp & ~7u, sh = 8u * (pp & 7u);
-                        uint64_t lo = *reinterpret_cast<const uint64_t*>(pk + a);
-                        uint64_t hi = *reinterpret_cast<const uint64_t*>(pk + a + 8);
-                        uint32_t c9 = pk[pp + 9];
-                        asm volatile("" : "+v"(lo), "+v"(hi), "+v"(c9));
-                        const uint32_t t = (uint32_t)(lo >> sh) & 0xFFu;
-                        const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));  // bytes p+1 .. p+8
-                        const bool z = t == 0u, f = t == 0xFFu;
-                        // message.zig:101-141: 00 -> zero word(s) (lut[0] selects nothing), FF ->
-                        // literal word (lut[FF] is the identity) + c literal words, other tags ->
-                        // scatter of popc(t) bytes
-                        stg[act ? w : kFlOut] = perm64(pay, lut[t]);
-                        const uint32_t c = f ? c9 : 0u;
-                        if (act && c) {  // FF run body: literal words p+10 .. p+10+8c
-                            for (uint32_t i = 1; i <= c; ++i) stg[w + i] = lds_u64_at(pk, pp + 2 + 8 * i);
-                        }
-                        w = act ? w + 1u + (z ? (uint32_t)(pay & 0xFFu) : 0u) + c : w;
-                        p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
-                    }
-                } else {
-                    for (;;) {  // one record per lane per pass; predicated body, uniform exit
-                        const bool act = mine && p < jend && w < W1;
-                        if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                        const uint32_t pp = act ? p : 0u;
-                        const uint32_t a = pp & ~7u, sh = 8u * (pp & 7u);
-                        uint64_t lo = *reinterpret_cast<const uint64_t*>(pk + a);
-                        uint64_t hi = *reinterpret_cast<const uint64_t*>(pk + a + 8);
-                        uint32_t c9 = pk[pp + 9];
-                        asm volatile("" : "+v"(lo), "+v"(hi), "+v"(c9));
-                        const uint32_t t = (uint32_t)(lo >> sh) & 0xFFu;
-                        const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));
-                        const bool z = t == 0u, f = t == 0xFFu;
-                        stg[(act && w >= W0) ? w - W0 : kFlOut] = perm64(pay, lut[t]);
-                        const uint32_t c = f ? c9 : 0u;
-                        if (act && c) {
-                            for (uint32_t i = 1; i <= c; ++i) {
-                                const uint32_t wi = w + i;
-                                if (wi >= W0 && wi < W1) stg[wi - W0] = lds_u64_at(pk, pp + 2 + 8 * i);
-                            }
-                        }
-                        w = act ? w + 1u + (z ? (uint32_t)(pay & 0xFFu) : 0u) + c : w;
-                        p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
-                    }
-                }
+                wave_lds_sync();  // pieces staged; the previous pass's code reads are done
+                reinterpret_cast<uint4*>(code)[lane] = make_uint4(kFlZero * 0x10001u, kFlZero * 0x10001u,
+                                                                  kFlZero * 0x10001u, kFlZero * 0x10001u);
                 wave_lds_sync();
+                const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
+                uint32_t p = mine ? pos : jend, w = wbase;
+                for (;;) {  // one record per lane per pass; predicated body, uniform exit
+                    const bool act = p < jend && w < W1;
+                    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                    const uint32_t pp = act ? p : 0u;
+                    uint32_t t = pk[pp];
+                    uint32_t b1 = pk[pp + 1];
+                    uint32_t c9 = pk[pp + 9];
+                    asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                    const bool z = t == 0u, f = t == 0xFFu;
+                    // message.zig:101-141: 00 -> zero word(s) (the list starts as kFlZero), FF ->
+                    // its first word (tag 0xFF selects the 8 bytes) + c literal words, other
+                    // tags -> scatter of popc(t) bytes
+                    code[(act && !z && w >= W0) ? w - W0 : kFlOut] = (uint16_t)pp;
+                    const uint32_t c = f ? c9 : 0u;
+                    if (act && c) {  // FF run body: literal word i at bytes pp+2+8i .. pp+9+8i
+                        for (uint32_t i = 1; i <= c; ++i) {
+                            const uint32_t wi = w + i;
+                            if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (pp + 1 + 8 * i));
+                        }
+                    }
+                    w = act ? w + 1u + (z ? b1 : 0u) + c : w;
+                    p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
+                }
+                FL_T(t4);
+                FL_ACC(3, t4 - t3);
+                wave_lds_sync();
+                // ---- expand by output word: coalesced stores straight from registers ----------
                 const uint32_t nw = W1 - W0;
                 if (a16) {
                     for (uint32_t i = 2 * lane; i < nw; i += 2 * kWave) {
-                        if (i + 1 < nw) *reinterpret_cast<uint4*>(dst + W0 + i) = *reinterpret_cast<const uint4*>(stg + i);
-                        else dst[W0 + i] = stg[i];
+                        const uint32_t cc = *reinterpret_cast<const uint32_t*>(code + i);
+                        const uint64_t x0 = fill_word(pk, lut, cc & 0xFFFFu);
+                        const uint64_t x1 = fill_word(pk, lut, cc >> 16);
+                        if (i + 1 < nw) *reinterpret_cast<uint4*>(dst + W0 + i) =
+                            make_uint4((uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32));
+                        else dst[W0 + i] = x0;
                     }
                     younger += (nw + 2 * kWave - 1) / (2 * kWave);
                 } else {
-                    for (uint32_t i = lane; i < nw; i += kWave) dst[W0 + i] = stg[i];
+                    for (uint32_t i = lane; i < nw; i += kWave) dst[W0 + i] = fill_word(pk, lut, code[i]);
                     younger += (nw + kWave - 1) / kWave;
                 }
             }
         }
+        FL_T(t5);
+        FL_ACC(4, t5 - t0);
         cur = nxt;
     }
+#ifdef CPK_FILL_PROF
+    if (lane == 0)
+        for (int i = 0; i < 5; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -2017,20 +2056,33 @@ static int decode_variant() {
     return e ? atoi(e) : 6;
 }
 
-// Persistent grid of the fill pass: 4 resident blocks per CU (LDS-bound), each
-// wave striding over the batch with one unit in flight ahead.
+// Persistent grid of the fill pass: as many blocks as are resident at once
+// (hipOccupancy..., LDS/VGPR-bound), each wave striding over the batch with one
+// unit in flight ahead.
 static uint32_t fill_blocks(uint32_t n) {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, c = 0;
+    static uint32_t resident = 0;
+    if (resident == 0) {
+        int dev = 0, cus = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-            c = 256;
-        cus = c;
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decode_fill_kernel, kFlWaves * kWave, 0) !=
+                hipSuccess || per <= 0)
+            per = 4;
+        resident = (uint32_t)(cus * per);
+        if (getenv("CPK_DEBUG_GRID")) fprintf(stderr, "fill grid: %d CUs x %d blocks\n", cus, per);
     }
     const uint32_t full = (n + kFlWaves - 1) / kFlWaves;
-    const uint32_t cap = 4u * (uint32_t)cus;
-    return full < cap ? full : cap;
+    return full < resident ? full : resident;
+}
+
+// Pass 1 of the indexed decoder: one wave (64 units) per block.
+template <bool SIZE_ONLY>
+static void launch_index(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
+                         const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                         hipStream_t stream) {
+    decode_index_kernel<SIZE_ONLY><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                   out_cap, out_len, status);
 }
 
 // Grid of the fallback pass for units a first pass declined: it strides over the
@@ -2047,9 +2099,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const int variant = decode_variant();
     if (!write) {  // size pass
         if (variant == 6) {
-            const uint32_t per = kIxWaves * kWave;
-            decode_index_kernel<true><<<(n + per - 1) / per, per, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                out_cap, out_len, status);
+            launch_index<true>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
             decode_lane_kernel<false, true><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(
                 in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
             return hipGetLastError();
@@ -2062,9 +2112,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     switch (variant) {
         case 0: break;  // wave per unit, below
         case 6: {       // index pass, fill pass, full path for what the first pass declined
-            const uint32_t per = kIxWaves * kWave;
-            decode_index_kernel<false><<<(n + per - 1) / per, per, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                 out_cap, out_len, status);
+            launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
             decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
                                                                                out_off, out_len, status);
             decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
@@ -2133,3 +2181,12 @@ hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t*
 }
 
 }  // namespace cpk
+
+#ifdef CPK_FILL_PROF
+// Diagnostic build only: read and clear the fill-kernel phase cycle sums.
+extern "C" int capnp_packed_debug_fill_prof(unsigned long long* out8) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_fill_prof), sizeof(z)) != hipSuccess) return 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(cpk::cpk_fill_prof), z, sizeof(z)) != hipSuccess;
+}
+#endif

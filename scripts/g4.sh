@@ -10,3 +10,4 @@ for t in 128 26 230; do
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 scripts/microbench.py --only decode --reps 5 > $O/prof.log 2>&1 || exit $?
 python3 scripts/kstats.py $O/prof/run_kernel_stats.csv
+bash scripts/g9.sh
