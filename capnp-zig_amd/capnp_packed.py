@@ -38,6 +38,12 @@ OUT_OF_SPACE = 4
 INVALID_ARGUMENT = 5
 DEVICE_ERROR = 6
 NO_DEVICE = 7
+# Reader.readPackedMessage (reader.zig:84-156)
+END_OF_STREAM = 8
+INVALID_SEGMENT_COUNT = 9
+SEGMENT_COUNT_LIMIT_EXCEEDED = 10
+MESSAGE_TOO_LARGE = 11
+INVALID_PACKED_MESSAGE = 12
 
 
 class PackedError(Exception):
@@ -72,24 +78,34 @@ class NoDevice(PackedError):
     status = NO_DEVICE
 
 
-_ERRORS = {c.status: c for c in (InvalidMessageSize, UnexpectedEof, Overflow, OutOfSpace,
-                                 InvalidArgument, DeviceError, NoDevice)}
-
-# Message.init errors (message.zig:341-394)
-class EndOfStream(Exception):
-    pass
+# Message.init (message.zig:341-394) and Reader.readPackedMessage (reader.zig:84-156) errors
+class EndOfStream(PackedError):
+    status = END_OF_STREAM
 
 
-class InvalidSegmentCount(Exception):
-    pass
+class InvalidSegmentCount(PackedError):
+    status = INVALID_SEGMENT_COUNT
 
 
-class SegmentCountLimitExceeded(Exception):
-    pass
+class SegmentCountLimitExceeded(PackedError):
+    status = SEGMENT_COUNT_LIMIT_EXCEEDED
+
+
+class MessageTooLarge(PackedError):  # reader.zig:140
+    status = MESSAGE_TOO_LARGE
+
+
+class InvalidPackedMessage(PackedError):  # reader.zig:151-153
+    status = INVALID_PACKED_MESSAGE
 
 
 class TruncatedMessage(Exception):
     pass
+
+
+_ERRORS = {c.status: c for c in (InvalidMessageSize, UnexpectedEof, Overflow, OutOfSpace,
+                                 InvalidArgument, DeviceError, NoDevice, EndOfStream, InvalidSegmentCount,
+                                 SegmentCountLimitExceeded, MessageTooLarge, InvalidPackedMessage)}
 
 
 _lib = None
@@ -109,6 +125,9 @@ SIGNATURES = {
     "capnp_packed_encoded_size_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
     "capnp_packed_decode_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "capnp_packed_decoded_size_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
+    "capnp_packed_read_message_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
+                                                       _vp, _vp]),
+    "capnp_packed_read_message": (ctypes.c_int, [_vp, _sz, _vp, _sz, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
     "capnp_packed_scan_scratch_bytes": (_sz, [ctypes.c_uint32]),
     "capnp_packed_lengths_to_offsets": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp,
                                                        _sz, _vp]),
@@ -296,6 +315,43 @@ class Reader:
     def init_packed(cls, data) -> "Reader":
         return cls(Message.init_packed(data))
 
+    @staticmethod
+    def read_packed_message(reader) -> bytes:
+        """Reader.readPackedMessage (reader.zig:84-156): decode the packed message at
+        the front of `reader` (bytes-like, or a binary file object with read/seek)
+        and return its framed bytes, stopping at the length its segment table
+        declares. A file object is left just past the message; on an error it is
+        left where it was."""
+        if hasattr(reader, "read"):
+            start = reader.tell()
+            data = reader.read()
+            try:
+                framed, used = read_packed_message_bytes(data)
+            except PackedError:
+                reader.seek(start)
+                raise
+            reader.seek(start + used)
+            return framed
+        return read_packed_message_bytes(reader)[0]
+
+
+def read_packed_message_bytes(data) -> tuple:
+    """(framed bytes, packed bytes consumed) of the message at the front of `data`
+    (reader.zig:84-156), through the single-buffer C-ABI entry point."""
+    data = bytes(data)
+    src = _cbuf(data)
+    cap = max(4096, 8 * len(data))
+    for _ in range(2):  # a zero-run heavy message can expand past the first guess
+        out = ctypes.create_string_buffer(cap)
+        n, used = _sz(), _sz()
+        st = lib().capnp_packed_read_message(src, len(data), out, cap, ctypes.byref(n), ctypes.byref(used))
+        if st == OUT_OF_SPACE and n.value > cap:
+            cap = n.value
+            continue
+        _raise(st, "readPackedMessage")
+        return out.raw[:n.value], used.value
+    raise OutOfSpace("readPackedMessage: framed length grew between calls")
+
 
 # ---------------------------------------------------------------------------
 # device-resident batch API (torch tensors in HBM)
@@ -339,6 +395,17 @@ def decoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> No
     n = in_off.numel()
     _raise(lib().capnp_packed_decoded_size_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(out_len),
                                                  _ptr(status), _stream(stream)), "decoded_size_batch")
+
+
+def read_message_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, consumed, status,
+                       stream=None) -> None:
+    """Batch Reader.readPackedMessage (reader.zig:84-156): one message from the front
+    of each unit (a reader's buffered packed stream) -> its slot; consumed[i] =
+    packed bytes the message took (0 on error), out_len[i] = framed bytes."""
+    n = in_off.numel()
+    _raise(lib().capnp_packed_read_message_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
+                                                 _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(consumed),
+                                                 _ptr(status), _stream(stream)), "read_message_batch")
 
 
 def lengths_to_offsets(lengths, base: int = 0, out=None, stream=None):

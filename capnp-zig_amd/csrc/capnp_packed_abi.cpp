@@ -97,14 +97,16 @@ struct HostCtx {
 
 HostCtx g_ctx;
 
-// Run one unit through a batch kernel. kind: 0 encode, 1 decode, 2 decoded size, 3 encoded size.
-int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out) {
+// Run one unit through a batch kernel. kind: 0 encode, 1 decode, 2 decoded size, 3 encoded size,
+// 4 read message (reader.zig:84-156; *used_out = packed bytes consumed).
+int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out,
+               uint64_t* used_out = nullptr) {
     int st = g_ctx.init();
     if (st) return st;
     if ((st = g_ctx.reserve(&g_ctx.d_in, &g_ctx.in_cap, n + 16))) return st;
-    const bool write = (kind == 0 || kind == 1);
+    const bool write = (kind == 0 || kind == 1 || kind == 4);
     if (write && (st = g_ctx.reserve(&g_ctx.d_out, &g_ctx.out_cap, slot + 16))) return st;
-    uint64_t meta[6] = {0, n, 0, slot, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status
+    uint64_t meta[7] = {0, n, 0, slot, 0, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status, consumed
     hipStream_t s = g_ctx.stream;
     hipError_t e = hipSuccess;
     if (n) e = hipMemcpyAsync(g_ctx.d_in, in, n, hipMemcpyHostToDevice, s);
@@ -114,6 +116,8 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
     int32_t* d_status = reinterpret_cast<int32_t*>(m + 5);
     if (kind == 0 || kind == 3)
         e = cpk::launch_encode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
+    else if (kind == 4)
+        e = cpk::launch_read_message(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, m + 6, d_status, s);
     else
         e = cpk::launch_decode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
@@ -123,6 +127,7 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
     int32_t status;
     std::memcpy(&status, &meta[5], sizeof(status));
     *len_out = meta[4];
+    if (used_out) *used_out = meta[6];
     if (status == CAPNP_PACKED_OK && write && meta[4]) {
         e = hipMemcpy(out, g_ctx.d_out, meta[4], hipMemcpyDeviceToHost);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpy(D2H out)");
@@ -157,6 +162,11 @@ const char* capnp_packed_status_name(int status) {
         case CAPNP_PACKED_INVALID_ARGUMENT: return "InvalidArgument";
         case CAPNP_PACKED_DEVICE_ERROR: return "DeviceError";
         case CAPNP_PACKED_NO_DEVICE: return "NoDevice";
+        case CAPNP_PACKED_END_OF_STREAM: return "EndOfStream";
+        case CAPNP_PACKED_INVALID_SEGMENT_COUNT: return "InvalidSegmentCount";
+        case CAPNP_PACKED_SEGMENT_COUNT_LIMIT_EXCEEDED: return "SegmentCountLimitExceeded";
+        case CAPNP_PACKED_MESSAGE_TOO_LARGE: return "MessageTooLarge";
+        case CAPNP_PACKED_INVALID_PACKED_MESSAGE: return "InvalidPackedMessage";
         default: return "Unknown";
     }
 }
@@ -249,6 +259,34 @@ int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_of
     hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, nullptr, nullptr, nullptr, d_out_len, d_status,
                                       false, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode-size launch");
+}
+
+int capnp_packed_read_message_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                                    const uint64_t* d_out_cap, uint64_t* d_out_len, uint64_t* d_consumed,
+                                    int32_t* d_status, void* stream) {
+    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
+    if (st || n == 0) return st;
+    if (!d_out_off || !d_out_cap || !d_consumed) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output arrays");
+    hipError_t e = cpk::launch_read_message(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                                            d_consumed, d_status, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "read-message launch");
+}
+
+int capnp_packed_read_message(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len,
+                              size_t* consumed) {
+    if (!out_len || !consumed) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "out_len/consumed is null");
+    *out_len = 0;
+    *consumed = 0;
+    if ((n && !in) || (cap && !out)) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null buffer");
+    int st = ensure_device();
+    if (st) return st;
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    uint64_t len = 0, used = 0;
+    st = run_single(4, in, n, out, cap, &len, &used);
+    *out_len = (size_t)len;
+    *consumed = (size_t)used;
+    return st;
 }
 
 size_t capnp_packed_scan_scratch_bytes(uint32_t n) { return cpk::scan_scratch_bytes(n); }

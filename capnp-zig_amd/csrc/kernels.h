@@ -15,6 +15,11 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream);
 
+// Reader.readPackedMessage over a batch of reader streams (reader.zig:84-156).
+hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                               uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
+                               uint64_t* consumed, int32_t* status, hipStream_t stream);
+
 hipError_t launch_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
                            uint64_t seed, uint32_t thr, hipStream_t stream);
 

@@ -52,6 +52,12 @@ enum : int32_t {
     ST_EOF = CAPNP_PACKED_UNEXPECTED_EOF,
     ST_SPACE = CAPNP_PACKED_OUT_OF_SPACE,
     ST_ARG = CAPNP_PACKED_INVALID_ARGUMENT,
+    // Reader.readPackedMessage (reader.zig:84-156)
+    ST_EOS = CAPNP_PACKED_END_OF_STREAM,
+    ST_SEGCOUNT = CAPNP_PACKED_INVALID_SEGMENT_COUNT,
+    ST_SEGLIMIT = CAPNP_PACKED_SEGMENT_COUNT_LIMIT_EXCEEDED,
+    ST_TOOLARGE = CAPNP_PACKED_MESSAGE_TOO_LARGE,
+    ST_OVERSHOOT = CAPNP_PACKED_INVALID_PACKED_MESSAGE,
 };
 // internal status between decode passes: the unit goes to a full (fallback) decoder
 constexpr int32_t kStNeedFull = 0x7FFF0001;
@@ -1493,11 +1499,25 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 // index p + 1 of the record array at the start of the unit's output slot (so a
 // round's four records and a 16-B store stay aligned). Pass 2 reads them before it
 // writes any output. The walk also yields the decoded size and the EOF status.
-template <bool SIZE_ONLY>
+//
+// RD selects the Reader.readPackedMessage passes (reader.zig:84-156; launch_read_message):
+//   kRdNone  unpackPacked / estimateUnpackedSize as above;
+//   kRdWalk  size-only walk that stops at the first record boundary where the decoded
+//            words reach out_len[unit] / 8 (the framed length read_header_kernel
+//            derived) and writes the bytes it took to consumed[unit]; units whose
+//            status is not OK on entry are left alone;
+//   kRdGate  the write pass over in_len = consumed, again skipping units whose
+//            status is not OK on entry.
+constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2;
+
+template <bool SIZE_ONLY, int RD = kRdNone>
 __global__ __launch_bounds__(kWave) void decode_index_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
-    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
+    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+    uint64_t* __restrict__ consumed) {
+    static_assert(RD != kRdWalk || SIZE_ONLY, "the read walk writes no output");
+    static_assert(RD != kRdGate || !SIZE_ONLY, "the gated pass is the write pass");
     constexpr uint32_t kRing = 144;  // two 64-B blocks + 16-B mirror
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWave * kRing];
     const uint32_t lane = lane_id();
@@ -1509,9 +1529,18 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
     uint64_t P64 = 0, cap = 0;
     uint8_t* dstb = nullptr;
     int32_t st = ST_OK;
+    bool gated = false;       // RD: an earlier pass already settled this unit
+    uint64_t lim_w = ~0ull;   // kRdWalk: words of the framed message
     if (valid) {
+        if (RD != kRdNone) gated = status[unit] != ST_OK;
         src = in + in_off[unit];
         P64 = in_len[unit];
+        if (RD == kRdWalk) {
+            lim_w = out_len[unit] >> 3;
+            // a message of <= 8 Mi + 257 words takes < 2^31 packed bytes (<= 10 B per word),
+            // so the walk always stops before this clamp
+            if (P64 > kIxSizeMax - 1) P64 = kIxSizeMax - 1;
+        }
         if (!SIZE_ONLY) {
             dstb = out + out_off[unit];
             cap = out_cap[unit];
@@ -1519,7 +1548,7 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
         }
     }
     const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    bool take = valid && st == ST_OK && P64 > 0;
+    bool take = valid && !gated && st == ST_OK && P64 > 0;
     if (take) {
         const uint64_t np = (s + P64 + 15) >> 4;
         const uint64_t nr = (s + P64 + 63) >> 6;  // rounds; records take 16 B per two rounds (+1)
@@ -1561,7 +1590,8 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
 
     uint32_t pos = take ? s : kIxDead;  // next tag (aligned space)
     uint64_t words = 0;                 // decoded words so far
-    uint64_t rec0 = 0;                  // records of the previous (even) round
+    uint64_t wrun = 0;                  // kRdWalk: decoded words so far, per record
+    uint64_t rec0 = 0;                 // records of the previous (even) round
     u32x4 rq0 = {0, 0, 0, 0}, rq1 = rq0, rq2 = rq0, rq3 = rq0;  // 64 B of records waiting for their store
     uint8_t* const ixp = (!SIZE_ONLY && take) ? dstb : cpk_sink64;
     const uint32_t nflush = (nr + 8) / 8;  // 64-B record stores of this unit
@@ -1592,7 +1622,8 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
         uint64_t bits = 0;  // tags that start in pieces 4k-1 .. 4k+2 (bit = offset o)
         uint64_t cnt = 0;   // words of the records of piece 4k-1+i (16-bit field i)
         for (;;) {  // one record per lane per pass; branch-free body, uniform exit
-            const bool act = pos < lim;  // a finished or failed lane has pos = kIxDead
+            // a finished or failed lane has pos = kIxDead; a read walk stops at the framed length
+            const bool act = pos < lim && (RD != kRdWalk || wrun < lim_w);
             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
             const uint8_t* const a = ring + ((act ? pos : 0u) & 127u);
             uint32_t t = a[0];
@@ -1609,7 +1640,9 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
             const uint32_t wd = 1u + (z ? b1 : 0u) + (f ? c9 : 0u);  // <= 256: a piece sums to <= 2048
             cnt += ok ? ((uint64_t)wd << (16u * (o >> 4))) : 0ull;
             pos = eof ? kIxDead : (ok ? pos + len : pos);
+            if (RD == kRdWalk) wrun += ok ? wd : 0u;
         }
+        if (RD == kRdWalk && __builtin_amdgcn_ballot_w64(pos < end && wrun < lim_w) == 0) break;  // all stopped
         words += (cnt & 0xFFFFu) + ((cnt >> 16) & 0xFFFFu) + ((cnt >> 32) & 0xFFFFu) + (cnt >> 48);
         if (!SIZE_ONLY) {
             const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
@@ -1647,7 +1680,17 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!valid) return;
+    if (!valid || gated) return;  // gated: status and out_len of an earlier pass stand
+    if (RD == kRdWalk) {
+        // reader.zig:91-93 / 146-153: the walk ended at the framed length (OK), past it
+        // (InvalidPackedMessage), or the stream ended first (EndOfStream, also for a
+        // record cut short: readByte / readNoEof)
+        const int32_t rs = (st != ST_OK || wrun < lim_w) ? ST_EOS : (wrun != lim_w ? ST_OVERSHOOT : ST_OK);
+        status[unit] = rs;
+        consumed[unit] = rs == ST_OK ? (uint64_t)(pos - s) : 0ull;
+        if (rs != ST_OK) out_len[unit] = 0;
+        return;
+    }
     if (st == kStNeedFull) {
         status[unit] = st;
         return;
@@ -1920,6 +1963,98 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 }
 
 // ---------------------------------------------------------------------------
+// Reader.readPackedMessage, batched (reader.zig:84-156)
+// ---------------------------------------------------------------------------
+// Unit i is one reader's buffered packed stream; one message is decoded from its
+// front. Four passes (launch_read_message):
+//   1. read_header_kernel: lane per unit, decodes records until the segment table
+//      is complete (one record for a 1-segment message) and writes the framed
+//      length to out_len, or the header error to status;
+//   2. decode_index_kernel<true, kRdWalk>: the coalesced tag walk, stopped at the
+//      framed length; writes consumed (packed bytes of the message) and the
+//      EndOfStream / InvalidPackedMessage outcome;
+//   3. + 4. the indexed decoder (index pass kRdGate, fill pass, full-path fallback)
+//      over in_len = consumed, skipping units with a non-OK status.
+constexpr uint64_t kMaxTotalWords = 8ull * 1024 * 1024;  // reader.zig:6
+constexpr uint64_t kMaxSegments = 512;                   // message.zig:310
+constexpr uint64_t kHdrMaxWords = 257;                   // (1 + 512 + pad) u32 = 257 words
+
+// Pass 1. Checks follow the reference's order: a record cut short by the end of
+// the stream (EndOfStream), then after the first record InvalidSegmentCount /
+// SegmentCountLimitExceeded (reader.zig:121-125), then once header_bytes are
+// decoded MessageTooLarge (:140). Segment sizes are summed from the header's
+// words as the records produce them (zero words add nothing).
+__global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len, uint32_t n,
+                                                             uint64_t* __restrict__ out_len,
+                                                             uint64_t* __restrict__ consumed,
+                                                             int32_t* __restrict__ status) {
+    const uint32_t unit = blockIdx.x * kBlock + threadIdx.x;
+    if (unit >= n) return;
+    const uint8_t* const p = in + in_off[unit];
+    const uint64_t P = in_len[unit];
+    uint64_t r = 0;          // read cursor
+    uint64_t words = 0;      // decoded words (out.items.len / 8)
+    uint64_t count = 0;      // segment count (set by word 0)
+    uint32_t count_m1 = 0;
+    uint64_t total = 0;      // sum of the sizes decoded so far
+    uint64_t needed = 0;
+    int32_t st = ST_OK;
+    for (;;) {
+        if (r >= P) { st = ST_EOS; break; }  // :95 readByte
+        const uint32_t t = p[r++];
+        uint64_t w0 = 0;
+        uint32_t c = 0;
+        const uint8_t* lit = p;
+        if (t == 0x00) {  // :96-99
+            if (r >= P) { st = ST_EOS; break; }
+            c = p[r++];
+        } else if (t == 0xFF) {  // :100-110
+            if (P - r < 9) { st = ST_EOS; break; }
+            w0 = gload_u64_unaligned(p + r);
+            c = p[r + 8];
+            r += 9;
+            if (P - r < 8ull * c) { st = ST_EOS; break; }
+            lit = p + r;
+            r += 8ull * c;
+        } else {  // :111-119
+            if (P - r < (uint64_t)__popc(t)) { st = ST_EOS; break; }
+            for (uint32_t k = 0; k < 8; ++k)
+                if ((t >> k) & 1u) w0 |= (uint64_t)p[r++] << (8 * k);
+        }
+        // the record's words that hold header u32s: u32 j of the frame is
+        // segment count - 1 (j = 0) or the size of segment j - 1 (1 <= j <= count)
+        const uint64_t nw = 1ull + c;
+        if (words == 0) {
+            count_m1 = (uint32_t)w0;
+            count = (uint64_t)count_m1 + 1;
+        }
+        if (t != 0x00) {
+            for (uint64_t i = 0; i < nw && words + i < kHdrMaxWords; ++i) {
+                const uint64_t w = i == 0 ? w0 : gload_u64_unaligned(lit + 8 * (i - 1));
+                const uint64_t j = 2 * (words + i);
+                if (j >= 1 && j <= count) total += (uint32_t)w;
+                if (j + 1 <= count) total += w >> 32;
+            }
+        }
+        words += nw;
+        // :121-144 (out.items.len >= 4 after any record)
+        if (count_m1 == 0xFFFFFFFFu) { st = ST_SEGCOUNT; break; }
+        if (count > kMaxSegments) { st = ST_SEGLIMIT; break; }
+        const uint64_t header_bytes = 4 * (1 + count + ((count & 1) ? 0 : 1));
+        if (8 * words >= header_bytes) {
+            if (total > kMaxTotalWords) { st = ST_TOOLARGE; break; }
+            needed = header_bytes + 8 * total;
+            break;
+        }
+    }
+    status[unit] = st;
+    out_len[unit] = st == ST_OK ? needed : 0;
+    consumed[unit] = 0;
+}
+
+// ---------------------------------------------------------------------------
 // synthetic generator and offset scan
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t seed, uint64_t unit, uint64_t word) {
@@ -2082,7 +2217,7 @@ static void launch_index(const uint8_t* in, const uint64_t* in_off, const uint64
                          const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
                          hipStream_t stream) {
     decode_index_kernel<SIZE_ONLY><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                   out_cap, out_len, status);
+                                                                                   out_cap, out_len, status, nullptr);
 }
 
 // Grid of the fallback pass for units a first pass declined: it strides over the
@@ -2150,6 +2285,25 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
     decode_wave_kernel<false><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                out_len, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                               uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
+                               uint64_t* consumed, int32_t* status, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t wv = (n + kWave - 1) / kWave;
+    read_header_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
+                                                                         status);
+    decode_index_kernel<true, kRdWalk><<<wv, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                  out_len, status, consumed);
+    // the message's own bytes from here on: in_len = consumed
+    decode_index_kernel<false, kRdGate><<<wv, kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off, out_cap,
+                                                                   out_len, status, nullptr);
+    decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off,
+                                                                       out_len, status);
+    decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
+                                                                        out_cap, out_len, status);
     return hipGetLastError();
 }
 

@@ -45,7 +45,13 @@ enum capnp_packed_status {
     CAPNP_PACKED_OUT_OF_SPACE = 4,         /* output capacity too small; *out_len holds the required size */
     CAPNP_PACKED_INVALID_ARGUMENT = 5,     /* null pointer, decreasing offsets, or a misaligned word-side offset */
     CAPNP_PACKED_DEVICE_ERROR = 6,         /* HIP runtime error; see capnp_packed_last_error() */
-    CAPNP_PACKED_NO_DEVICE = 7             /* no gfx950 device / HIP code object not loadable */
+    CAPNP_PACKED_NO_DEVICE = 7,            /* no gfx950 device / HIP code object not loadable */
+    /* Reader.readPackedMessage (reader.zig:84-156) only: */
+    CAPNP_PACKED_END_OF_STREAM = 8,             /* the stream ends inside the message (readByte/readNoEof) */
+    CAPNP_PACKED_INVALID_SEGMENT_COUNT = 9,     /* segment count - 1 == 0xFFFFFFFF (reader.zig:123) */
+    CAPNP_PACKED_SEGMENT_COUNT_LIMIT_EXCEEDED = 10, /* more than 512 segments (reader.zig:125) */
+    CAPNP_PACKED_MESSAGE_TOO_LARGE = 11,        /* more than 8 Mi words (reader.zig:140) */
+    CAPNP_PACKED_INVALID_PACKED_MESSAGE = 12    /* the last record overshoots the framed length (reader.zig:151-153) */
 };
 
 /* Version / capability query (precedent: src/wasm/capnp_host_abi.zig:60-70). */
@@ -123,6 +129,30 @@ int capnp_packed_decode_batch(const uint8_t* d_in, const uint64_t* d_in_off, con
 /* Batch estimateUnpackedSize (message.zig:152-191). */
 int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                     uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Batch Reader.readPackedMessage (reader.zig:84-156). Unit i is the buffered
+ * packed byte stream of one reader (e.g. one connection). ONE message is decoded
+ * from its front, stopping at the framed length its segment table declares; the
+ * bytes after it (the next message) are not read.
+ *   d_out_len[i]  framed (unpacked) bytes written to the slot
+ *   d_consumed[i] packed bytes the message took: the caller advances the reader
+ *                 by it and calls again for the next message
+ * Per-unit errors leave d_consumed = 0 and d_out_len = 0:
+ *   END_OF_STREAM (the message is incomplete: call again with more bytes),
+ *   INVALID_SEGMENT_COUNT, SEGMENT_COUNT_LIMIT_EXCEEDED, MESSAGE_TOO_LARGE,
+ *   INVALID_PACKED_MESSAGE (the last record overshoots the framed length).
+ * OUT_OF_SPACE instead reports the framed length in d_out_len and the message's
+ * packed length in d_consumed (retry with a larger slot). */
+int capnp_packed_read_message_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                                    const uint64_t* d_out_cap, uint64_t* d_out_len, uint64_t* d_consumed,
+                                    int32_t* d_status, void* stream);
+
+/* Single-buffer Reader.readPackedMessage on HOST memory: decodes the message at
+ * the front of in[0..n) into out[0..*out_len); *consumed = packed bytes used.
+ * On OUT_OF_SPACE, *out_len is the framed length. */
+int capnp_packed_read_message(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len,
+                              size_t* consumed);
 
 /* Exclusive scan of n lengths into n+1 offsets (d_off[0] = base, d_off[n] =
  * base + total), on device.

@@ -47,6 +47,22 @@ def test_version_and_status_names():
     assert names == ["Ok", "InvalidMessageSize", "UnexpectedEof", "Overflow", "OutOfSpace",
                      "InvalidArgument", "DeviceError", "NoDevice"]
     assert cp.encode_bound(4096) == 5120 and cp.encode_bound(0) == 0
+    # Reader.readPackedMessage errors (reader.zig:84-156)
+    names = [cp.lib().capnp_packed_status_name(i).decode() for i in range(8, 13)]
+    assert names == ["EndOfStream", "InvalidSegmentCount", "SegmentCountLimitExceeded", "MessageTooLarge",
+                     "InvalidPackedMessage"]
+    for st in range(13):
+        if st:
+            assert cp._ERRORS[st].status == st
+
+
+def test_read_message_argument_validation_without_device():
+    n, used = ctypes.c_size_t(5), ctypes.c_size_t(5)
+    assert cp.lib().capnp_packed_read_message(None, 8, None, 0, ctypes.byref(n), ctypes.byref(used)) == \
+        cp.INVALID_ARGUMENT
+    assert n.value == 0 and used.value == 0
+    assert cp.lib().capnp_packed_read_message(b"\x00\x00", 2, None, 0, None, ctypes.byref(used)) == \
+        cp.INVALID_ARGUMENT
 
 
 def test_gfx950_code_object_present():
