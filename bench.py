@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory leg")
+    ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
     return ap.parse_args()
 
 
@@ -197,7 +198,7 @@ def host_path(args, dev, n_units=1 << 16):
                 b["pk"][:hi - lo].copy_(h_pk[lo:hi], non_blocking=True)
                 b["len"].copy_(h_len[c * per:(c + 1) * per], non_blocking=True)
                 cp.lengths_to_offsets(b["len"], out=b["off"], stream=sm)
-                cp.decode_batch(b["pk"], b["off"], b["len"], b["un"], b["u_off"], b["u_len"],
+                cp.decode_batch(b["pk"], b["off"][:-1], b["len"], b["un"], b["u_off"], b["u_len"],
                                 b["olen"], b["st"], stream=sm)
                 h_out[c * per * ub:(c + 1) * per * ub].copy_(b["un"], non_blocking=True)
 
@@ -228,6 +229,41 @@ def host_path(args, dev, n_units=1 << 16):
                 "note": "GiB/s of unpacked bytes; pinned host buffers, 8 chunks over 2 streams, dense "
                         "packed stream on the host side (PCIe Gen5 x16, 63 GB/s spec)"})
     return res
+
+
+def read_message_leg(args, dev, reps=10):
+    """SURVEY §8(f) row 1, Reader.readPackedMessage (reader.zig:84-156) batched: the
+    same 1M x 4 KiB units made into framed messages (one segment of 511 words), packed
+    into slots, then read back one message per reader stream, each stream holding its
+    message plus 8 bytes of whatever follows. Device-resident, HIP events on the
+    launch stream; reported beside `value`, never as it."""
+    n, ub = args.units, args.unit_bytes
+    stream = torch.cuda.current_stream()
+    wl = Workload(n, ub, args.seed, args.zero_thresh, unit_base=0, dev=dev)
+    wl.d_in.view(torch.int64).view(n, ub // 8)[:, 0] = (ub // 8 - 1) << 32  # segment table
+    wl.encode(stream)
+    used = torch.zeros(n, dtype=torch.int64, device=dev)
+    tail = torch.minimum(wl.plen + 8, wl.pk_cap)
+
+    def run():
+        cp.read_message_batch(wl.d_pk, wl.pk_off, tail, wl.d_out, wl.in_off, wl.in_len, wl.ulen, used, wl.ust,
+                              stream=stream)
+
+    run()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    ev[0].record(stream)
+    for _ in range(reps):
+        run()
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    ok = bool((wl.ust == 0).all().item() and torch.equal(used, wl.plen) and torch.equal(wl.d_out, wl.d_in))
+    P = int(wl.plen.sum().item())
+    return {"ms": round(ms, 4), "GiB_s": round(n * ub / (ms * 1e-3) / 2 ** 30, 2),
+            "alg_GB_s": round((n * ub + P + 8 * n + 48 * n) / (ms * 1e-3) / 1e9, 1),
+            "messages": n, "framed_bytes": ub, "bit_exact": ok,
+            "note": "GiB/s of framed (unpacked) bytes; header pass + framed-length walk + indexed decode"}
 
 
 def load_traffic(config_key):
@@ -273,6 +309,10 @@ def main():
                            "encode_ms": round(em, 4), "decode_ms": round(dm, 4),
                            "packed_ratio": round(int(g.sum().item()) / (world * n * ub), 4),
                            "bit_exact_roundtrip": wl.verify()}
+    if world == 1 and not args.no_read_message:
+        del wl
+        torch.cuda.empty_cache()
+        extra["read_message"] = read_message_leg(args, dev)
 
     if rank == 0:
         steps = args.steps

@@ -367,17 +367,27 @@ def _stream(stream) -> int:
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
 
 
+def _units(in_off, *per_unit) -> int:
+    """Unit count of a batch (in_off's length); every per-unit tensor must hold at
+    least that many entries (the kernels index them by unit)."""
+    n = in_off.numel()
+    for t in per_unit:
+        if t is not None and t.numel() < n:
+            raise InvalidArgument(f"per-unit tensor has {t.numel()} entries for {n} units")
+    return n
+
+
 def encode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None) -> None:
     """Batch packPacked: unit i = d_in[in_off[i] : in_off[i]+in_len[i]] -> slot
     d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit."""
-    n = in_off.numel()
+    n = _units(in_off, in_len, out_off, out_cap, out_len, status)
     _raise(lib().capnp_packed_encode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out), _ptr(out_off),
                                            _ptr(out_cap), _ptr(out_len), _ptr(status), _stream(stream)),
            "encode_batch")
 
 
 def encoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> None:
-    n = in_off.numel()
+    n = _units(in_off, in_len, out_len, status)
     _raise(lib().capnp_packed_encoded_size_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(out_len),
                                                  _ptr(status), _stream(stream)), "encoded_size_batch")
 
@@ -385,14 +395,14 @@ def encoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> No
 def decode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None) -> None:
     """Batch unpackPacked: unit i = d_in[in_off[i] : in_off[i]+in_len[i]] -> slot
     d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit."""
-    n = in_off.numel()
+    n = _units(in_off, in_len, out_off, out_cap, out_len, status)
     _raise(lib().capnp_packed_decode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out), _ptr(out_off),
                                            _ptr(out_cap), _ptr(out_len), _ptr(status), _stream(stream)),
            "decode_batch")
 
 
 def decoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> None:
-    n = in_off.numel()
+    n = _units(in_off, in_len, out_len, status)
     _raise(lib().capnp_packed_decoded_size_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(out_len),
                                                  _ptr(status), _stream(stream)), "decoded_size_batch")
 
@@ -402,7 +412,7 @@ def read_message_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, c
     """Batch Reader.readPackedMessage (reader.zig:84-156): one message from the front
     of each unit (a reader's buffered packed stream) -> its slot; consumed[i] =
     packed bytes the message took (0 on error), out_len[i] = framed bytes."""
-    n = in_off.numel()
+    n = _units(in_off, in_len, out_off, out_cap, out_len, consumed, status)
     _raise(lib().capnp_packed_read_message_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
                                                  _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(consumed),
                                                  _ptr(status), _stream(stream)), "read_message_batch")
