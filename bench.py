@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory leg")
     ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
+    ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
     return ap.parse_args()
 
 
@@ -231,6 +232,61 @@ def host_path(args, dev, n_units=1 << 16):
     return res
 
 
+def pareto_sizes(n, seed=0xC0DE0005):
+    """unit size = 8 * floor(clamp(64 (1-u)^(-1/1.1), 64, 262144) / 8),
+    a truncated Pareto (alpha = 1.1, mean ~424 B); u from a seeded numpy generator."""
+    import numpy as np
+    u = np.random.default_rng(seed).random(n)
+    return (8 * np.floor(np.clip(64.0 * (1.0 - u) ** (-1.0 / 1.1), 64, 262144) / 8)).astype(np.int64)
+
+
+def skewed_leg(args, dev, n=1 << 20, reps=10):
+    """Config C5 (skewed sizes, p = 0.5): encode into capacity slots + decode from them,
+    device-resident, HIP events on the launch stream. Reported beside `value`."""
+    stream = torch.cuda.current_stream()
+    sizes = torch.from_numpy(pareto_sizes(n)).to(dev)
+    in_off = torch.zeros(n, dtype=torch.int64, device=dev)
+    in_off[1:] = torch.cumsum(sizes, 0)[:-1]
+    U = int(sizes.sum().item())
+    d_in = cp.generate(1, U, seed=0xC0DE0005, zero_thresh=args.zero_thresh, device=dev)
+    caps = (sizes // 8) * 10
+    slots = (caps + 15) // 16 * 16
+    pk_off = torch.zeros(n, dtype=torch.int64, device=dev)
+    pk_off[1:] = torch.cumsum(slots, 0)[:-1]
+    d_pk = torch.empty(int(slots.sum().item()), dtype=torch.uint8, device=dev)
+    plen = torch.zeros(n, dtype=torch.int64, device=dev)
+    pst = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_out = torch.empty(U, dtype=torch.uint8, device=dev)
+    ulen = torch.zeros(n, dtype=torch.int64, device=dev)
+    ust = torch.zeros(n, dtype=torch.int32, device=dev)
+    enc = lambda: cp.encode_batch(d_in, in_off, sizes, d_pk, pk_off, caps, plen, pst, stream=stream)  # noqa: E731
+    dec = lambda: cp.decode_batch(d_pk, pk_off, plen, d_out, in_off, sizes, ulen, ust, stream=stream)  # noqa: E731
+    enc()
+    dec()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    torch.cuda.synchronize()
+    t = [0.0, 0.0]
+    for _ in range(reps):
+        ev[0].record(stream)
+        enc()
+        ev[1].record(stream)
+        dec()
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        t[0] += ev[0].elapsed_time(ev[1])
+        t[1] += ev[1].elapsed_time(ev[2])
+    em, dm = t[0] / reps, t[1] / reps
+    ok = bool((pst == 0).all().item() and (ust == 0).all().item() and torch.equal(ulen, sizes)
+              and torch.equal(d_out, d_in))
+    big = sizes > 4096
+    return {"units": n, "unpacked_bytes": U, "units_over_4KiB": int(big.sum().item()),
+            "bytes_in_units_over_4KiB": int(sizes[big].sum().item()),
+            "encode_ms": round(em, 4), "decode_ms": round(dm, 4),
+            "GiB_s": round(U / ((em + dm) * 1e-3) / 2 ** 30, 2),
+            "packed_ratio": round(int(plen.sum().item()) / U, 4), "bit_exact_roundtrip": ok,
+            "note": "SURVEY config C5: truncated Pareto unit sizes 64 B..256 KiB, p = zero_thresh/256"}
+
+
 def read_message_leg(args, dev, reps=10):
     """SURVEY §8(f) row 1, Reader.readPackedMessage (reader.zig:84-156) batched: the
     same 1M x 4 KiB units made into framed messages (one segment of 511 words), packed
@@ -313,6 +369,9 @@ def main():
         del wl
         torch.cuda.empty_cache()
         extra["read_message"] = read_message_leg(args, dev)
+    if world == 1 and not args.no_skewed:
+        torch.cuda.empty_cache()
+        extra["c5_skewed"] = skewed_leg(args, dev)
 
     if rank == 0:
         steps = args.steps

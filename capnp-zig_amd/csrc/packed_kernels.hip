@@ -300,95 +300,88 @@ __device__ void serial_unpack(const uint8_t* p, uint64_t n, uint8_t* out) {
 // ---------------------------------------------------------------------------
 // ENCODE
 // ---------------------------------------------------------------------------
-template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint64_t* __restrict__ in_len,
-                                                        uint32_t n, uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        const uint64_t* __restrict__ out_cap,
-                                                        uint64_t* __restrict__ out_len,
-                                                        int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * (WRITE ? kEncLds : kEncLds)];
-    __shared__ uint64_t lut[256];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WRITE) {
-        lut[threadIdx.x] = compact_selector(threadIdx.x);
-        __syncthreads();
-    }
-    const uint32_t unit = blockIdx.x * kWavesPerBlock + wave;
-    if (unit >= n) return;
-    uint8_t* lds = smem + wave * kEncLds;
+// One wave encodes one 512-word (4 KiB) tile of a unit: encode_tile. A unit of at
+// most 512 words is a single tile (the headline path). Longer units are walked by
+// the same wave tile after tile (encode_kernel's tiled loop), with two carries:
+//   run starts (cz, cf): the start of the zero-class / literal-class run that is
+//     still open at the tile start, so a run continuing from earlier tiles keeps
+//     its 256-word head positions (message.zig:211-225 / 231-251);
+//   lookahead (nbz, nbf): the first Z / F break at or after the tile end (first
+//     non-zero word / first word with a zero byte), read from the next tile, so a
+//     head near the tile end gets its count min(256, run end - i) - 1; a break
+//     more than 256 words ahead cannot change a count, so 256 words suffice.
 
-    const uint64_t b0 = in_off[unit];
-    const uint64_t nbytes = in_len[unit];
-    uint64_t ob = 0, cap = 0;
-    int32_t st = ST_OK;
-    if (WRITE) {
-        ob = out_off[unit];
-        cap = out_cap[unit];
-    }
-    if (reinterpret_cast<uintptr_t>(in + b0) & 7) st = ST_ARG;
-    if (st == ST_OK && (nbytes & 7)) st = ST_SIZE;  // message.zig:201
-    if (st != ST_OK) {
-        if (lane == 0) { out_len[unit] = 0; status[unit] = st; }
-        return;
-    }
-    if (nbytes / 8 > kEncMaxWords) {
-        // serial fallback
-        if (lane == 0) {
-            uint64_t P = serial_pack(in + b0, nbytes / 8, nullptr);
-            int32_t s2 = ST_OK;
-            if (WRITE) {
-                if (P > cap) s2 = ST_SPACE;
-                else serial_pack(in + b0, nbytes / 8, out + ob);
-            }
-            out_len[unit] = P;
-            status[unit] = s2;
-        }
-        return;
-    }
-    const uint32_t words = (uint32_t)(nbytes >> 3);
-
-    // ---- stage the unit into LDS, word w at row (w>>3)*80 + (w&7)*8 ------------
-    {
-        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(in + b0) & 15);  // 0 or 8
-        const uint8_t* g = in + b0 - s;
-        const uint32_t nch = (s + (uint32_t)nbytes + 15) >> 4;
-        uint4 v[5];
+// Stage words [0, words) of src (8-aligned) into the row layout: word w at
+// lds[(w >> 3) * kEncRow + (w & 7) * 8].
+__device__ __forceinline__ void encode_stage(uint8_t* lds, const uint8_t* src, uint32_t words, uint32_t lane) {
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);  // 0 or 8
+    const uint8_t* g = src - s;
+    const uint32_t nch = (s + 8 * words + 15) >> 4;
+    uint4 v[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            if ((uint32_t)(64 * k) < nch) {
-                uint32_t c = min(lane + 64u * k, nch - 1);
-                v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
-            }
+    for (int k = 0; k < 5; ++k) {
+        if ((uint32_t)(64 * k) < nch) {
+            uint32_t c = min(lane + 64u * k, nch - 1);
+            v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);
         }
+    }
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            uint32_t c = lane + 64 * k;
-            if ((uint32_t)(64 * k) < nch && c < nch) {
-                if (s == 0) {
-                    uint32_t w = 2 * c;
-                    *reinterpret_cast<uint4*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = v[k];
-                } else {
-                    uint64_t lo = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
-                    uint64_t hi = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
-                    if (c > 0) {
-                        uint32_t w = 2 * c - 1;
-                        *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = lo;
-                    }
-                    uint32_t w = 2 * c;
-                    if (w < words) *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = hi;
+    for (int k = 0; k < 5; ++k) {
+        uint32_t c = lane + 64 * k;
+        if ((uint32_t)(64 * k) < nch && c < nch) {
+            if (s == 0) {
+                uint32_t w = 2 * c;
+                *reinterpret_cast<uint4*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = v[k];
+            } else {
+                uint64_t lo = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+                uint64_t hi = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+                if (c > 0) {
+                    uint32_t w = 2 * c - 1;
+                    *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = lo;
                 }
+                uint32_t w = 2 * c;
+                if (w < words) *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = hi;
             }
         }
     }
-    wave_lds_sync();
+}
 
-    // ---- lane j owns words [8j, 8j+8) ------------------------------------------
-    const uint32_t base = lane * 8;
-    const uint32_t nw = base < words ? min(8u, words - base) : 0u;
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, kWave));
+    return v;
+}
+
+// First Z break and first F break among words [0, nw) of src, nw <= 256, as
+// offsets (nw when there is none); wave-uniform results.
+__device__ __forceinline__ void encode_lookahead(const uint8_t* src, uint32_t nw, uint32_t lane, uint32_t& bz,
+                                                 uint32_t& bf) {
+    uint32_t fz = nw, ff = nw;
+#pragma unroll
+    for (int t = 3; t >= 0; --t) {
+        const uint32_t i = 4 * lane + t;
+        if (i < nw) {
+            const uint32_t tg = nonzero_tag(*reinterpret_cast<const uint64_t*>(src + 8 * i));
+            if (tg != 0) fz = i;
+            if (tg != 0xFF) ff = i;
+        }
+    }
+    bz = wave_min(fz);
+    bf = wave_min(ff);
+}
+
+// Encode one staged tile: words [tb, tb + words) of the unit (absolute word
+// indices; tb = 0 for a single tile). SINGLE: the whole unit (no carries; run
+// crossings are tested per lane boundary). Returns the tile's packed size; writes
+// the packed bytes to dst when WRITE and they fit in `room`.
+template <bool WRITE, bool SINGLE>
+__device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lut, uint32_t lane, uint32_t words,
+                                                uint32_t tb, uint32_t& cz_c, uint32_t& cf_c, uint32_t nbz,
+                                                uint32_t nbf, uint8_t* dst, uint64_t room) {
+    const uint32_t wend = tb + words;  // absolute end of the tile
+    // ---- lane j owns words [tb + 8j, tb + 8j + 8) --------------------------------
+    const uint32_t base = tb + lane * 8;
+    const uint32_t nw = lane * 8 < words ? min(8u, words - lane * 8) : 0u;
     uint64_t w[8];
     if (nw) {
         const uint4* row = reinterpret_cast<const uint4*>(lds + lane * kEncRow);
@@ -413,32 +406,41 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
             if (tag[t] == 0xFF) fmask |= 1u << t;
         }
     }
-    // break positions for the zero-run (Z) and literal-run (F) classes
-    uint32_t lbz = 0, lbf = 0, fbz = words, fbf = words;
+    // break positions for the zero-run (Z) and literal-run (F) classes: last break + 1
+    // (seeded with the carried run start) and first break (seeded with the lookahead)
+    uint32_t lbz = cz_c, lbf = cf_c, fbz = nbz, fbf = nbf;
 #pragma unroll
     for (int t = 7; t >= 0; --t) {
         uint32_t i = base + t;
-        if (!((zmask >> t) & 1u)) { lbz = max(lbz, i + 1); fbz = i; }
-        if (!((fmask >> t) & 1u)) { lbf = max(lbf, i + 1); fbf = i; }
+        if ((uint32_t)t < nw) {
+            if (!((zmask >> t) & 1u)) { lbz = max(lbz, i + 1); fbz = i; }
+            if (!((fmask >> t) & 1u)) { lbf = max(lbf, i + 1); fbf = i; }
+        }
     }
-    fbz = min(fbz, words);
-    fbf = min(fbf, words);
     // run start carried into this lane = last break before it (+1); run end = first break after it.
-    // When no zero run and no literal run crosses a lane boundary (the common case
-    // away from very sparse or very dense data) the carries are the lane's own
-    // bounds and the four wave scans are skipped.
-    const uint64_t bz0 = __ballot(zmask & 1u), bz7 = __ballot((zmask >> 7) & 1u);
-    const uint64_t bf0 = __ballot(fmask & 1u), bf7 = __ballot((fmask >> 7) & 1u);
-    uint32_t cz = base, cf = base, ez = min(base + 8, words), ef = ez;
-    if ((bz0 & (bz7 << 1)) | (bf0 & (bf7 << 1))) {
+    // In a single tile where no zero run and no literal run crosses a lane boundary (the
+    // common case away from very sparse or very dense data) the carries are the lane's
+    // own bounds and the four wave scans are skipped.
+    uint32_t cz = base, cf = base, ez = min(base + 8, wend), ef = ez;
+    bool scan = true;
+    if (SINGLE) {
+        const uint64_t bz0 = __ballot(zmask & 1u), bz7 = __ballot((zmask >> 7) & 1u);
+        const uint64_t bf0 = __ballot(fmask & 1u), bf7 = __ballot((fmask >> 7) & 1u);
+        scan = ((bz0 & (bz7 << 1)) | (bf0 & (bf7 << 1))) != 0;
+    }
+    if (scan) {
         cz = __shfl_up(wave_incl_max(lbz, lane), 1, kWave);
         cf = __shfl_up(wave_incl_max(lbf, lane), 1, kWave);
         ez = __shfl_down(wave_incl_suffix_min(fbz, lane), 1, kWave);
         ef = __shfl_down(wave_incl_suffix_min(fbf, lane), 1, kWave);
-        if (lane == 0) { cz = 0; cf = 0; }
-        if (lane == 63) { ez = words; ef = words; }
-        ez = min(ez, words);
-        ef = min(ef, words);
+        if (lane == 0) { cz = cz_c; cf = cf_c; }
+        if (lane == 63) { ez = nbz; ef = nbf; }
+    }
+    // carries for the next tile: the run starts open at the tile end
+    uint32_t lz_all = 0, lf_all = 0;
+    if (!SINGLE) {
+        lz_all = readlane(wave_incl_max(lbz, lane), 63);
+        lf_all = readlane(wave_incl_max(lbf, lane), 63);
     }
 
     uint32_t rs[8];  // run start of word t's class run (Z or F)
@@ -454,8 +456,10 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     for (int t = 7; t >= 0; --t) {
         uint32_t i = base + t;
         re[t] = ((zmask >> t) & 1u) ? ez : ef;
-        if (!((zmask >> t) & 1u)) ez = i;
-        if (!((fmask >> t) & 1u)) ef = i;
+        if ((uint32_t)t < nw) {
+            if (!((zmask >> t) & 1u)) ez = i;
+            if (!((fmask >> t) & 1u)) ef = i;
+        }
     }
     uint32_t sz[8], cnt[8];
     uint32_t total = 0;
@@ -475,18 +479,12 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     const uint32_t incl = wave_incl_sum(total, lane);
     const uint32_t P = readlane(incl, 63);
     const uint32_t o = incl - total;
-
-    if (!WRITE) {
-        if (lane == 0) { out_len[unit] = P; status[unit] = ST_OK; }
-        return;
-    }
-    if ((uint64_t)P > cap) {
-        if (lane == 0) { out_len[unit] = P; status[unit] = ST_SPACE; }
-        return;
-    }
+    cz_c = lz_all;
+    cf_c = lf_all;
+    if (!WRITE || (uint64_t)P > room) return P;
 
     // ---- assemble the packed bytes in LDS (reusing the staging slice) -------------
-    const uint32_t so = (uint32_t)(reinterpret_cast<uintptr_t>(out + ob) & 15);
+    const uint32_t so = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
     const uint32_t nch_out = (so + P + 15) >> 4;
     wave_lds_sync();  // every lane has its words in registers
 #pragma unroll
@@ -526,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
 
     // ---- coalesced write-back ------------------------------------------------------
     {
-        uint8_t* gdst = out + ob - so;  // 16-B aligned
+        uint8_t* gdst = dst - so;  // 16-B aligned
         const uint32_t lo = so, hi = so + P;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -542,7 +540,139 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
             }
         }
     }
-    if (lane == 0) { out_len[unit] = P; status[unit] = ST_OK; }
+    return P;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint64_t* __restrict__ in_len,
+                                                        uint32_t n, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint64_t* __restrict__ out_cap,
+                                                        uint64_t* __restrict__ out_len,
+                                                        int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    const uint32_t unit = blockIdx.x * kWavesPerBlock + wave;
+    if (unit >= n) return;
+    uint8_t* lds = smem + wave * kEncLds;
+
+    const uint64_t b0 = in_off[unit];
+    const uint64_t nbytes = in_len[unit];
+    uint64_t ob = 0, cap = 0;
+    int32_t st = ST_OK;
+    if (WRITE) {
+        ob = out_off[unit];
+        cap = out_cap[unit];
+    }
+    if (reinterpret_cast<uintptr_t>(in + b0) & 7) st = ST_ARG;
+    if (st == ST_OK && (nbytes & 7)) st = ST_SIZE;  // message.zig:201
+    if (st != ST_OK) {
+        if (lane == 0) { out_len[unit] = 0; status[unit] = st; }
+        return;
+    }
+    const uint8_t* const src = in + b0;
+    if (nbytes / 8 > 0xFFFFF000ull) {  // absolute word indices are u32: serial path (> 32 GiB units)
+        if (lane == 0) {
+            uint64_t P = serial_pack(src, nbytes / 8, nullptr);
+            int32_t s2 = ST_OK;
+            if (WRITE) {
+                if (P > cap) s2 = ST_SPACE;
+                else serial_pack(src, nbytes / 8, out + ob);
+            }
+            out_len[unit] = P;
+            status[unit] = s2;
+        }
+        return;
+    }
+    const uint32_t words = (uint32_t)(nbytes >> 3);
+    if (words <= kEncMaxWords) {  // one tile (the headline 4-KiB units)
+        encode_stage(lds, src, words, lane);
+        wave_lds_sync();
+        uint32_t cz = 0, cf = 0;
+        const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        if (lane == 0) {
+            out_len[unit] = P;
+            status[unit] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
+        }
+        return;
+    }
+    // longer units: encode_tiled_kernel (a separate kernel keeps this one at its
+    // register budget)
+    if (lane == 0) status[unit] = kStNeedFull;
+}
+
+// Units longer than one tile, marked kStNeedFull by encode_kernel. A small grid
+// strides over the batch; each wave tests 64 statuses per load and encodes the
+// marked units one after another, tile by tile.
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __restrict__ in,
+                                                              const uint64_t* __restrict__ in_off,
+                                                              const uint64_t* __restrict__ in_len,
+                                                              uint32_t n, uint8_t* __restrict__ out,
+                                                              const uint64_t* __restrict__ out_off,
+                                                              const uint64_t* __restrict__ out_cap,
+                                                              uint64_t* __restrict__ out_len,
+                                                              int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    uint8_t* lds = smem + wave * kEncLds;
+    const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;
+    for (uint32_t ubase = (blockIdx.x * kWavesPerBlock + wave) * kWave; ubase < n; ubase += stride) {
+    const uint32_t u = ubase + lane;
+    uint64_t todo = __ballot(u < n && status[u] == kStNeedFull);
+    while (todo) {  // wave-uniform
+    const uint32_t unit = ubase + (uint32_t)__builtin_ctzll(todo);
+    todo &= todo - 1;
+    const uint8_t* const src = in + in_off[unit];
+    const uint32_t words = (uint32_t)(in_len[unit] >> 3);
+    uint64_t ob = 0, cap = 0;
+    if (WRITE) {
+        ob = out_off[unit];
+        cap = out_cap[unit];
+    }
+    uint32_t cz = 0, cf = 0;
+    uint64_t pos = 0;   // packed bytes so far
+    bool fits = true;   // every tile so far was written (WRITE)
+    for (uint32_t tb = 0; tb < words; tb += kEncMaxWords) {
+        const uint32_t tw = min(kEncMaxWords, words - tb);
+        const uint32_t te = tb + tw;
+        uint32_t nbz = words, nbf = words;
+        if (te < words) {
+            const uint32_t la = min(256u, words - te);
+            uint32_t bz, bf;
+            encode_lookahead(src + 8ull * te, la, lane, bz, bf);
+            nbz = bz < la ? te + bz : (la == 256u ? te + 256u : words);
+            nbf = bf < la ? te + bf : (la == 256u ? te + 256u : words);
+        }
+        wave_lds_sync();  // the previous tile's write-back read the slice
+        encode_stage(lds, src + 8ull * tb, tw, lane);
+        wave_lds_sync();
+        const uint64_t room = (WRITE && fits && pos <= cap) ? cap - pos : 0;
+        const uint32_t Pt = encode_tile<WRITE, false>(lds, lut, lane, tw, tb, cz, cf, nbz, nbf, out + ob + pos,
+                                                      room);
+        if ((uint64_t)Pt > room) fits = false;
+        pos += Pt;
+    }
+    if (lane == 0) {
+        out_len[unit] = pos;
+        status[unit] = (WRITE && !fits) ? ST_SPACE : ST_OK;
+    }
+    }  // marked units
+    }  // unit groups
 }
 
 // ---------------------------------------------------------------------------
@@ -2172,12 +2302,20 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (write)
+    // units of more than 512 words: encode_tiled_kernel over a grid that strides the batch
+    const uint32_t groups = (n + kWave - 1) / kWave;
+    const uint32_t tiled_blocks = min((groups + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    if (write) {
         encode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status);
-    else
+        encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                        out_cap, out_len, status);
+    } else {
         encode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status);
+        encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                         out_cap, out_len, status);
+    }
     return hipGetLastError();
 }
 

@@ -1,0 +1,164 @@
+"""GPU parity on SURVEY §8(d)'s configs C1 and C5 (C2-C4 shapes are in
+test_gpu_parity.py / test_sharding.py).
+
+C1: the reference's CPU bench shape made concrete as SURVEY asks: one framed message
+    of 64 segments x 1 KiB (p = 0.5) behind a valid segment table, packed through the
+    single-buffer C-ABI (MessageBuilder.toPackedBytes, message.zig:2175-2179) and read
+    back (Message.initPacked, message.zig:400-408), bit-exact against the oracle.
+C5: skewed unit sizes (truncated Pareto, alpha = 1.1, 64 B .. 256 KiB) in one batch,
+    including units far beyond the 4-KiB fast-path tile, every unit against the oracle.
+"""
+import numpy as np
+import pytest
+
+import capnp_packed as cp
+import oracle
+import pyref
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def c1_segments(seed=0xC0DE0001):
+    data = oracle.generate(64, 1024, seed=seed, zero_thresh=128)
+    return [data[i * 1024:(i + 1) * 1024].tobytes() for i in range(64)]
+
+
+def test_c1_64_segment_message_single_buffer():
+    segs = c1_segments()
+    b = cp.MessageBuilder()
+    for s in segs:
+        b.create_segment(s)
+    framed = b.to_bytes()
+    assert framed == pyref.frame(segs) and len(framed) == 8 * 33 + 64 * 1024
+    packed = b.to_packed_bytes()
+    st, exp = oracle.pack(framed)
+    assert st == oracle.OK and packed == exp
+    msg = cp.Message.init_packed(packed)
+    assert [bytes(s) for s in msg.segments] == segs and msg.backing_data == framed
+    assert cp.Reader.read_packed_message(packed + b"\x00") == framed
+
+
+def test_c1_batch_of_messages():
+    """64 C1 messages (different seeds) through the batch entry points."""
+    msgs = [pyref.frame(c1_segments(0xC0DE0100 + k)) for k in range(64)]
+    ub = len(msgs[0])
+    d_in = torch.from_numpy(np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()).to(DEV)
+    n = len(msgs)
+    in_off, in_len = cp.uniform_layout(n, ub)
+    slot = (cp.encode_bound(ub) + 15) // 16 * 16
+    pk_off, pk_cap = cp.uniform_layout(n, slot)
+    d_pk = torch.zeros(n * slot, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_batch(d_in, in_off, in_len, d_pk, pk_off, pk_cap, plen, pst)
+    d_out = torch.zeros(n * ub, dtype=torch.uint8, device=DEV)
+    ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.decode_batch(d_pk, pk_off, plen, d_out, in_off, in_len, ulen, ust)
+    torch.cuda.synchronize()
+    pk, lens = d_pk.cpu().numpy(), plen.cpu().numpy()
+    for k, m in enumerate(msgs):
+        st, exp = oracle.pack(m)
+        assert pk[k * slot:k * slot + lens[k]].tobytes() == exp, f"message {k}"
+    assert (pst.cpu() == 0).all() and (ust.cpu() == 0).all() and torch.equal(d_out, d_in)
+
+
+def pareto_sizes(n, seed):
+    u = np.random.default_rng(seed).random(n)
+    return (8 * np.floor(np.clip(64.0 * (1.0 - u) ** (-1.0 / 1.1), 64, 262144) / 8)).astype(np.int64)
+
+
+@pytest.mark.parametrize("thr", [26, 128, 230])
+def test_c5_skewed_sizes_every_unit(thr):
+    sizes = pareto_sizes(3000, seed=0xC0DE0005 + thr)
+    # units around and far beyond the 512-word tile, and both size extremes
+    extra = [4088, 4096, 4104, 8192, 12288 + 8, 65536, 262144, 64, 8]
+    sizes = np.concatenate([sizes, np.array(extra, dtype=np.int64)])
+    n = len(sizes)
+    off = np.zeros(n + 1, dtype=np.int64)
+    off[1:] = np.cumsum(sizes)
+    U = int(off[-1])
+    host = oracle.generate(1, U, seed=0xC0DE0005, zero_thresh=thr)
+    # long zero and literal runs across tile boundaries in the big units
+    big = np.nonzero(sizes >= 8192)[0]
+    for j, i in enumerate(big):
+        a = int(off[i])
+        host[a + 4000:a + 4000 + 3000] = 0 if j % 2 else 0x5A
+    d_in = torch.from_numpy(host).to(DEV)
+    t_off = torch.from_numpy(off[:-1].copy()).to(DEV)
+    t_len = torch.from_numpy(sizes).to(DEV)
+    caps = (sizes // 8) * 10
+    slots = (caps + 15) // 16 * 16
+    poff = np.zeros(n, dtype=np.int64)
+    poff[1:] = np.cumsum(slots)[:-1]
+    d_pk = torch.zeros(int(slots.sum()) + 16, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    t_poff = torch.from_numpy(poff).to(DEV)
+    cp.encode_batch(d_in, t_off, t_len, d_pk, t_poff, torch.from_numpy(caps).to(DEV), plen, pst)
+    d_out = torch.zeros(U + 16, dtype=torch.uint8, device=DEV)
+    ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.decode_batch(d_pk, t_poff, plen, d_out, t_off, t_len, ulen, ust)
+    torch.cuda.synchronize()
+    pk, lens, sts = d_pk.cpu().numpy(), plen.cpu().numpy(), pst.cpu().numpy()
+    for i in range(n):
+        st, exp = oracle.pack(host[off[i]:off[i + 1]].tobytes())
+        assert sts[i] == cp.OK and pk[poff[i]:poff[i] + lens[i]].tobytes() == exp, f"unit {i} ({sizes[i]} B)"
+    assert (ust.cpu() == 0).all() and torch.equal(ulen, t_len)
+    assert np.array_equal(d_out.cpu().numpy()[:U], host)
+
+
+def _encode_units(units):
+    offs, pos = [], 0
+    for u in units:
+        offs.append(pos)
+        pos += len(u)
+    host = np.zeros(pos + 16, dtype=np.uint8)
+    for o, u in zip(offs, units):
+        host[o:o + len(u)] = np.frombuffer(u, dtype=np.uint8)
+    n = len(units)
+    caps = [10 * (len(u) // 8) for u in units]
+    poffs, q = [], 0
+    for c in caps:
+        poffs.append(q)
+        q += (c + 15) // 16 * 16
+    t = lambda xs: torch.tensor(xs, dtype=torch.int64, device=DEV)  # noqa: E731
+    d_out = torch.zeros(q + 16, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_batch(torch.from_numpy(host).to(DEV), t(offs), t([len(u) for u in units]), d_out, t(poffs), t(caps),
+                    plen, pst)
+    sz = torch.zeros(n, dtype=torch.int64, device=DEV)
+    sst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encoded_size_batch(torch.from_numpy(host).to(DEV), t(offs), t([len(u) for u in units]), sz, sst)
+    torch.cuda.synchronize()
+    h, lens = d_out.cpu().numpy(), plen.cpu().numpy()
+    assert (pst.cpu() == 0).all() and (sst.cpu() == 0).all() and torch.equal(sz, plen)
+    return [h[poffs[i]:poffs[i] + lens[i]].tobytes() for i in range(n)]
+
+
+def test_tiled_encode_run_carries():
+    """Units past the 512-word tile: zero and literal runs that start before a tile
+    boundary and end after it (heads at 256-word steps from the run start), runs
+    ending exactly at a tile end, and breaks just past the 256-word lookahead."""
+    rng = np.random.default_rng(5)
+    lit = lambda k: rng.integers(1, 256, 8 * k, dtype=np.uint8).tobytes()  # noqa: E731
+    mixed = lambda k: bytes(rng.integers(0, 256, 8 * k, dtype=np.uint8) * (rng.random(8 * k) < 0.5))  # noqa: E731
+    units = []
+    for kind in (lambda k: bytes(8 * k), lit):
+        for start in (1, 255, 256, 300, 400, 511, 512):
+            for length in (1, 255, 256, 257, 600, 1023, 1500):
+                units.append(mixed(start) + kind(length) + mixed(64))
+        units.append(kind(2048))
+        units.append(kind(512) + mixed(1))
+        units.append(mixed(511) + kind(1) + mixed(600))
+    units.append(bytes(8 * 513))
+    units.append(lit(513))
+    units.append(mixed(8 * 1024))
+    got = _encode_units(units)
+    for i, u in enumerate(units):
+        st, exp = oracle.pack(u)
+        assert got[i] == exp, f"unit {i} ({len(u) // 8} words)"
