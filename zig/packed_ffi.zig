@@ -6,6 +6,8 @@
 //!   packPacked            message.zig:200-271
 //!   unpackPacked          message.zig:88-145
 //!   estimateUnpackedSize  message.zig:152-191
+//! and `readPackedMessageBuffered` serves Reader.readPackedMessage (reader.zig:84-156)
+//! for readers whose bytes are already buffered (a socket framer's read buffer).
 //! Allocation follows the reference's contract: the returned slice is
 //! allocator-owned with its exact length (the reference returns
 //! `out.toOwnedSlice`, message.zig:144/270), so callers free it unchanged.
@@ -23,6 +25,11 @@ pub const Status = enum(c_int) {
     invalid_argument = 5,
     device_error = 6,
     no_device = 7,
+    end_of_stream = 8,
+    invalid_segment_count = 9,
+    segment_count_limit_exceeded = 10,
+    message_too_large = 11,
+    invalid_packed_message = 12,
     _,
 };
 
@@ -33,6 +40,7 @@ extern "capnp_packed" fn capnp_packed_encode_bound(n: usize) usize;
 extern "capnp_packed" fn capnp_packed_encode(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize) c_int;
 extern "capnp_packed" fn capnp_packed_decoded_size(in: [*]const u8, n: usize, out_size: *usize) c_int;
 extern "capnp_packed" fn capnp_packed_decode(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize) c_int;
+extern "capnp_packed" fn capnp_packed_read_message(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize, consumed: *usize) c_int;
 
 // ---- device batch entry points (pointers are device memory) ----------------
 pub extern "capnp_packed" fn capnp_packed_encode_batch(
@@ -53,6 +61,11 @@ pub extern "capnp_packed" fn capnp_packed_decoded_size_batch(
     d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
     d_out_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
 ) c_int;
+pub extern "capnp_packed" fn capnp_packed_read_message_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
+    d_out_len: [*]u64, d_consumed: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
 pub extern "capnp_packed" fn capnp_packed_scan_scratch_bytes(n: u32) usize;
 pub extern "capnp_packed" fn capnp_packed_lengths_to_offsets(
     d_len: [*]const u64, n: u32, base: u64, d_off: [*]u64,
@@ -68,6 +81,12 @@ pub const Error = error{
     OutOfMemory,
     PackedDeviceError,
     NoDevice,
+    // Reader.readPackedMessage (reader.zig:84-156)
+    EndOfStream,
+    InvalidSegmentCount,
+    SegmentCountLimitExceeded,
+    MessageTooLarge,
+    InvalidPackedMessage,
 };
 
 fn check(status: c_int) Error!void {
@@ -78,6 +97,11 @@ fn check(status: c_int) Error!void {
         .overflow => error.Overflow,
         .out_of_space => error.OutOfMemory, // capacity is sized by us; unreachable in practice
         .no_device => error.NoDevice,
+        .end_of_stream => error.EndOfStream,
+        .invalid_segment_count => error.InvalidSegmentCount,
+        .segment_count_limit_exceeded => error.SegmentCountLimitExceeded,
+        .message_too_large => error.MessageTooLarge,
+        .invalid_packed_message => error.InvalidPackedMessage,
         else => {
             std.log.err("capnp_packed: {s}", .{capnp_packed_last_error()});
             return error.PackedDeviceError;
@@ -112,6 +136,33 @@ pub fn unpackPacked(allocator: std.mem.Allocator, packed_bytes: []const u8) Erro
     try check(capnp_packed_decode(packed_bytes.ptr, packed_bytes.len, out.ptr, out.len, &len));
     std.debug.assert(len == total);
     return out;
+}
+
+pub const ReadResult = struct { framed: []u8, consumed: usize };
+
+/// reader.zig:84 `readPackedMessage(allocator, reader) ![]const u8` over bytes the
+/// caller has already buffered: decodes the message at the front of `buffered`,
+/// returns its framed bytes (allocator-owned, exact length) and the packed bytes it
+/// took; the caller advances its buffer by `consumed`. EndOfStream means the buffer
+/// holds only part of the message (read more and call again).
+pub fn readPackedMessageBuffered(allocator: std.mem.Allocator, buffered: []const u8) Error!ReadResult {
+    var cap: usize = @max(4096, 8 * buffered.len);
+    while (true) {
+        const buf = try allocator.alloc(u8, cap);
+        var len: usize = 0;
+        var used: usize = 0;
+        const st = capnp_packed_read_message(buffered.ptr, buffered.len, buf.ptr, buf.len, &len, &used);
+        if (st == @intFromEnum(Status.out_of_space) and len > cap) {
+            allocator.free(buf); // a zero-run heavy message: retry with its framed length
+            cap = len;
+            continue;
+        }
+        check(st) catch |err| {
+            allocator.free(buf);
+            return err;
+        };
+        return .{ .framed = try allocator.realloc(buf, len), .consumed = used };
+    }
 }
 
 pub fn abiVersion() u32 {
