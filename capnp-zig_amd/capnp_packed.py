@@ -44,6 +44,8 @@ INVALID_SEGMENT_COUNT = 9
 SEGMENT_COUNT_LIMIT_EXCEEDED = 10
 MESSAGE_TOO_LARGE = 11
 INVALID_PACKED_MESSAGE = 12
+# Message.init (message.zig:341-394)
+TRUNCATED_MESSAGE = 13
 
 
 class PackedError(Exception):
@@ -99,13 +101,14 @@ class InvalidPackedMessage(PackedError):  # reader.zig:151-153
     status = INVALID_PACKED_MESSAGE
 
 
-class TruncatedMessage(Exception):
-    pass
+class TruncatedMessage(PackedError):  # message.zig:353/380
+    status = TRUNCATED_MESSAGE
 
 
 _ERRORS = {c.status: c for c in (InvalidMessageSize, UnexpectedEof, Overflow, OutOfSpace,
                                  InvalidArgument, DeviceError, NoDevice, EndOfStream, InvalidSegmentCount,
-                                 SegmentCountLimitExceeded, MessageTooLarge, InvalidPackedMessage)}
+                                 SegmentCountLimitExceeded, MessageTooLarge, InvalidPackedMessage,
+                                 TruncatedMessage)}
 
 
 _lib = None
@@ -128,6 +131,10 @@ SIGNATURES = {
     "capnp_packed_read_message_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
                                                        _vp, _vp]),
     "capnp_packed_read_message": (ctypes.c_int, [_vp, _sz, _vp, _sz, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    "capnp_packed_encode_message_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp,
+                                                         _vp, _vp]),
+    "capnp_packed_message_init_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp,
+                                                       _vp, _vp, _vp]),
     "capnp_packed_scan_scratch_bytes": (_sz, [ctypes.c_uint32]),
     "capnp_packed_lengths_to_offsets": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp,
                                                        _sz, _vp]),
@@ -416,6 +423,31 @@ def read_message_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, c
     _raise(lib().capnp_packed_read_message_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
                                                  _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(consumed),
                                                  _ptr(status), _stream(stream)), "read_message_batch")
+
+
+def encode_message_batch(seg_ptr, seg_len, seg_first, seg_count, d_out, out_off, out_cap, out_len, status,
+                         stream=None) -> None:
+    """MessageBuilder.toPackedBytes (message.zig:2123-2179) for a batch of messages,
+    packed straight from their segments. seg_ptr / seg_len: int64 tensors of segment
+    device addresses and byte lengths; seg_first / seg_count: int32 tensors, one
+    entry per message. d_out None = packed sizes only."""
+    n = _units(seg_first, seg_count, out_len, status)
+    if d_out is not None:
+        _units(seg_first, out_off, out_cap)
+    _raise(lib().capnp_packed_encode_message_batch(_ptr(seg_ptr), _ptr(seg_len), _ptr(seg_first), _ptr(seg_count),
+                                                   n, _ptr(d_out), _ptr(out_off), _ptr(out_cap), _ptr(out_len),
+                                                   _ptr(status), _stream(stream)), "encode_message_batch")
+
+
+def message_init_batch(d_in, in_off, in_len, max_segs, seg_count, seg_off, seg_len, status, stream=None) -> None:
+    """Message.init (message.zig:341-394) segment tables of a batch of framed messages:
+    seg_count[i] (int32), seg_off / seg_len rows of max_segs entries (int64)."""
+    n = _units(in_off, in_len, seg_count, status)
+    if max_segs and (seg_off.numel() < n * max_segs or seg_len.numel() < n * max_segs):
+        raise InvalidArgument("segment tables need n * max_segs entries")
+    _raise(lib().capnp_packed_message_init_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, max_segs,
+                                                 _ptr(seg_count), _ptr(seg_off), _ptr(seg_len), _ptr(status),
+                                                 _stream(stream)), "message_init_batch")
 
 
 def lengths_to_offsets(lengths, base: int = 0, out=None, stream=None):

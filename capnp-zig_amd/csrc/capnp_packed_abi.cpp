@@ -167,6 +167,7 @@ const char* capnp_packed_status_name(int status) {
         case CAPNP_PACKED_SEGMENT_COUNT_LIMIT_EXCEEDED: return "SegmentCountLimitExceeded";
         case CAPNP_PACKED_MESSAGE_TOO_LARGE: return "MessageTooLarge";
         case CAPNP_PACKED_INVALID_PACKED_MESSAGE: return "InvalidPackedMessage";
+        case CAPNP_PACKED_TRUNCATED_MESSAGE: return "TruncatedMessage";
         default: return "Unknown";
     }
 }
@@ -287,6 +288,35 @@ int capnp_packed_read_message(const uint8_t* in, size_t n, uint8_t* out, size_t 
     *out_len = (size_t)len;
     *consumed = (size_t)used;
     return st;
+}
+
+int capnp_packed_encode_message_batch(const uint64_t* d_seg_ptr, const uint64_t* d_seg_len,
+                                      const uint32_t* d_seg_first, const uint32_t* d_seg_count, uint32_t n,
+                                      uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                                      uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    if (n == 0) return CAPNP_PACKED_OK;
+    if (!d_seg_first || !d_seg_count || !d_out_len || !d_status)
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null batch pointer");
+    const bool write = d_out != nullptr;
+    if (write && (!d_out_off || !d_out_cap)) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
+    int st = ensure_device();
+    if (st) return st;
+    hipError_t e = cpk::launch_encode_message(d_seg_ptr, d_seg_len, d_seg_first, d_seg_count, n, d_out, d_out_off,
+                                              d_out_cap, d_out_len, d_status, write, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "encode-message launch");
+}
+
+int capnp_packed_message_init_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint32_t max_segs, uint32_t* d_seg_count, uint64_t* d_seg_off,
+                                    uint64_t* d_seg_len, int32_t* d_status, void* stream) {
+    if (n == 0) return CAPNP_PACKED_OK;
+    if (!d_in_off || !d_in_len || !d_seg_count || !d_status || (max_segs && (!d_seg_off || !d_seg_len)))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null batch pointer");
+    int st = ensure_device();
+    if (st) return st;
+    hipError_t e = cpk::launch_message_init(d_in, d_in_off, d_in_len, n, max_segs, d_seg_count, d_seg_off, d_seg_len,
+                                            d_status, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "message-init launch");
 }
 
 size_t capnp_packed_scan_scratch_bytes(uint32_t n) { return cpk::scan_scratch_bytes(n); }

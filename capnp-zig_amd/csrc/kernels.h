@@ -20,6 +20,17 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                                uint64_t* consumed, int32_t* status, hipStream_t stream);
 
+// MessageBuilder.toPackedBytes from segment lists (message.zig:2123-2179).
+hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_len, const uint32_t* seg_first,
+                                 const uint32_t* seg_count, uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                 const uint64_t* out_cap, uint64_t* out_len, int32_t* status, bool write,
+                                 hipStream_t stream);
+
+// Message.init segment-table parse (message.zig:341-394).
+hipError_t launch_message_init(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                               uint32_t max_segs, uint32_t* seg_count, uint64_t* seg_off, uint64_t* seg_len,
+                               int32_t* status, hipStream_t stream);
+
 hipError_t launch_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
                            uint64_t seed, uint32_t thr, hipStream_t stream);
 

@@ -58,6 +58,7 @@ enum : int32_t {
     ST_SEGLIMIT = CAPNP_PACKED_SEGMENT_COUNT_LIMIT_EXCEEDED,
     ST_TOOLARGE = CAPNP_PACKED_MESSAGE_TOO_LARGE,
     ST_OVERSHOOT = CAPNP_PACKED_INVALID_PACKED_MESSAGE,
+    ST_TRUNC = CAPNP_PACKED_TRUNCATED_MESSAGE,  // Message.init (message.zig:353/380)
 };
 // internal status between decode passes: the unit goes to a full (fallback) decoder
 constexpr int32_t kStNeedFull = 0x7FFF0001;
@@ -673,6 +674,227 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
     }
     }  // marked units
     }  // unit groups
+}
+
+// ---------------------------------------------------------------------------
+// ENCODE straight from segment lists: MessageBuilder.toPackedBytes
+// (message.zig:2175-2179 = packPacked(toBytes()), toBytes 2123-2170) without the
+// framed copy. One wave per message walks the VIRTUAL framed stream
+//   [segment count - 1, size_0 .. size_{c-1}, pad] ++ segment_0 ++ .. ++ segment_{c-1}
+// tile by tile through encode_tile (the same carries as encode_tiled_kernel); each
+// lane gathers its 8 words of a tile from the header or from the segment that
+// holds them (word offsets of the segments in LDS).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig:310)
+
+struct MsgView {
+    const uint32_t* woff;   // LDS: word offset of segment s in the payload, s <= count
+    const uint64_t* base;   // LDS: device address of segment s
+    uint32_t count;         // segments (>= 1)
+    uint32_t hw;            // header words
+};
+
+// Word q of the framed stream (q < total words). `s` is a segment hint: the segment
+// holding the previous payload word (advanced forward, so a lane's consecutive words
+// cost one search).
+__device__ __forceinline__ uint64_t msg_word(const MsgView& m, uint32_t q, uint32_t& s) {
+    if (q < m.hw) {  // toBytes 2147-2163: u32 j = count - 1 (j = 0), size_{j-1} (1 <= j <= count), pad
+        uint32_t v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t j = 2 * q + h;
+            v[h] = j == 0 ? m.count - 1 : (j <= m.count ? m.woff[j] - m.woff[j - 1] : 0u);
+        }
+        return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+    }
+    const uint32_t p = q - m.hw;
+    if (s >= m.count || p < m.woff[s]) {  // (re)search: largest s with woff[s] <= p, non-empty
+        uint32_t lo = 0, hi = m.count;  // woff[lo] <= p < woff[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (m.woff[mid] <= p) lo = mid;
+            else hi = mid;
+        }
+        s = lo;
+    }
+    while (p >= m.woff[s + 1]) ++s;  // skip to the segment holding p (empty ones included)
+    return *reinterpret_cast<const uint64_t*>(m.base[s] + 8ull * (p - m.woff[s]));
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* __restrict__ seg_ptr,
+                                                                const uint64_t* __restrict__ seg_len,
+                                                                const uint32_t* __restrict__ seg_first,
+                                                                const uint32_t* __restrict__ seg_count, uint32_t n,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint64_t* __restrict__ out_len,
+                                                                int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint32_t woff_all[kWavesPerBlock * (kMsgMaxSegs + 1)];
+    __shared__ uint64_t base_all[kWavesPerBlock * kMsgMaxSegs];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    const uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
+    if (msg >= n) return;
+    uint8_t* const lds = smem + wave * kEncLds;
+    uint32_t* const woff = woff_all + wave * (kMsgMaxSegs + 1);
+    uint64_t* const base = base_all + wave * kMsgMaxSegs;
+
+    // ---- segment table: lane l takes segments 8l .. 8l+7 ------------------------------
+    const uint32_t c_in = seg_count[msg];
+    const uint32_t first = seg_first[msg];
+    const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
+    if (count > kMsgMaxSegs) {
+        if (lane == 0) { out_len[msg] = 0; status[msg] = ST_ARG; }
+        return;
+    }
+    uint32_t wsum = 0;
+    bool bad = false;
+    uint32_t wl[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const uint32_t s = 8 * lane + t;
+        wl[t] = 0;
+        if (s < count) {
+            uint64_t len = 0, ptr = 0;
+            if (c_in) {
+                len = seg_len[first + s];
+                ptr = seg_ptr[first + s];
+            }
+            // segments are whole words at 8-B aligned addresses (a MessageBuilder's always are)
+            bad |= (len & 7) != 0 || (ptr & 7) != 0 || (len >> 3) > 0xFFFFFFFFull;
+            wl[t] = (uint32_t)(len >> 3);
+            base[s] = ptr;
+            wsum += wl[t];
+        }
+    }
+    const uint32_t incl = wave_incl_sum(wsum, lane);
+    uint32_t acc = incl - wsum;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const uint32_t s = 8 * lane + t;
+        if (s < count) woff[s] = acc;
+        acc += wl[t];
+    }
+    const uint32_t payload = readlane(incl, 63);
+    if (lane == 63) woff[count] = payload;
+    const uint32_t hw = (1 + count + ((count & 1) ? 0 : 1)) / 2;  // toBytes 2135-2137, in words
+    const uint64_t words64 = (uint64_t)hw + payload;
+    if (__builtin_amdgcn_ballot_w64(bad) != 0 || words64 > 0xFFFFF000ull) {
+        if (lane == 0) { out_len[msg] = 0; status[msg] = ST_ARG; }
+        return;
+    }
+    wave_lds_sync();
+    const MsgView m{woff, base, count, hw};
+    const uint32_t words = (uint32_t)words64;
+    uint64_t ob = 0, cap = 0;
+    if (WRITE) {
+        ob = out_off[msg];
+        cap = out_cap[msg];
+    }
+
+    // ---- tiles, as in encode_tiled_kernel ------------------------------------------------
+    uint32_t cz = 0, cf = 0, hint = 0xFFFFFFFFu;
+    uint64_t pos = 0;
+    bool fits = true;
+    for (uint32_t tb = 0; tb < words; tb += kEncMaxWords) {
+        const uint32_t tw = min(kEncMaxWords, words - tb);
+        const uint32_t te = tb + tw;
+        uint32_t nbz = words, nbf = words;
+        if (te < words) {  // first Z / F break in the 256 words after the tile
+            const uint32_t la = min(256u, words - te);
+            uint32_t fz = la, ff = la, h2 = 0xFFFFFFFFu;
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t i = 4 * lane + t;
+                if (i < la) {
+                    const uint32_t tg = nonzero_tag(msg_word(m, te + i, h2));
+                    if (tg != 0 && fz == la) fz = i;
+                    if (tg != 0xFF && ff == la) ff = i;
+                }
+            }
+            const uint32_t bz = wave_min(fz), bf = wave_min(ff);
+            nbz = bz < la ? te + bz : (la == 256u ? te + 256u : words);
+            nbf = bf < la ? te + bf : (la == 256u ? te + 256u : words);
+        }
+        wave_lds_sync();  // the previous tile's write-back read the slice
+        {  // stage: lane l gathers words tb + 8l .. tb + 8l + 7 into its row
+            uint64_t w8[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t i = 8 * lane + t;
+                w8[t] = i < tw ? msg_word(m, tb + i, hint) : 0ull;
+            }
+            uint4* const row = reinterpret_cast<uint4*>(lds + lane * kEncRow);
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                row[qd] = make_uint4((uint32_t)w8[2 * qd], (uint32_t)(w8[2 * qd] >> 32), (uint32_t)w8[2 * qd + 1],
+                                     (uint32_t)(w8[2 * qd + 1] >> 32));
+        }
+        wave_lds_sync();
+        const uint64_t room = (WRITE && fits && pos <= cap) ? cap - pos : 0;
+        const uint32_t Pt = encode_tile<WRITE, false>(lds, lut, lane, tw, tb, cz, cf, nbz, nbf, out + ob + pos,
+                                                      room);
+        if ((uint64_t)Pt > room) fits = false;
+        pos += Pt;
+    }
+    if (lane == 0) {
+        out_len[msg] = pos;
+        status[msg] = (WRITE && !fits) ? ST_SPACE : ST_OK;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Message.init on device (message.zig:341-394): the segment table of each framed
+// message, lane per message. seg_off / seg_len get max_segs entries per message
+// (row i at i * max_segs; segments past max_segs are counted, not listed).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void message_init_kernel(const uint8_t* __restrict__ in,
+                                                              const uint64_t* __restrict__ in_off,
+                                                              const uint64_t* __restrict__ in_len, uint32_t n,
+                                                              uint32_t max_segs, uint32_t* __restrict__ seg_count,
+                                                              uint64_t* __restrict__ seg_off,
+                                                              uint64_t* __restrict__ seg_len,
+                                                              int32_t* __restrict__ status) {
+    const uint32_t msg = blockIdx.x * kBlock + threadIdx.x;
+    if (msg >= n) return;
+    const uint8_t* const d = in + in_off[msg];
+    const uint64_t len = in_len[msg];
+    auto u32at = [&](uint64_t o) {
+        return (uint32_t)d[o] | ((uint32_t)d[o + 1] << 8) | ((uint32_t)d[o + 2] << 16) | ((uint32_t)d[o + 3] << 24);
+    };
+    int32_t st = ST_OK;
+    uint64_t count = 0;
+    if (len < 4) {
+        st = ST_EOS;  // :343 readInt
+    } else {
+        const uint32_t m1 = u32at(0);
+        if (m1 == 0xFFFFFFFFu) st = ST_SEGCOUNT;  // :346
+        else if ((uint64_t)m1 + 1 > kMsgMaxSegs) st = ST_SEGLIMIT;  // :348
+        else {
+            count = (uint64_t)m1 + 1;
+            const uint64_t header = 4 * (1 + count + ((count & 1) ? 0 : 1));
+            if (header > len) st = ST_TRUNC;  // :353
+            uint64_t o = header;
+            for (uint64_t i = 0; st == ST_OK && i < count; ++i) {
+                const uint64_t end = o + 8ull * u32at(4 + 4 * i);
+                if (end > len) { st = ST_TRUNC; break; }  // :380
+                if (i < max_segs) {
+                    seg_off[(uint64_t)msg * max_segs + i] = o;
+                    seg_len[(uint64_t)msg * max_segs + i] = end - o;
+                }
+                o = end;
+            }
+        }
+    }
+    seg_count[msg] = st == ST_OK ? (uint32_t)count : 0u;
+    status[msg] = st;
 }
 
 // ---------------------------------------------------------------------------
@@ -2423,6 +2645,29 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
     decode_wave_kernel<false><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                out_len, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_len, const uint32_t* seg_first,
+                                 const uint32_t* seg_count, uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                 const uint64_t* out_cap, uint64_t* out_len, int32_t* status, bool write,
+                                 hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (write)
+        encode_message_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count, n,
+                                                                           out, out_off, out_cap, out_len, status);
+    else
+        encode_message_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count,
+                                                                            n, out, out_off, out_cap, out_len, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_message_init(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                               uint32_t max_segs, uint32_t* seg_count, uint64_t* seg_off, uint64_t* seg_len,
+                               int32_t* status, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    message_init_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, max_segs,
+                                                                          seg_count, seg_off, seg_len, status);
     return hipGetLastError();
 }
 

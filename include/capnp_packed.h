@@ -51,7 +51,9 @@ enum capnp_packed_status {
     CAPNP_PACKED_INVALID_SEGMENT_COUNT = 9,     /* segment count - 1 == 0xFFFFFFFF (reader.zig:123) */
     CAPNP_PACKED_SEGMENT_COUNT_LIMIT_EXCEEDED = 10, /* more than 512 segments (reader.zig:125) */
     CAPNP_PACKED_MESSAGE_TOO_LARGE = 11,        /* more than 8 Mi words (reader.zig:140) */
-    CAPNP_PACKED_INVALID_PACKED_MESSAGE = 12    /* the last record overshoots the framed length (reader.zig:151-153) */
+    CAPNP_PACKED_INVALID_PACKED_MESSAGE = 12,   /* the last record overshoots the framed length (reader.zig:151-153) */
+    /* Message.init (message.zig:341-394) only: */
+    CAPNP_PACKED_TRUNCATED_MESSAGE = 13         /* header or a segment runs past the data (message.zig:353/380) */
 };
 
 /* Version / capability query (precedent: src/wasm/capnp_host_abi.zig:60-70). */
@@ -153,6 +155,31 @@ int capnp_packed_read_message_batch(const uint8_t* d_in, const uint64_t* d_in_of
  * On OUT_OF_SPACE, *out_len is the framed length. */
 int capnp_packed_read_message(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len,
                               size_t* consumed);
+
+/* MessageBuilder.toPackedBytes (message.zig:2175-2179 = packPacked(toBytes()),
+ * toBytes 2123-2170) for n messages, packed straight from their segments: the
+ * framed bytes (segment table + segments) are never materialised. Message i has
+ * d_seg_count[i] segments (0 = one empty segment, as toBytes adds one) listed
+ * from index d_seg_first[i] of d_seg_ptr (device addresses, 8-byte aligned) and
+ * d_seg_len (bytes, multiples of 8, as a MessageBuilder's segments are). At most
+ * 512 segments per message (Message.max_segment_count, message.zig:310): more,
+ * or a misaligned segment, gives INVALID_ARGUMENT. Output as in
+ * capnp_packed_encode_batch; d_out == NULL computes the packed sizes only. */
+int capnp_packed_encode_message_batch(const uint64_t* d_seg_ptr, const uint64_t* d_seg_len,
+                                      const uint32_t* d_seg_first, const uint32_t* d_seg_count, uint32_t n,
+                                      uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                                      uint64_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Message.init (message.zig:341-394) segment-table parse of n framed messages
+ * d_in[d_in_off[i] .. + d_in_len[i]) (e.g. the output of a decode batch).
+ * d_seg_count[i] = segments; segment j < max_segs of message i is
+ * d_in[d_in_off[i] + d_seg_off[i*max_segs + j] .. + d_seg_len[i*max_segs + j]).
+ * Errors per message: END_OF_STREAM (< 4 bytes), INVALID_SEGMENT_COUNT,
+ * SEGMENT_COUNT_LIMIT_EXCEEDED, TRUNCATED_MESSAGE. Trailing bytes after the last
+ * segment are ignored, as in the reference. */
+int capnp_packed_message_init_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                    uint32_t n, uint32_t max_segs, uint32_t* d_seg_count, uint64_t* d_seg_off,
+                                    uint64_t* d_seg_len, int32_t* d_status, void* stream);
 
 /* Exclusive scan of n lengths into n+1 offsets (d_off[0] = base, d_off[n] =
  * base + total), on device.

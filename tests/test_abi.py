@@ -48,10 +48,10 @@ def test_version_and_status_names():
                      "InvalidArgument", "DeviceError", "NoDevice"]
     assert cp.encode_bound(4096) == 5120 and cp.encode_bound(0) == 0
     # Reader.readPackedMessage errors (reader.zig:84-156)
-    names = [cp.lib().capnp_packed_status_name(i).decode() for i in range(8, 13)]
+    names = [cp.lib().capnp_packed_status_name(i).decode() for i in range(8, 14)]
     assert names == ["EndOfStream", "InvalidSegmentCount", "SegmentCountLimitExceeded", "MessageTooLarge",
-                     "InvalidPackedMessage"]
-    for st in range(13):
+                     "InvalidPackedMessage", "TruncatedMessage"]
+    for st in range(14):
         if st:
             assert cp._ERRORS[st].status == st
 

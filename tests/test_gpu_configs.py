@@ -162,3 +162,138 @@ def test_tiled_encode_run_carries():
     for i, u in enumerate(units):
         st, exp = oracle.pack(u)
         assert got[i] == exp, f"unit {i} ({len(u) // 8} words)"
+
+
+# ---------------------------------------------------------------------------
+# framing fused with the codec
+# ---------------------------------------------------------------------------
+
+def _segment_pool(messages, rng):
+    """Every segment of every message placed at a shuffled, 8-aligned offset of one
+    device pool; returns (pool, seg_ptr, seg_len, seg_first, seg_count)."""
+    flat = [s for m in messages for s in m]
+    order = rng.permutation(len(flat)) if flat else np.zeros(0, dtype=np.int64)
+    offs = [0] * len(flat)
+    pos = 0
+    for k in order:
+        pos += 8 * int(rng.integers(0, 3))  # gaps between segments
+        offs[k] = pos
+        pos += len(flat[k])
+    host = np.zeros(pos + 16, dtype=np.uint8)
+    for o, s in zip(offs, flat):
+        host[o:o + len(s)] = np.frombuffer(s, dtype=np.uint8)
+    pool = torch.from_numpy(host).to(DEV)
+    base = pool.data_ptr()
+    seg_ptr = torch.tensor([base + o for o in offs] or [0], dtype=torch.int64, device=DEV)
+    seg_len = torch.tensor([len(s) for s in flat] or [0], dtype=torch.int64, device=DEV)
+    first, k = [], 0
+    for m in messages:
+        first.append(k)
+        k += len(m)
+    return (pool, seg_ptr, seg_len, torch.tensor(first, dtype=torch.int32, device=DEV),
+            torch.tensor([len(m) for m in messages], dtype=torch.int32, device=DEV))
+
+
+def _frame(segs):
+    return pyref.frame(segs if segs else [b""])  # toBytes adds one empty segment (message.zig:2128-2130)
+
+
+def test_encode_message_batch_matches_toPackedBytes():
+    rng = np.random.default_rng(17)
+
+    def seg(words, p):
+        b = rng.integers(1, 256, 8 * words, dtype=np.uint8)
+        b[rng.random(8 * words) < p] = 0
+        return b.tobytes()
+
+    messages = [[], [b""], [seg(1, .5)], [seg(0, .5), seg(3, .5)]]
+    for _ in range(200):
+        p = float(rng.choice([0.1, 0.5, 0.9, 1.0, 0.0]))
+        messages.append([seg(int(rng.integers(0, 300)), p) for _ in range(int(rng.integers(1, 12)))])
+    messages.append([seg(1, .5) for _ in range(512)])            # the segment limit, header of 257 words
+    messages.append([seg(700, .5), seg(2000, 0.97), seg(5, 0.0)])  # tiles, zero and literal runs across segments
+    messages.append([bytes(8 * 600), bytes(8 * 600)])             # one zero run over two segments and tiles
+    pool, seg_ptr, seg_len, first, count = _segment_pool(messages, rng)
+    n = len(messages)
+    caps = [cp.encode_bound(len(_frame(m))) for m in messages]
+    offs, q = [], 0
+    for c in caps:
+        offs.append(q)
+        q += (c + 15) // 16 * 16
+    t = lambda xs: torch.tensor(xs, dtype=torch.int64, device=DEV)  # noqa: E731
+    d_out = torch.zeros(q + 16, dtype=torch.uint8, device=DEV)
+    out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_message_batch(seg_ptr, seg_len, first, count, d_out, t(offs), t(caps), out_len, status)
+    sizes = torch.zeros(n, dtype=torch.int64, device=DEV)
+    sst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_message_batch(seg_ptr, seg_len, first, count, None, None, None, sizes, sst)
+    torch.cuda.synchronize()
+    h, lens, sts = d_out.cpu().numpy(), out_len.cpu().numpy(), status.cpu().numpy()
+    for i, m in enumerate(messages):
+        st, exp = oracle.pack(_frame(m))
+        assert st == oracle.OK
+        assert sts[i] == cp.OK and h[offs[i]:offs[i] + lens[i]].tobytes() == exp, f"message {i}"
+    assert torch.equal(sizes, out_len) and (sst.cpu() == 0).all()
+
+
+def test_encode_message_batch_errors():
+    rng = np.random.default_rng(3)
+    messages = [[bytes(8)] * 513, [bytes(8), bytes(12)], [bytes(range(1, 65))]]
+    pool, seg_ptr, seg_len, first, count = _segment_pool(messages, rng)
+    n = len(messages)
+    t = lambda xs: torch.tensor(xs, dtype=torch.int64, device=DEV)  # noqa: E731
+    d_out = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_message_batch(seg_ptr, seg_len, first, count, d_out, t([0, 1024, 2048]), t([1024, 1024, 20]),
+                            out_len, status)
+    torch.cuda.synchronize()
+    exp_len = len(oracle.pack(_frame(messages[2]))[1])
+    assert status.cpu().tolist() == [cp.INVALID_ARGUMENT, cp.INVALID_ARGUMENT, cp.OUT_OF_SPACE]
+    assert int(out_len[2]) == exp_len
+
+
+def test_message_init_batch_matches_message_init():
+    rng = np.random.default_rng(23)
+    frames = []
+    for _ in range(300):
+        segs = [bytes(8 * int(rng.integers(0, 20))) for _ in range(int(rng.integers(1, 9)))]
+        f = pyref.frame(segs)
+        kind = int(rng.integers(0, 6))
+        if kind == 1:
+            f = f + bytes(8 * int(rng.integers(1, 4)))      # trailing bytes are ignored
+        elif kind == 2:
+            f = f[:int(rng.integers(0, len(f)))]              # truncated anywhere
+        frames.append(f)
+    frames += [b"", b"\x00\x00", b"\xff\xff\xff\xff" + bytes(12), struct_u32(512) + bytes(4 * 514 + 8),
+               struct_u32(511) + bytes(4 * 513)]
+    offs, pos = [], 0
+    for f in frames:
+        offs.append(pos)
+        pos += (len(f) + 7) // 8 * 8
+    host = np.zeros(pos + 8, dtype=np.uint8)
+    for o, f in zip(offs, frames):
+        host[o:o + len(f)] = np.frombuffer(f, dtype=np.uint8)
+    n, ms = len(frames), 16
+    cnt = torch.zeros(n, dtype=torch.int32, device=DEV)
+    so = torch.zeros(n * ms, dtype=torch.int64, device=DEV)
+    sl = torch.zeros(n * ms, dtype=torch.int64, device=DEV)
+    st = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.message_init_batch(torch.from_numpy(host).to(DEV), torch.tensor(offs, dtype=torch.int64, device=DEV),
+                          torch.tensor([len(f) for f in frames], dtype=torch.int64, device=DEV), ms, cnt, so, sl, st)
+    torch.cuda.synchronize()
+    codes = {0: cp.OK, -1: cp.END_OF_STREAM, -2: cp.INVALID_SEGMENT_COUNT, -3: cp.SEGMENT_COUNT_LIMIT_EXCEEDED,
+             -4: cp.TRUNCATED_MESSAGE}
+    cnt, so, sl, st = cnt.cpu().numpy(), so.cpu().numpy(), sl.cpu().numpy(), st.cpu().numpy()
+    for i, f in enumerate(frames):
+        rc, table = oracle.message_init(f, max_segs=ms)
+        assert st[i] == codes[rc], f"frame {i}"
+        if rc == 0:
+            assert cnt[i] == len(table) or (cnt[i] > ms and len(table) == ms)
+            got = [(int(so[i * ms + j]), int(sl[i * ms + j])) for j in range(min(int(cnt[i]), ms))]
+            assert got == [(int(a), int(b)) for a, b in table], f"frame {i}"
+
+
+def struct_u32(v):
+    return int(v).to_bytes(4, "little")
