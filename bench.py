@@ -287,6 +287,79 @@ def skewed_leg(args, dev, n=1 << 20, reps=10):
             "note": "SURVEY config C5: truncated Pareto unit sizes 64 B..256 KiB, p = zero_thresh/256"}
 
 
+def message_leg(args, dev, reps=10, segs=4, seg_words=127):
+    """SURVEY §8(f) row 2, framing fused with the codec: 1M messages of 4 segments x
+    127 words (framed 4088 B) from a segment pool, packed straight from the segment
+    lists (encode_message_batch), against toBytes as a device gather + encode_batch;
+    then Message.init on device (message_init_batch) over the decoded frames.
+    Reported beside `value`, never as it."""
+    n = args.units
+    stream = torch.cuda.current_stream()
+    sb = 8 * seg_words
+    pool = cp.generate(n * segs, sb, seed=0xC0DE0006, zero_thresh=args.zero_thresh, device=dev)
+    seg_ptr = pool.data_ptr() + torch.arange(n * segs, dtype=torch.int64, device=dev) * sb
+    seg_len = torch.full((n * segs,), sb, dtype=torch.int64, device=dev)
+    first = torch.arange(0, n * segs, segs, dtype=torch.int32, device=dev)
+    count = torch.full((n,), segs, dtype=torch.int32, device=dev)
+    hw = (1 + segs + (0 if segs % 2 else 1)) // 2
+    fb = 8 * hw + segs * sb
+    slot = (cp.encode_bound(fb) + 15) // 16 * 16
+    pk_off, pk_cap = cp.uniform_layout(n, slot, device=dev)
+    pk_cap.fill_(cp.encode_bound(fb))
+    d_pk = torch.empty(n * slot, dtype=torch.uint8, device=dev)
+    plen = torch.zeros(n, dtype=torch.int64, device=dev)
+    pst = torch.zeros(n, dtype=torch.int32, device=dev)
+    # toBytes materialised: header words + segment copy, then encode_batch (the unfused path)
+    framed = torch.empty(n * fb, dtype=torch.uint8, device=dev)
+    hdr = torch.zeros(2 * hw, dtype=torch.int32, device=dev)
+    hdr[0] = segs - 1
+    hdr[1:1 + segs] = seg_words
+    f_off, f_len = cp.uniform_layout(n, fb, device=dev)
+    plen2 = torch.zeros_like(plen)
+    fv = framed.view(n, fb)
+
+    def fused():
+        cp.encode_message_batch(seg_ptr, seg_len, first, count, d_pk, pk_off, pk_cap, plen, pst, stream=stream)
+
+    def unfused():
+        fv[:, :8 * hw].copy_(hdr.view(torch.uint8).expand(n, 8 * hw))
+        fv[:, 8 * hw:].copy_(pool.view(n, segs * sb))
+        cp.encode_batch(framed, f_off, f_len, d_pk, pk_off, pk_cap, plen2, pst, stream=stream)
+
+    def timed(fn):
+        fn()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        for _ in range(reps):
+            fn()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) / reps
+
+    t_unfused = timed(unfused)
+    ok = bool((pst == 0).all().item())
+    t_fused = timed(fused)
+    ok = ok and bool((pst == 0).all().item() and torch.equal(plen, plen2))
+    # decode the packed messages and parse their segment tables on device
+    d_out = torch.empty(n * fb, dtype=torch.uint8, device=dev)
+    ulen = torch.zeros(n, dtype=torch.int64, device=dev)
+    ust = torch.zeros(n, dtype=torch.int32, device=dev)
+    cp.decode_batch(d_pk, pk_off, plen, d_out, f_off, f_len, ulen, ust, stream=stream)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    so = torch.zeros(n * segs, dtype=torch.int64, device=dev)
+    sl = torch.zeros(n * segs, dtype=torch.int64, device=dev)
+    mst = torch.zeros(n, dtype=torch.int32, device=dev)
+    t_init = timed(lambda: cp.message_init_batch(d_out, f_off, f_len, segs, cnt, so, sl, mst, stream=stream))
+    ok = ok and bool(torch.equal(d_out, framed) and (mst == 0).all().item() and (cnt == segs).all().item()
+                     and (sl == sb).all().item())
+    return {"messages": n, "segments_per_message": segs, "framed_bytes": fb,
+            "fused_encode_ms": round(t_fused, 4), "tobytes_copy_plus_encode_ms": round(t_unfused, 4),
+            "fused_GiB_s": round(n * fb / (t_fused * 1e-3) / 2 ** 30, 2),
+            "message_init_ms": round(t_init, 4), "bit_exact": ok,
+            "note": "GiB/s of framed bytes; fused = encode_message_batch from segment lists (no framed copy)"}
+
+
 def read_message_leg(args, dev, reps=10):
     """SURVEY §8(f) row 1, Reader.readPackedMessage (reader.zig:84-156) batched: the
     same 1M x 4 KiB units made into framed messages (one segment of 511 words), packed
@@ -369,6 +442,9 @@ def main():
         del wl
         torch.cuda.empty_cache()
         extra["read_message"] = read_message_leg(args, dev)
+    if world == 1 and not args.no_read_message:
+        torch.cuda.empty_cache()
+        extra["message_framing"] = message_leg(args, dev)
     if world == 1 and not args.no_skewed:
         torch.cuda.empty_cache()
         extra["c5_skewed"] = skewed_leg(args, dev)

@@ -689,7 +689,7 @@ constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig
 
 struct MsgView {
     const uint32_t* woff;   // LDS: word offset of segment s in the payload, s <= count
-    const uint64_t* base;   // LDS: device address of segment s
+    const uint64_t* base;   // device address of segment s (LDS copy, or the caller's array)
     uint32_t count;         // segments (>= 1)
     uint32_t hw;            // header words
 };
@@ -721,31 +721,67 @@ __device__ __forceinline__ uint64_t msg_word(const MsgView& m, uint32_t q, uint3
     return *reinterpret_cast<const uint64_t*>(m.base[s] + 8ull * (p - m.woff[s]));
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* __restrict__ seg_ptr,
-                                                                const uint64_t* __restrict__ seg_len,
-                                                                const uint32_t* __restrict__ seg_first,
-                                                                const uint32_t* __restrict__ seg_count, uint32_t n,
-                                                                uint8_t* __restrict__ out,
-                                                                const uint64_t* __restrict__ out_off,
-                                                                const uint64_t* __restrict__ out_cap,
-                                                                uint64_t* __restrict__ out_len,
-                                                                int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint32_t woff_all[kWavesPerBlock * (kMsgMaxSegs + 1)];
-    __shared__ uint64_t base_all[kWavesPerBlock * kMsgMaxSegs];
-    __shared__ uint64_t lut[256];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WRITE) {
-        lut[threadIdx.x] = compact_selector(threadIdx.x);
-        __syncthreads();
+// Stage framed words [tb, tb + tw) (tw <= 512) into the row layout. Lane l gathers
+// words tb + l + 64j: consecutive lanes read consecutive words (coalesced within a
+// segment), and all 8 addresses are formed before any load is issued, so the 8
+// loads are in flight together.
+__device__ __forceinline__ void msg_stage(const MsgView& m, uint32_t tb, uint32_t tw, uint32_t lane, uint32_t& hint,
+                                          uint8_t* lds) {
+    const uint64_t* src[8];
+    uint64_t hv[8];
+    uint32_t wlo = 1, whi = 0;  // cached segment window [wlo, whi) of payload words (empty)
+    uint64_t wbase = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t i = lane + 64 * j;
+        src[j] = nullptr;
+        hv[j] = 0;
+        if (i < tw) {
+            const uint32_t q = tb + i;
+            if (q < m.hw) {
+                hv[j] = msg_word(m, q, hint);  // header word (no load)
+            } else {
+                const uint32_t p = q - m.hw;
+                if (p < wlo || p >= whi) {  // leave the cached segment window: search, then cache
+                    if (hint >= m.count || p < m.woff[hint]) {
+                        uint32_t lo = 0, hi = m.count;
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (m.woff[mid] <= p) lo = mid;
+                            else hi = mid;
+                        }
+                        hint = lo;
+                    }
+                    while (p >= m.woff[hint + 1]) ++hint;
+                    wlo = m.woff[hint];
+                    whi = m.woff[hint + 1];
+                    wbase = m.base[hint];
+                }
+                src[j] = reinterpret_cast<const uint64_t*>(wbase + 8ull * (p - wlo));
+            }
+        }
     }
-    const uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
-    if (msg >= n) return;
-    uint8_t* const lds = smem + wave * kEncLds;
-    uint32_t* const woff = woff_all + wave * (kMsgMaxSegs + 1);
-    uint64_t* const base = base_all + wave * kMsgMaxSegs;
+    uint64_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = src[j] ? *src[j] : hv[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t i = lane + 64 * j;
+        if (i < tw) *reinterpret_cast<uint64_t*>(lds + (i >> 3) * kEncRow + (i & 7) * 8) = x[j];
+    }
+}
+
+// One message (see encode_message_kernel); lds / woff / base are the wave's slices.
+template <bool WRITE, bool TILED>
+__device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, const uint64_t* lut, uint8_t* lds,
+                                                   uint32_t* woff, uint64_t* base,
+                                                   const uint64_t* __restrict__ seg_ptr,
+                                                   const uint64_t* __restrict__ seg_len,
+                                                   const uint32_t* __restrict__ seg_first,
+                                                   const uint32_t* __restrict__ seg_count, uint8_t* __restrict__ out,
+                                                   const uint64_t* __restrict__ out_off,
+                                                   const uint64_t* __restrict__ out_cap,
+                                                   uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
 
     // ---- segment table: lane l takes segments 8l .. 8l+7 ------------------------------
     const uint32_t c_in = seg_count[msg];
@@ -771,7 +807,7 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
             // segments are whole words at 8-B aligned addresses (a MessageBuilder's always are)
             bad |= (len & 7) != 0 || (ptr & 7) != 0 || (len >> 3) > 0xFFFFFFFFull;
             wl[t] = (uint32_t)(len >> 3);
-            base[s] = ptr;
+            if (TILED) base[s] = ptr;
             wsum += wl[t];
         }
     }
@@ -791,13 +827,29 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
         if (lane == 0) { out_len[msg] = 0; status[msg] = ST_ARG; }
         return;
     }
-    wave_lds_sync();
-    const MsgView m{woff, base, count, hw};
     const uint32_t words = (uint32_t)words64;
+    if (!TILED && words > kEncMaxWords) {
+        if (lane == 0) status[msg] = kStNeedFull;
+        return;
+    }
+    wave_lds_sync();
+    const MsgView m{woff, TILED ? base : (c_in ? seg_ptr + first : nullptr), count, hw};
     uint64_t ob = 0, cap = 0;
     if (WRITE) {
         ob = out_off[msg];
         cap = out_cap[msg];
+    }
+    if (!TILED) {  // one tile
+        uint32_t hint = 0xFFFFFFFFu;
+        msg_stage(m, 0, words, lane, hint, lds);
+        wave_lds_sync();
+        uint32_t cz = 0, cf = 0;
+        const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        if (lane == 0) {
+            out_len[msg] = P;
+            status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
+        }
+        return;
     }
 
     // ---- tiles, as in encode_tiled_kernel ------------------------------------------------
@@ -824,19 +876,7 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
             nbf = bf < la ? te + bf : (la == 256u ? te + 256u : words);
         }
         wave_lds_sync();  // the previous tile's write-back read the slice
-        {  // stage: lane l gathers words tb + 8l .. tb + 8l + 7 into its row
-            uint64_t w8[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const uint32_t i = 8 * lane + t;
-                w8[t] = i < tw ? msg_word(m, tb + i, hint) : 0ull;
-            }
-            uint4* const row = reinterpret_cast<uint4*>(lds + lane * kEncRow);
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                row[qd] = make_uint4((uint32_t)w8[2 * qd], (uint32_t)(w8[2 * qd] >> 32), (uint32_t)w8[2 * qd + 1],
-                                     (uint32_t)(w8[2 * qd + 1] >> 32));
-        }
+        msg_stage(m, tb, tw, lane, hint, lds);
         wave_lds_sync();
         const uint64_t room = (WRITE && fits && pos <= cap) ? cap - pos : 0;
         const uint32_t Pt = encode_tile<WRITE, false>(lds, lut, lane, tw, tb, cz, cf, nbz, nbf, out + ob + pos,
@@ -847,6 +887,54 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
     if (lane == 0) {
         out_len[msg] = pos;
         status[msg] = (WRITE && !fits) ? ST_SPACE : ST_OK;
+    }
+}
+
+// TILED = false: every message; one framed tile (<= 512 words) is encoded here with
+// the single-tile encode_tile (segment addresses read from the caller's array, so
+// the wave's LDS is the tile plus the word offsets), longer messages are marked for
+// TILED = true, which keeps the addresses in LDS and walks the tiles.
+// The multi-tile pass strides over the batch with a small grid, 64 statuses per load.
+template <bool WRITE, bool TILED>
+__global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* __restrict__ seg_ptr,
+                                                                const uint64_t* __restrict__ seg_len,
+                                                                const uint32_t* __restrict__ seg_first,
+                                                                const uint32_t* __restrict__ seg_count, uint32_t n,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint64_t* __restrict__ out_len,
+                                                                int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint32_t woff_all[kWavesPerBlock * (kMsgMaxSegs + 1)];
+    __shared__ uint64_t base_all[TILED ? kWavesPerBlock * kMsgMaxSegs : 1];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    uint8_t* const lds = smem + wave * kEncLds;
+    uint32_t* const woff = woff_all + wave * (kMsgMaxSegs + 1);
+    uint64_t* const base = TILED ? base_all + wave * kMsgMaxSegs : nullptr;
+    if (!TILED) {
+        const uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
+        if (msg < n)
+            encode_message_one<WRITE, false>(msg, lane, lut, lds, woff, base, seg_ptr, seg_len, seg_first, seg_count,
+                                             out, out_off, out_cap, out_len, status);
+        return;
+    }
+    const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;
+    for (uint32_t ubase = (blockIdx.x * kWavesPerBlock + wave) * kWave; ubase < n; ubase += stride) {
+        const uint32_t u = ubase + lane;
+        uint64_t todo = __ballot(u < n && status[u] == kStNeedFull);
+        while (todo) {
+            const uint32_t msg = ubase + (uint32_t)__builtin_ctzll(todo);
+            todo &= todo - 1;
+            encode_message_one<WRITE, true>(msg, lane, lut, lds, woff, base, seg_ptr, seg_len, seg_first, seg_count,
+                                            out, out_off, out_cap, out_len, status);
+        }
     }
 }
 
@@ -2653,12 +2741,19 @@ hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_le
                                  const uint64_t* out_cap, uint64_t* out_len, int32_t* status, bool write,
                                  hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (write)
-        encode_message_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count, n,
-                                                                           out, out_off, out_cap, out_len, status);
-    else
-        encode_message_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count,
-                                                                            n, out, out_off, out_cap, out_len, status);
+    // every message, then the marked multi-tile ones (a grid striding over the statuses)
+    const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    if (write) {
+        encode_message_kernel<true, false><<<blocks_for(n), kBlock, 0, stream>>>(
+            seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
+        encode_message_kernel<true, true><<<tiled_blocks, kBlock, 0, stream>>>(
+            seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
+    } else {
+        encode_message_kernel<false, false><<<blocks_for(n), kBlock, 0, stream>>>(
+            seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
+        encode_message_kernel<false, true><<<tiled_blocks, kBlock, 0, stream>>>(
+            seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
+    }
     return hipGetLastError();
 }
 
