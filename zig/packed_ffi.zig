@@ -30,6 +30,7 @@ pub const Status = enum(c_int) {
     segment_count_limit_exceeded = 10,
     message_too_large = 11,
     invalid_packed_message = 12,
+    truncated_message = 13,
     _,
 };
 
@@ -66,6 +67,18 @@ pub extern "capnp_packed" fn capnp_packed_read_message_batch(
     d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
     d_out_len: [*]u64, d_consumed: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
 ) c_int;
+/// MessageBuilder.toPackedBytes for n messages straight from their segment lists
+/// (message.zig:2123-2179 without the toBytes copy); d_out = null: sizes only.
+pub extern "capnp_packed" fn capnp_packed_encode_message_batch(
+    d_seg_ptr: [*]const u64, d_seg_len: [*]const u64, d_seg_first: [*]const u32, d_seg_count: [*]const u32,
+    n: u32, d_out: ?[*]u8, d_out_off: ?[*]const u64, d_out_cap: ?[*]const u64,
+    d_out_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
+/// Message.init segment-table parse (message.zig:341-394) of n framed messages.
+pub extern "capnp_packed" fn capnp_packed_message_init_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32, max_segs: u32,
+    d_seg_count: [*]u32, d_seg_off: [*]u64, d_seg_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
+) c_int;
 pub extern "capnp_packed" fn capnp_packed_scan_scratch_bytes(n: u32) usize;
 pub extern "capnp_packed" fn capnp_packed_lengths_to_offsets(
     d_len: [*]const u64, n: u32, base: u64, d_off: [*]u64,
@@ -87,6 +100,8 @@ pub const Error = error{
     SegmentCountLimitExceeded,
     MessageTooLarge,
     InvalidPackedMessage,
+    // Message.init (message.zig:341-394)
+    TruncatedMessage,
 };
 
 fn check(status: c_int) Error!void {
@@ -102,6 +117,7 @@ fn check(status: c_int) Error!void {
         .segment_count_limit_exceeded => error.SegmentCountLimitExceeded,
         .message_too_large => error.MessageTooLarge,
         .invalid_packed_message => error.InvalidPackedMessage,
+        .truncated_message => error.TruncatedMessage,
         else => {
             std.log.err("capnp_packed: {s}", .{capnp_packed_last_error()});
             return error.PackedDeviceError;
