@@ -31,6 +31,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "capnp_packed.h"
 #include "kernels.h"
 
@@ -605,14 +607,24 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
         }
         return;
     }
-    // longer units: encode_tiled_kernel (a separate kernel keeps this one at its
+    // longer units belong to encode_tiled_kernel, which selects them by the same test
+    // (encode_tiled_unit) and may be running beside this kernel on the side stream:
+    // nothing of theirs is written here (a separate kernel keeps this one at its
     // register budget)
-    if (lane == 0) status[unit] = kStNeedFull;
 }
 
-// Units longer than one tile, marked kStNeedFull by encode_kernel. A small grid
-// strides over the batch; each wave tests 64 statuses per load and encodes the
-// marked units one after another, tile by tile.
+// The units encode_tiled_kernel owns: valid word streams (8-aligned start, whole
+// words) of more than one tile, within the u32 word-index range. encode_kernel
+// returns early for exactly these, so the two kernels never write the same unit and
+// can run concurrently (launch_encode).
+__device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t off, uint64_t len) {
+    return !(reinterpret_cast<uintptr_t>(in + off) & 7) && !(len & 7) && (len >> 3) > kEncMaxWords &&
+           (len >> 3) <= 0xFFFFF000ull;
+}
+
+// Units longer than one tile (encode_tiled_unit). A small grid strides over the
+// batch; each wave tests 64 units per load and encodes the selected units one after
+// another, tile by tile.
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __restrict__ in,
                                                               const uint64_t* __restrict__ in_off,
@@ -634,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
     const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;
     for (uint32_t ubase = (blockIdx.x * kWavesPerBlock + wave) * kWave; ubase < n; ubase += stride) {
     const uint32_t u = ubase + lane;
-    uint64_t todo = __ballot(u < n && status[u] == kStNeedFull);
+    uint64_t todo = __ballot(u < n && encode_tiled_unit(in, in_off[u], in_len[u]));
     while (todo) {  // wave-uniform
     const uint32_t unit = ubase + (uint32_t)__builtin_ctzll(todo);
     todo &= todo - 1;
@@ -1536,7 +1548,14 @@ __device__ uint64_t* cpk_wv_prof;
 #define WV_COUNT(k, v) do { } while (0)
 #endif
 
-template <bool CK>
+// SEL: kWvAll every unit (wave per unit); kWvMarked the units a first pass marked
+// kStNeedFull; kWvLong the units decode_long_unit selects (the indexed decoder's
+// fallback, which owns them from the start and may run beside passes 1 and 2).
+constexpr int kWvAll = 0, kWvMarked = 1, kWvLong = 2;
+__device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
+                                                 uint64_t out_off, uint64_t cap);
+
+template <int SEL>
 __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __restrict__ in,
                                                                const uint64_t* __restrict__ in_off,
                                                                const uint64_t* __restrict__ in_len, uint32_t n,
@@ -1558,13 +1577,15 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     // then takes only the units it marked kStNeedFull, with a small grid striding
     // over the batch (every other status is final or the fill pass's).
     // The wave tests 64 statuses per load (CK) and walks the marked units in order.
+    constexpr bool CK = SEL != kWvAll;
     const uint32_t stride = CK ? gridDim.x * kWvWaves * kWave : gridDim.x * kWvWaves;
     for (uint32_t ubase = CK ? (blockIdx.x * kWvWaves + wave) * kWave : blockIdx.x * kWvWaves + wave; ubase < n;
          ubase += stride) {
     uint64_t todo = 1;
     if (CK) {
         const uint32_t u = ubase + lane;
-        todo = __ballot(u < n && status[u] == kStNeedFull);
+        if (SEL == kWvMarked) todo = __ballot(u < n && status[u] == kStNeedFull);
+        else todo = __ballot(u < n && decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u]));
     }
     while (todo) {  // wave-uniform
     const uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : ubase;
@@ -1911,10 +1932,24 @@ __global__ __launch_bounds__(kExBlock) void decode_expand_kernel(const uint8_t* 
 //          offsets from a scan of the records' word counts, expand into LDS and
 //          store coalesced.
 // Units pass 2 cannot stage (> kFlPieces pieces) or whose slot cannot hold the
-// records get kStNeedFull from pass 1 and go to decode_wave_kernel<true>.
+// records (decode_long_unit) belong to decode_wave_kernel<kWvLong>, which runs beside
+// passes 1 and 2 on the side stream; the read-message passes mark them kStNeedFull
+// for decode_wave_kernel<kWvMarked> instead.
 constexpr uint32_t kIxDead = 0xFFFFFFFFu;         // walk position of a lane with nothing (more) to walk
 constexpr uint32_t kFlPieces = 320;               // pass-2 window: 64 lanes x 5 pieces
 constexpr uint64_t kIxSizeMax = 1ull << 31;       // size-only walk: longer units use decode_lane_kernel
+
+// The units the indexed decoder's fallback owns (decode_wave_kernel<kWvLong>): an
+// 8-aligned output slot and a packed length pass 2 cannot stage (> kFlPieces pieces),
+// or a slot too small for pass 1's piece records. Passes 1 and 2 leave exactly these
+// units alone, so the fallback can run beside them (launch_decode).
+__device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
+                                                 uint64_t out_off, uint64_t cap) {
+    if (P == 0 || (reinterpret_cast<uintptr_t>(out + out_off) & 7)) return false;
+    const uint64_t s = reinterpret_cast<uintptr_t>(in + in_off) & 15;
+    const uint64_t np = (s + P + 15) >> 4, nr = (s + P + 63) >> 6;
+    return !(np <= kFlPieces && cap >= 64 * ((nr + 8) / 8));
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -2132,7 +2167,9 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
         return;
     }
     if (st == kStNeedFull) {
-        status[unit] = st;
+        // the unindexed write pass leaves the unit to the fallback, which owns it from
+        // the start (decode_long_unit); the other passes mark it for their successor
+        if (SIZE_ONLY || RD != kRdNone) status[unit] = st;
         return;
     }
     if (st != ST_OK) {
@@ -2214,6 +2251,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                                                                        uint32_t n, uint8_t* __restrict__ out,
                                                                        const uint64_t* __restrict__ out_off,
                                                                        const uint64_t* __restrict__ out_len,
+                                                                       const uint64_t* __restrict__ out_cap,
                                                                        const int32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFlWaves * kFlPk];
     __shared__ __attribute__((aligned(16))) uint16_t code_all[kFlWaves * (kFlOut + 8)];  // + a dummy slot
@@ -2236,10 +2274,15 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
         m_st = -1;
         if (uu < n) {
             m_in = in_off[uu];
-            m_P = (uint32_t)in_len[uu];
+            const uint64_t P = in_len[uu];
+            m_P = (uint32_t)P;
             m_out = out_off[uu];
-            m_T = (uint32_t)(out_len[uu] >> 3);
-            m_st = status[uu];
+            // the fallback's units (it may be writing their status right now) are skipped
+            // without reading what pass 1 left for them
+            if (!decode_long_unit(in, m_in, P, out, m_out, out_cap[uu])) {
+                m_T = (uint32_t)(out_len[uu] >> 3);
+                m_st = status[uu];
+            }
         }
     };
     auto meta = [&](uint32_t j) {  // the batch's unit j (wave-uniform j)
@@ -2608,25 +2651,82 @@ namespace cpk {
 
 static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) / kWavesPerBlock; }
 
+// Side stream for the long-unit kernels (encode_tiled_kernel, the decode fallback).
+// They select their units by a test on the unit's own lengths, so they need nothing
+// from the main kernels and run beside them: a batch whose few long units would
+// otherwise run alone after the main grid (config C5's tail) overlaps them with it.
+// fork(): the side stream waits for everything already on the caller's stream;
+// join(): the caller's stream waits for the side stream's kernel. One side stream
+// and event pair per device, created on first use; the mutex keeps one caller's
+// record/wait pairs together. Both are capturable into a hipGraph.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static std::mutex g_side_mu;
+static SideStream g_side[64];
+
+class SideLaunch {
+  public:
+    explicit SideLaunch(hipStream_t main) : main_(main), lock_(g_side_mu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+        SideStream& ss = g_side[dev];
+        if (!ss.s) {
+            if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) { ss.s = nullptr; return; }
+            if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
+                (void)hipStreamDestroy(ss.s);
+                ss.s = nullptr;
+                return;
+            }
+        }
+        if (hipEventRecord(ss.fork, main_) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess)
+            return;
+        side_ = &ss;
+    }
+    // the stream the long-unit kernel goes on: the side stream, or the caller's own
+    // when the side stream could not be set up (then the kernels simply serialise)
+    hipStream_t stream() const { return side_ ? side_->s : main_; }
+    hipError_t join() {
+        if (!side_) return hipSuccess;
+        hipError_t e = hipEventRecord(side_->join, side_->s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(main_, side_->join, 0);
+        side_ = nullptr;
+        return e;
+    }
+    ~SideLaunch() { (void)join(); }
+
+  private:
+    hipStream_t main_;
+    std::lock_guard<std::mutex> lock_;
+    SideStream* side_ = nullptr;
+};
+
 hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     // units of more than 512 words: encode_tiled_kernel over a grid that strides the batch
     const uint32_t groups = (n + kWave - 1) / kWave;
+    // (side stream, launched first so the long units start early; the two kernels own
+    // disjoint units: encode_tiled_unit)
     const uint32_t tiled_blocks = min((groups + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    SideLaunch side(stream);
     if (write) {
+        encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off,
+                                                                               out_cap, out_len, status);
         encode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status);
-        encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                        out_cap, out_len, status);
     } else {
+        encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off,
+                                                                                out_cap, out_len, status);
         encode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status);
-        encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                         out_cap, out_len, status);
     }
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    const hipError_t j = side.join();
+    return e != hipSuccess ? e : j;
 }
 
 // Decoder selection, read per launch so tests can exercise every
@@ -2695,20 +2795,25 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     switch (variant) {
         case 0: break;  // wave per unit, below
         case 6: {       // index pass, fill pass, full path for what the first pass declined
+            // the fallback owns the long units from the start (decode_long_unit): it goes
+            // first, on the side stream, beside passes 1 and 2
+            SideLaunch side(stream);
+            decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
+                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
             launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
             decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                               out_off, out_len, status);
-            decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                out_cap, out_len, status);
-            return hipGetLastError();
+                                                                               out_off, out_len, out_cap, status);
+            const hipError_t e = hipGetLastError();
+            const hipError_t j = side.join();
+            return e != hipSuccess ? e : j;
         }
         case 5: {       // checkpoint pass, expansion pass, full path for what the first pass declined
             decode_ckpt_kernel<<<(n + kCkBlock - 1) / kCkBlock, kCkBlock, 0, stream>>>(
                 in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
             decode_expand_kernel<<<(n + kExWaves - 1) / kExWaves, kExBlock, 0, stream>>>(
                 in, in_off, in_len, n, out, out_off, out_len, status);
-            decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                out_cap, out_len, status);
+            decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out,
+                                                                                     out_off, out_cap, out_len, status);
             return hipGetLastError();
         }
         case 3: {
@@ -2731,7 +2836,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
         }
     }
     const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
-    decode_wave_kernel<false><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+    decode_wave_kernel<kWvAll><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                out_len, status);
     return hipGetLastError();
 }
@@ -2779,8 +2884,8 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
     decode_index_kernel<false, kRdGate><<<wv, kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off, out_cap,
                                                                    out_len, status, nullptr);
     decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off,
-                                                                       out_len, status);
-    decode_wave_kernel<true><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
+                                                                       out_len, out_cap, status);
+    decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
                                                                         out_cap, out_len, status);
     return hipGetLastError();
 }
