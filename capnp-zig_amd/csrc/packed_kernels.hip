@@ -622,9 +622,44 @@ __device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t of
            (len >> 3) <= 0xFFFFF000ull;
 }
 
-// Units longer than one tile (encode_tiled_unit). A small grid strides over the
-// batch; each wave tests 64 units per load and encodes the selected units one after
-// another, tile by tile.
+// Long-unit work queue (device memory, filled by select_long_kernel on the side
+// stream) for a batch of n units: q[0] = long units listed, q[1] = next entry to
+// take, q[2] = huge units listed (more than kQHuge bytes in), q[3] unused; the long
+// units at q[4 ..] upwards, the huge ones from q[4 + n - 1] downwards. A worker wave
+// takes entries one at a time (a lane-0 vector atomic), huge units first, so the
+// units that set the tail start first and the rest spread over every worker wave.
+constexpr uint64_t kQHuge = 65536;
+constexpr uint32_t kQHead = 4;
+__device__ __forceinline__ uint32_t queue_listed(const uint32_t* q) { return q[0] + q[2]; }
+__device__ __forceinline__ bool queue_take(uint32_t* q, uint32_t n, uint32_t lane, uint32_t& unit) {
+    uint32_t i = 0;
+    if (lane == 0) i = atomicAdd(q + 1, 1u);
+    i = (uint32_t)__shfl((int)i, 0, kWave);
+    const uint32_t nh = q[2];
+    if (i < nh) {
+        unit = q[kQHead + n - 1 - i];
+        return true;
+    }
+    if (i - nh >= q[0]) return false;
+    unit = q[kQHead + i - nh];
+    return true;
+}
+
+__device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
+                                                 uint64_t out_off, uint64_t cap);
+
+// KIND 0: units encode_tiled_unit selects; 1: units decode_long_unit selects. One
+// thread per unit; a wave appends its selected units with one atomic.
+template <int KIND>
+__global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restrict__ in,
+                                                          const uint64_t* __restrict__ in_off,
+                                                          const uint64_t* __restrict__ in_len, uint32_t n,
+                                                          uint8_t* __restrict__ out,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          const uint64_t* __restrict__ out_cap, uint32_t* q);
+
+// Units longer than one tile (encode_tiled_unit), taken from the long-unit queue
+// and encoded one after another, tile by tile.
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __restrict__ in,
                                                               const uint64_t* __restrict__ in_off,
@@ -633,23 +668,19 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
                                                               const uint64_t* __restrict__ out_off,
                                                               const uint64_t* __restrict__ out_cap,
                                                               uint64_t* __restrict__ out_len,
-                                                              int32_t* __restrict__ status) {
+                                                              int32_t* __restrict__ status, uint32_t* q) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
     __shared__ uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (queue_listed(q) == 0) return;  // no long units (block-uniform)
     if (WRITE) {
         lut[threadIdx.x] = compact_selector(threadIdx.x);
         __syncthreads();
     }
     uint8_t* lds = smem + wave * kEncLds;
-    const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;
-    for (uint32_t ubase = (blockIdx.x * kWavesPerBlock + wave) * kWave; ubase < n; ubase += stride) {
-    const uint32_t u = ubase + lane;
-    uint64_t todo = __ballot(u < n && encode_tiled_unit(in, in_off[u], in_len[u]));
-    while (todo) {  // wave-uniform
-    const uint32_t unit = ubase + (uint32_t)__builtin_ctzll(todo);
-    todo &= todo - 1;
+    uint32_t unit = 0;
+    while (queue_take(q, n, lane, unit)) {  // wave-uniform
     const uint8_t* const src = in + in_off[unit];
     const uint32_t words = (uint32_t)(in_len[unit] >> 3);
     uint64_t ob = 0, cap = 0;
@@ -684,8 +715,36 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
         out_len[unit] = pos;
         status[unit] = (WRITE && !fits) ? ST_SPACE : ST_OK;
     }
-    }  // marked units
-    }  // unit groups
+    }  // queued units
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restrict__ in,
+                                                          const uint64_t* __restrict__ in_off,
+                                                          const uint64_t* __restrict__ in_len, uint32_t n,
+                                                          uint8_t* __restrict__ out,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          const uint64_t* __restrict__ out_cap, uint32_t* q) {
+    const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+    bool p = false;
+    if (u < n) {
+        p = KIND == 0 ? encode_tiled_unit(in, in_off[u], in_len[u])
+                      : decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u]);
+    }
+    const bool huge = p && in_len[u] > kQHuge;
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // long units, then huge units (list layout: queue_take)
+        const bool mine = h ? huge : (p && !huge);
+        const uint64_t m = __ballot(mine);
+        if (m == 0) continue;  // wave-uniform
+        const uint32_t first = (uint32_t)__builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(q + (h ? 2 : 0), (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, (int)first, kWave);
+        const uint32_t i = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (mine) q[h ? kQHead + n - 1 - i : kQHead + i] = u;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1552,8 +1611,6 @@ __device__ uint64_t* cpk_wv_prof;
 // kStNeedFull; kWvLong the units decode_long_unit selects (the indexed decoder's
 // fallback, which owns them from the start and may run beside passes 1 and 2).
 constexpr int kWvAll = 0, kWvMarked = 1, kWvLong = 2;
-__device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
-                                                 uint64_t out_off, uint64_t cap);
 
 template <int SEL>
 __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __restrict__ in,
@@ -1563,7 +1620,7 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
                                                                const uint64_t* __restrict__ out_off,
                                                                const uint64_t* __restrict__ out_cap,
                                                                uint64_t* __restrict__ out_len,
-                                                               int32_t* __restrict__ status) {
+                                                               int32_t* __restrict__ status, uint32_t* q) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
     __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
     __shared__ uint64_t lut[256];  // tag -> v_perm selector that scatters the packed bytes (FF: identity, 00: zero)
@@ -1577,19 +1634,25 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     // then takes only the units it marked kStNeedFull, with a small grid striding
     // over the batch (every other status is final or the fill pass's).
     // The wave tests 64 statuses per load (CK) and walks the marked units in order.
-    constexpr bool CK = SEL != kWvAll;
-    const uint32_t stride = CK ? gridDim.x * kWvWaves * kWave : gridDim.x * kWvWaves;
-    for (uint32_t ubase = CK ? (blockIdx.x * kWvWaves + wave) * kWave : blockIdx.x * kWvWaves + wave; ubase < n;
-         ubase += stride) {
+    // kWvLong: the units come from the long-unit queue (queue_take), one at a time.
+    constexpr bool CK = SEL == kWvMarked;
+    const bool QD = SEL == kWvLong;
+    if (QD && queue_listed(q) == 0) return;  // no long units
+    const uint32_t stride = QD ? 0u : CK ? gridDim.x * kWvWaves * kWave : gridDim.x * kWvWaves;
+    for (uint32_t ubase = QD ? 0u : CK ? (blockIdx.x * kWvWaves + wave) * kWave : blockIdx.x * kWvWaves + wave;
+         ubase < n; ubase += stride) {
     uint64_t todo = 1;
     if (CK) {
         const uint32_t u = ubase + lane;
-        if (SEL == kWvMarked) todo = __ballot(u < n && status[u] == kStNeedFull);
-        else todo = __ballot(u < n && decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u]));
+        todo = __ballot(u < n && status[u] == kStNeedFull);
     }
     while (todo) {  // wave-uniform
-    const uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : ubase;
-    todo &= todo - 1;
+    uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : ubase;
+    if (QD) {
+        if (!queue_take(q, n, lane, unit)) return;  // todo stays set: the next entry
+    } else {
+        todo &= todo - 1;
+    }
     const uint8_t* src = in + in_off[unit];
     const uint64_t P = in_len[unit];
     uint8_t* dstb = out + out_off[unit];
@@ -2662,6 +2725,8 @@ static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) 
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    uint32_t* q = nullptr;  // long-unit queue (queue_take): 2 counters + qcap entries
+    uint64_t qcap = 0;
 };
 static std::mutex g_side_mu;
 static SideStream g_side[64];
@@ -2672,6 +2737,17 @@ class SideLaunch {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
         SideStream& ss = g_side[dev];
+        static const bool concurrent = [] {  // CPK_SIDE_STREAM=0: long units after the main grid
+            const char* e = getenv("CPK_SIDE_STREAM");
+            return !(e && e[0] == '0');
+        }();
+        if (!concurrent) {
+            own_ = ss;
+            own_.s = main_;
+            side_ = &own_;
+            serial_ = &ss;
+            return;
+        }
         if (!ss.s) {
             if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) { ss.s = nullptr; return; }
             if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
@@ -2685,10 +2761,39 @@ class SideLaunch {
             return;
         side_ = &ss;
     }
-    // the stream the long-unit kernel goes on: the side stream, or the caller's own
-    // when the side stream could not be set up (then the kernels simply serialise)
+    // the stream the long-unit kernels go on (valid once queue() succeeded)
     hipStream_t stream() const { return side_ ? side_->s : main_; }
+    // The long-unit queue for a batch of n units, its counters cleared on the side
+    // stream; nullptr when the side stream or the queue cannot be set up. Growing it
+    // waits for the side stream's earlier work (a first call inside a hipGraph capture
+    // that needs to grow it fails: run one batch of that size before capturing).
+    uint32_t* queue(uint32_t n) {
+        if (!side_) return nullptr;
+        if (side_->qcap < n) {
+            if (side_->q) {
+                if (hipStreamSynchronize(side_->s) != hipSuccess) return nullptr;
+                (void)hipFree(side_->q);
+                side_->q = nullptr;
+                side_->qcap = 0;
+            }
+            if (hipMalloc(reinterpret_cast<void**>(&side_->q), (kQHead + (uint64_t)n) * sizeof(uint32_t)) !=
+                hipSuccess) {
+                side_->q = nullptr;
+                return nullptr;
+            }
+            side_->qcap = n;
+        }
+        if (hipMemsetAsync(side_->q, 0, kQHead * sizeof(uint32_t), side_->s) != hipSuccess) return nullptr;
+        return side_->q;
+    }
     hipError_t join() {
+        if (serial_) {  // the queue may have grown: keep it
+            serial_->q = own_.q;
+            serial_->qcap = own_.qcap;
+            serial_ = nullptr;
+            side_ = nullptr;
+            return hipSuccess;
+        }
         if (!side_) return hipSuccess;
         hipError_t e = hipEventRecord(side_->join, side_->s);
         if (e == hipSuccess) e = hipStreamWaitEvent(main_, side_->join, 0);
@@ -2701,6 +2806,8 @@ class SideLaunch {
     hipStream_t main_;
     std::lock_guard<std::mutex> lock_;
     SideStream* side_ = nullptr;
+    SideStream own_;                // serial mode: the caller's stream, the device's queue
+    SideStream* serial_ = nullptr;
 };
 
 hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
@@ -2713,14 +2820,18 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     // disjoint units: encode_tiled_unit)
     const uint32_t tiled_blocks = min((groups + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
     SideLaunch side(stream);
+    uint32_t* const q = side.queue(n);
+    if (!q) return hipErrorOutOfMemory;
+    const hipStream_t ss = side.stream();
+    select_long_kernel<0><<<(n + 255) / 256, 256, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap, q);
     if (write) {
-        encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off,
-                                                                               out_cap, out_len, status);
+        encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                    out_len, status, q);
         encode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status);
     } else {
-        encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off,
-                                                                                out_cap, out_len, status);
+        encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                     out_len, status, q);
         encode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status);
     }
@@ -2798,8 +2909,12 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
             // the fallback owns the long units from the start (decode_long_unit): it goes
             // first, on the side stream, beside passes 1 and 2
             SideLaunch side(stream);
+            uint32_t* const q = side.queue(n);
+            if (!q) return hipErrorOutOfMemory;
+            select_long_kernel<1><<<(n + 255) / 256, 256, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off,
+                                                                             out_cap, q);
             decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
-                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+                in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
             launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
             decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
                                                                                out_off, out_len, out_cap, status);
@@ -2813,7 +2928,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
             decode_expand_kernel<<<(n + kExWaves - 1) / kExWaves, kExBlock, 0, stream>>>(
                 in, in_off, in_len, n, out, out_off, out_len, status);
             decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                                     out_off, out_cap, out_len, status);
+                                                                                     out_off, out_cap, out_len, status, nullptr);
             return hipGetLastError();
         }
         case 3: {
@@ -2837,7 +2952,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     }
     const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
     decode_wave_kernel<kWvAll><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                               out_len, status);
+                                                               out_len, status, nullptr);
     return hipGetLastError();
 }
 
@@ -2886,7 +3001,7 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
     decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off,
                                                                        out_len, out_cap, status);
     decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
-                                                                        out_cap, out_len, status);
+                                                                        out_cap, out_len, status, nullptr);
     return hipGetLastError();
 }
 
