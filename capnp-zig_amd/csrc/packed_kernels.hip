@@ -2163,7 +2163,8 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
             // a finished or failed lane has pos = kIxDead; a read walk stops at the framed length
             const bool act = pos < lim && (RD != kRdWalk || wrun < lim_w);
             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-            const uint8_t* const a = ring + ((act ? pos : 0u) & 127u);
+            // any pos (kIxDead included) reads inside the lane's 144-B ring: no select
+            const uint8_t* const a = ring + (pos & 127u);
             uint32_t t = a[0];
             uint32_t b1 = a[1];
             uint32_t c9 = a[9];
@@ -2174,9 +2175,9 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
             const bool ok = act && !eof;
             st = eof ? ST_EOF : st;
             const uint32_t o = (pos + 16u - ob) & 63u;
-            bits |= ok ? (1ull << o) : 0ull;
+            bits |= (uint64_t)ok << o;
             const uint32_t wd = 1u + (z ? b1 : 0u) + (f ? c9 : 0u);  // <= 256: a piece sums to <= 2048
-            cnt += ok ? ((uint64_t)wd << (16u * (o >> 4))) : 0ull;
+            cnt += (uint64_t)(ok ? wd : 0u) << (o & 48u);            // field o >> 4
             pos = eof ? kIxDead : (ok ? pos + len : pos);
             if (RD == kRdWalk) wrun += ok ? wd : 0u;
         }
