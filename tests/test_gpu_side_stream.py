@@ -1,0 +1,134 @@
+"""Long units on the side stream: encode_tiled_kernel and the decode
+fallback take the long units from a device queue on a per-device side stream, joined
+back into the caller's stream. These tests check that the fork/join orders them with
+the caller's own work:
+- on a caller-created (non-default) stream, with the result read right after a
+  synchronisation of that stream only;
+- back-to-back batches of different long-unit mixes, so a later batch's queue reset
+  cannot overtake an earlier batch's workers;
+- captured into a hipGraph (torch.cuda.graph) and replayed on new data;
+- a batch with no long units and one of long units only (the empty-queue and
+  all-queue ends).
+Every unit is checked against the oracle (message.zig:200-271 / 88-145) or by
+decode(encode(x)) == x.
+"""
+import numpy as np
+import pytest
+
+import capnp_packed as cp
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def mixed_sizes(n, seed, long_every=7, huge_every=61):
+    rng = np.random.default_rng(seed)
+    sizes = (rng.integers(1, 512, n) * 8).astype(np.int64)            # one tile
+    sizes[::long_every] = rng.integers(513, 8192, len(sizes[::long_every])) * 8  # tiled / fallback
+    sizes[::huge_every] = rng.integers(8193, 24576, len(sizes[::huge_every])) * 8  # > 64 KiB: front of the queue
+    return sizes
+
+
+class Batch:
+    def __init__(self, sizes, seed, thr=128):
+        n = len(sizes)
+        self.n = n
+        self.sizes = torch.from_numpy(sizes).to(DEV)
+        self.in_off = torch.zeros(n, dtype=torch.int64, device=DEV)
+        self.in_off[1:] = torch.cumsum(self.sizes, 0)[:-1]
+        self.U = int(sizes.sum())
+        self.seed, self.thr = seed, thr
+        self.d_in = cp.generate(1, self.U, seed=seed, zero_thresh=thr, device=DEV)
+        self.cap = (self.sizes // 8) * 10
+        slots = (self.cap + 15) // 16 * 16
+        self.pk_off = torch.zeros(n, dtype=torch.int64, device=DEV)
+        self.pk_off[1:] = torch.cumsum(slots, 0)[:-1]
+        self.d_pk = torch.zeros(int(slots.sum().item()), dtype=torch.uint8, device=DEV)
+        self.plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+        self.pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+        self.d_out = torch.zeros(self.U, dtype=torch.uint8, device=DEV)
+        self.ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
+        self.ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+
+    def run(self, stream=None):
+        cp.encode_batch(self.d_in, self.in_off, self.sizes, self.d_pk, self.pk_off, self.cap, self.plen, self.pst,
+                        stream=stream)
+        cp.decode_batch(self.d_pk, self.pk_off, self.plen, self.d_out, self.in_off, self.sizes, self.ulen, self.ust,
+                        stream=stream)
+
+    def check_roundtrip(self):
+        assert (self.pst == 0).all().item() and (self.ust == 0).all().item()
+        assert torch.equal(self.ulen, self.sizes)
+        assert torch.equal(self.d_out, self.d_in)
+
+    def check_oracle(self, units):
+        h_in = self.d_in.cpu().numpy()
+        pk = self.d_pk.cpu().numpy()
+        plen, off, pko = self.plen.cpu().numpy(), self.in_off.cpu().numpy(), self.pk_off.cpu().numpy()
+        sz = self.sizes.cpu().numpy()
+        for i in units:
+            st, exp = oracle.pack(h_in[off[i]:off[i] + sz[i]].tobytes())
+            assert st == oracle.OK and int(plen[i]) == len(exp), f"unit {i} ({sz[i]} B): packed length"
+            assert pk[pko[i]:pko[i] + len(exp)].tobytes() == exp, f"unit {i} ({sz[i]} B): packed bytes"
+
+
+def test_side_stream_on_caller_stream():
+    b = Batch(mixed_sizes(3000, 1), seed=0xC0DE0101)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.run(stream=s)
+    s.synchronize()  # only the caller's stream: the join must cover the side work
+    b.check_roundtrip()
+    long_units = [i for i, x in enumerate(b.sizes.cpu().numpy()) if x > 4096]
+    b.check_oracle(long_units[:200] + list(range(0, 3000, 97)))
+
+
+@pytest.mark.parametrize("thr", [26, 128, 230])
+def test_back_to_back_batches(thr):
+    # three batches, launched without synchronisation in between: each batch resets the
+    # shared queue on the side stream after the previous batch's workers
+    bs = [Batch(mixed_sizes(n, 10 + k, long_every=le), seed=0xC0DE0200 + k, thr=thr)
+          for k, (n, le) in enumerate([(2000, 5), (700, 2), (4000, 1000)])]
+    for b in bs:
+        b.run()
+    torch.cuda.synchronize()
+    for b in bs:
+        b.check_roundtrip()
+    bs[1].check_oracle(range(0, 700, 3))
+
+
+def test_no_long_units_and_only_long_units():
+    short = Batch(np.full(5000, 4096, dtype=np.int64), seed=0xC0DE0301)
+    only = Batch((np.arange(1, 65) * 4104).astype(np.int64), seed=0xC0DE0302)
+    short.run()
+    only.run()
+    torch.cuda.synchronize()
+    short.check_roundtrip()
+    only.check_roundtrip()
+    only.check_oracle(range(64))
+
+
+def test_graph_capture_replay():
+    b = Batch(mixed_sizes(1500, 3), seed=0xC0DE0401)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.run(stream=s)  # warm-up: sizes the device queue before capture
+    s.synchronize()
+    b.check_roundtrip()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.run()
+    # new data in the same buffers, then replay the captured encode + decode
+    cp.generate(1, b.U, seed=0xC0DE0402, zero_thresh=128, out=b.d_in, device=DEV)
+    b.pst.fill_(-1)
+    b.ust.fill_(-1)
+    b.d_out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    b.check_roundtrip()
+    long_units = [i for i, x in enumerate(b.sizes.cpu().numpy()) if x > 4096]
+    b.check_oracle(long_units[:100])
