@@ -20,6 +20,10 @@
  * Threading: all functions are thread-safe. The single-buffer host functions
  * serialise on one internal device context; batch functions are reentrant for
  * distinct streams. One-time device init is guarded by std::call_once.
+ * encode/encoded_size/decode batches put their long units (more than 4 KiB in;
+ * packed units beyond the fast decoder's window) on an internal per-device side
+ * stream that is forked from and joined back into `stream` inside the call, so
+ * ordering on `stream` is as if everything ran on it.
  */
 #ifndef CAPNP_PACKED_H
 #define CAPNP_PACKED_H
@@ -107,8 +111,10 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
  *
  * `stream` is a hipStream_t (NULL = default stream). Calls are asynchronous:
  * they enqueue kernels and return. The return value reports launch errors only;
- * per-unit results are in d_status / d_out_len. Nothing is allocated inside, so
- * the calls can be captured in a hipGraph.
+ * per-unit results are in d_status / d_out_len. The only allocation is the
+ * per-device long-unit queue (4 B per unit), made or grown when a batch is larger
+ * than any earlier one on that device: run one batch of the largest size before
+ * capturing calls into a hipGraph (capture then works, tests/test_gpu_side_stream.py).
  * ------------------------------------------------------------------------ */
 
 /* Batch packPacked (message.zig:200-271), one unit = one packPacked call. */
