@@ -2026,9 +2026,9 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 // chain once (message.zig:152-191), lockstep by 64-B input block. Every byte is
 // fetched from HBM once: round k's loads are quad-coalesced (4 lanes x 16 B = one
 // unit's 64-B block, 16 units per instruction), issued one round ahead into
-// registers, and written to the lane-major LDS ring: unit u keeps blocks k-1 and
-// k at ring_u + (k & 1) * 64 (plus a mirror of the even block's first 16 B at
-// +128, for reads that wrap). Round k walks the tags in [64k - 16, 64k + 48), i.e.
+// registers, and written to the lane-major LDS ring: unit u keeps block k at
+// ring_u + 16 and block k-1's last 16 B at ring_u (moved there by u's lane at the
+// start of round k): 80 B per lane. Round k walks the tags in [64k - 16, 64k + 48), i.e.
 // pieces 4k-1 .. 4k+2, whose count bytes (+1, +9) are all resident; a final round
 // (k = rounds) walks the last piece.
 //
@@ -2056,7 +2056,7 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
     uint64_t* __restrict__ consumed) {
     static_assert(RD != kRdWalk || SIZE_ONLY, "the read walk writes no output");
     static_assert(RD != kRdGate || !SIZE_ONLY, "the gated pass is the write pass");
-    constexpr uint32_t kRing = 144;  // two 64-B blocks + 16-B mirror
+    constexpr uint32_t kRing = 80;  // [0, 16): block k-1's last piece, [16, 80): block k
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWave * kRing];
     const uint32_t lane = lane_id();
     const uint32_t unit = blockIdx.x * kWave + lane;
@@ -2123,8 +2123,8 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
         d2 = qsrc[2][min(4 * k + qp, qlast[2])];
         d3 = qsrc[3][min(4 * k + qp, qlast[3])];
     };
-    uint8_t* const wq = ring_all + (lane / 4) * kRing + 16 * qp;  // unit 16m + l/4: + 16 * kRing * m
-    const uint8_t* const ring = ring_all + lane * kRing;
+    uint8_t* const wq = ring_all + (lane / 4) * kRing + 16 + 16 * qp;  // unit 16m + l/4: + 16 * kRing * m
+    uint8_t* const ring = ring_all + lane * kRing;
 
     uint32_t pos = take ? s : kIxDead;  // next tag (aligned space)
     uint64_t words = 0;                 // decoded words so far
@@ -2140,18 +2140,19 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
             // k-1 when it flushed (k-1 = 7 mod 8)
             if (!SIZE_ONLY && (k & 7) == 0 && k > 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            wave_lds_sync();  // every lane is done with block k-2's half of the ring
-            uint8_t* const w = wq + (k & 1) * 64;
-            *reinterpret_cast<uint4*>(w) = d0;
-            *reinterpret_cast<uint4*>(w + 16 * kRing) = d1;
-            *reinterpret_cast<uint4*>(w + 32 * kRing) = d2;
-            *reinterpret_cast<uint4*>(w + 48 * kRing) = d3;
-            if (!(k & 1) && qp == 0) {  // mirror of the even block's first piece
-                *reinterpret_cast<uint4*>(w + 128) = d0;
-                *reinterpret_cast<uint4*>(w + 128 + 16 * kRing) = d1;
-                *reinterpret_cast<uint4*>(w + 128 + 32 * kRing) = d2;
-                *reinterpret_cast<uint4*>(w + 128 + 48 * kRing) = d3;
-            }
+        }
+        if (k > 0) {
+            wave_lds_sync();  // every lane is done with round k-1's reads
+            // the lane's own ring: block k-1's last piece moves to the front (round k
+            // reads it for tags in piece 4k-1; the final round k = maxr too)
+            *reinterpret_cast<uint4*>(ring) = *reinterpret_cast<const uint4*>(ring + 64);
+            wave_lds_sync();  // before the quad writes below overwrite ring + 64
+        }
+        if (k < maxr) {
+            *reinterpret_cast<uint4*>(wq) = d0;
+            *reinterpret_cast<uint4*>(wq + 16 * kRing) = d1;
+            *reinterpret_cast<uint4*>(wq + 32 * kRing) = d2;
+            *reinterpret_cast<uint4*>(wq + 48 * kRing) = d3;
             if (k + 1 < maxr) load(k + 1);
             wave_lds_sync();
         }
@@ -2163,8 +2164,9 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
             // a finished or failed lane has pos = kIxDead; a read walk stops at the framed length
             const bool act = pos < lim && (RD != kRdWalk || wrun < lim_w);
             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-            // any pos (kIxDead included) reads inside the lane's 144-B ring: no select
-            const uint8_t* const a = ring + (pos & 127u);
+            // ring offset o = pos + 16 - ob: block k-1's last piece at [0, 16), block k at
+            // [16, 80); any pos (kIxDead, or past lim) reads inside the lane's ring
+            const uint8_t* const a = ring + ((pos + 16u - ob) & 63u);
             uint32_t t = a[0];
             uint32_t b1 = a[1];
             uint32_t c9 = a[9];
