@@ -20,6 +20,8 @@ import ctypes
 import os
 import struct
 
+import numpy as np
+
 try:  # load torch first so libcapnp_packed.so binds to the same HIP runtime instance
     import torch
 except ImportError:  # pragma: no cover - the ABI still loads for symbol checks
@@ -358,6 +360,132 @@ def read_packed_message_bytes(data) -> tuple:
         _raise(st, "readPackedMessage")
         return out.raw[:n.value], used.value
     raise OutOfSpace("readPackedMessage: framed length grew between calls")
+
+
+# ---------------------------------------------------------------------------
+# Framing for packed byte streams
+# ---------------------------------------------------------------------------
+
+class PackedFramer:
+    """The RPC `Framer` (src/rpc/level0/framing.zig:4-90) for a PACKED byte stream.
+    It has the same surface: push / buffered_bytes / reset / pop_frame.
+    - push() appends a socket read.
+    - pop_frame() returns the framed (unpacked) bytes of the next whole message, or None
+      while the buffered bytes do not hold one yet (the reader's EndOfStream).
+    - pop_frame() raises the reader's other errors (reader.zig:84-156). The caller then
+      reset()s, as Connection.handleRead does (level2/connection.zig:175-184).
+    - A message's end is only known by decoding its packed records. So pop_frame runs
+      Reader.readPackedMessage on the device through the single-buffer C-ABI.
+    - PackedConnections batches this across many connections."""
+
+    max_frame_words = 8 * 1024 * 1024  # framing.zig:5 / reader.zig:6
+    max_segment_count = MAX_SEGMENT_COUNT
+
+    def __init__(self):
+        self.buffer = bytearray()
+
+    def push(self, data) -> None:
+        if len(data):
+            self.buffer += bytes(data)
+
+    def buffered_bytes(self) -> int:
+        return len(self.buffer)
+
+    def reset(self) -> None:
+        self.buffer.clear()
+
+    def pop_frame(self):
+        if not self.buffer:
+            return None
+        try:
+            framed, used = read_packed_message_bytes(self.buffer)
+        except EndOfStream:
+            return None
+        del self.buffer[:used]
+        return framed
+
+
+class PackedConnections:
+    """Connection.handleRead (src/rpc/level2/connection.zig:153-203) over many
+    connections at once. Each connection has its own PackedFramer buffer.
+    - handle_read(reads) pushes every connection's socket read, copies the buffered
+      bytes to the device once, and pops frames in rounds. Each round is one
+      read_message_batch with one unit per connection that may still hold a message.
+    - Per connection, the result is the list of frames popped (in order), or a PackedError.
+    - On the error the connection's framer is reset and the connection is closed for
+      further reads, as handleRead does (175-184). Frames popped before the error are
+      dropped with it; handleRead would already have delivered them, so
+      `frames_before_error` keeps them.
+    - A connection whose buffer ends inside a message keeps those bytes for its next read
+      (the reader's EndOfStream = popFrame's null)."""
+
+    def __init__(self, n_conns: int, device="cuda"):
+        self.framers = [PackedFramer() for _ in range(n_conns)]
+        self.closed = [False] * n_conns
+        self.frames_before_error = {}
+        self.device = torch.device(device)
+
+    def handle_read(self, reads: dict) -> dict:
+        for c, data in reads.items():
+            if not self.closed[c]:
+                self.framers[c].push(data)
+        conns = [c for c in range(len(self.framers)) if not self.closed[c] and self.framers[c].buffered_bytes()]
+        result = {c: [] for c in conns}
+        if not conns:
+            return result
+        dev = self.device
+        lens = np.array([self.framers[c].buffered_bytes() for c in conns], dtype=np.int64)
+        base = np.zeros(len(conns), dtype=np.int64)
+        base[1:] = np.cumsum(lens)[:-1]
+        host = np.frombuffer(b"".join(bytes(self.framers[c].buffer) for c in conns), dtype=np.uint8)
+        d_in = torch.from_numpy(host.copy()).to(dev) if host.size else torch.zeros(1, dtype=torch.uint8, device=dev)
+        used = np.zeros(len(conns), dtype=np.int64)  # packed bytes popped so far, per connection
+        live = np.ones(len(conns), dtype=bool)
+        cap = np.maximum(4096, 8 * lens)  # first guess at each frame's size; grown on OutOfSpace
+        while True:
+            idx = np.nonzero(live & (used < lens))[0]
+            if idx.size == 0:
+                break
+            k = idx.size
+            in_off = torch.from_numpy(base[idx] + used[idx]).to(dev)
+            in_len = torch.from_numpy(lens[idx] - used[idx]).to(dev)
+            caps = (cap[idx] + 7) // 8 * 8
+            out_off_h = np.zeros(k, dtype=np.int64)
+            out_off_h[1:] = np.cumsum(caps)[:-1]
+            out_off = torch.from_numpy(out_off_h).to(dev)
+            out_cap = torch.from_numpy(caps).to(dev)
+            d_out = torch.empty(int(caps.sum()), dtype=torch.uint8, device=dev)
+            out_len = torch.zeros(k, dtype=torch.int64, device=dev)
+            consumed = torch.zeros(k, dtype=torch.int64, device=dev)
+            status = torch.zeros(k, dtype=torch.int32, device=dev)
+            read_message_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, consumed, status)
+            st = status.cpu().numpy()
+            ol = out_len.cpu().numpy()
+            cons = consumed.cpu().numpy()
+            grow = st == OUT_OF_SPACE
+            if grow.any():  # redo the round with the framed lengths the reader reported
+                cap[idx[grow]] = np.maximum(cap[idx[grow]] * 2, ol[grow])
+                continue
+            out_h = d_out.cpu().numpy() if (st == OK).any() else None
+            for j, i in enumerate(idx):
+                c = conns[i]
+                if st[j] == OK:
+                    result[c].append(out_h[out_off_h[j]:out_off_h[j] + ol[j]].tobytes())
+                    used[i] += cons[j]
+                elif st[j] == END_OF_STREAM:
+                    live[i] = False  # the rest waits for the next read
+                else:
+                    live[i] = False
+                    err = _ERRORS.get(int(st[j]), DeviceError)(
+                        f"readPackedMessage: {lib().capnp_packed_status_name(int(st[j])).decode()}")
+                    self.frames_before_error[c] = result[c]
+                    result[c] = err
+                    self.framers[c].reset()
+                    self.closed[c] = True
+        for i, c in enumerate(conns):
+            if not self.closed[c]:
+                del self.framers[c].buffer[:int(used[i])]
+        return result
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,131 @@
+"""framing packed byte streams as they come off a socket.
+`PackedFramer` mirrors the RPC Framer (src/rpc/level0/framing.zig:4-90: push /
+bufferedBytes / reset / popFrame) for a packed stream. `PackedConnections` runs
+Connection.handleRead (src/rpc/level2/connection.zig:153-203) for many connections in
+one device batch per round.
+
+The expected frames are the framed messages the streams were built from. Every popped
+frame and error is also checked against the oracle's restatement of
+Reader.readPackedMessage (reader.zig:84-156), applied to the same buffered bytes.
+"""
+import numpy as np
+import pytest
+
+import capnp_packed as cp
+import oracle
+import pyref
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+# oracle_read_packed_message's codes -> the C-ABI statuses (as in test_gpu_read_message.py)
+ORACLE_TO_ABI = {0: cp.OK, -1: cp.END_OF_STREAM, -2: cp.INVALID_SEGMENT_COUNT,
+                 -3: cp.SEGMENT_COUNT_LIMIT_EXCEEDED, -6: cp.MESSAGE_TOO_LARGE, -7: cp.INVALID_PACKED_MESSAGE}
+
+
+def random_message(rng):
+    segs = []
+    for _ in range(int(rng.integers(1, 5))):
+        n = 8 * int(rng.integers(0, 160))
+        b = rng.integers(0, 256, n).astype(np.uint8)
+        b[rng.random(n) < rng.choice([0.1, 0.5, 0.9])] = 0
+        segs.append(b.tobytes())
+    return pyref.frame(segs)
+
+
+def make_stream(rng, n_msgs):
+    msgs = [random_message(rng) for _ in range(n_msgs)]
+    packed = []
+    for f in msgs:
+        st, p = oracle.pack(f)
+        assert st == oracle.OK
+        packed.append(p)
+    return msgs, packed
+
+
+def oracle_frames(data: bytes):
+    """Pop frames from `data` with the oracle reader until it stops: (frames, rest, code)."""
+    frames = []
+    while data:
+        rc, framed, used = oracle.read_packed_message(data, cap=1 << 22)
+        if rc != 0:
+            return frames, data, ORACLE_TO_ABI[rc]
+        frames.append(framed)
+        data = data[used:]
+    return frames, data, cp.OK
+
+
+def chunks(rng, data: bytes, k: int):
+    cut = sorted(rng.integers(0, len(data) + 1, k - 1).tolist()) if len(data) else [0] * (k - 1)
+    edges = [0] + cut + [len(data)]
+    return [data[edges[i]:edges[i + 1]] for i in range(k)]
+
+
+def test_packed_framer_socket_reads():
+    rng = np.random.default_rng(0xF4A3)
+    msgs, packed = make_stream(rng, 24)
+    stream = b"".join(packed)
+    f = cp.PackedFramer()
+    got = []
+    for piece in chunks(rng, stream, 40):  # socket reads of arbitrary sizes
+        f.push(piece)
+        while True:
+            fr = f.pop_frame()
+            if fr is None:
+                break
+            got.append(fr)
+    assert got == msgs and f.buffered_bytes() == 0
+    # a read that ends inside a message keeps the bytes (popFrame's null)
+    f.push(packed[0][:-1])
+    assert f.pop_frame() is None and f.buffered_bytes() == len(packed[0]) - 1
+    f.push(packed[0][-1:])
+    assert f.pop_frame() == msgs[0]
+
+
+def test_packed_framer_error_then_reset():
+    rng = np.random.default_rng(7)
+    msgs, packed = make_stream(rng, 2)
+    bad = bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF])  # segment count - 1 = 0xFFFFFFFF
+    rc, _, _ = oracle.read_packed_message(bad + packed[1], cap=1 << 20)
+    rc = ORACLE_TO_ABI[rc]
+    assert rc == cp.INVALID_SEGMENT_COUNT
+    f = cp.PackedFramer()
+    f.push(packed[0] + bad + packed[1])
+    assert f.pop_frame() == msgs[0]
+    with pytest.raises(cp.PackedError) as e:
+        f.pop_frame()
+    assert e.value.status == rc
+    f.reset()  # Connection.handleRead resets the framer after a framing error
+    assert f.buffered_bytes() == 0 and f.pop_frame() is None
+
+
+@pytest.mark.parametrize("n_conns", [1, 48])
+def test_packed_connections_batched(n_conns):
+    rng = np.random.default_rng(0xC0 + n_conns)
+    bad = bytes([0x03, 0x57, 0x02])  # segment count 600 > 512
+    streams, expect = [], []
+    for c in range(n_conns):
+        msgs, packed = make_stream(rng, int(rng.integers(0, 7)))
+        data = b"".join(packed)
+        if c % 11 == 5 and msgs:  # a corrupt connection: one good message, then garbage
+            data = packed[0] + bad + b"".join(packed[1:])
+        streams.append(data)
+        expect.append(oracle_frames(data))
+    conns = cp.PackedConnections(n_conns)
+    reads = [chunks(rng, s, 4) for s in streams]
+    delivered = [[] for _ in range(n_conns)]
+    errors = {}
+    for r in range(4):
+        res = conns.handle_read({c: reads[c][r] for c in range(n_conns)})
+        for c, v in res.items():
+            if isinstance(v, cp.PackedError):
+                errors[c] = v
+                delivered[c] += conns.frames_before_error.get(c, [])
+            else:
+                delivered[c] += v
+    for c in range(n_conns):
+        frames, rest, rc = expect[c]
+        assert delivered[c] == frames, f"connection {c}"
+        if rc in (cp.OK, cp.END_OF_STREAM):
+            assert c not in errors and conns.framers[c].buffered_bytes() == (len(rest) if rc else 0)
+        else:
+            assert errors[c].status == rc and conns.closed[c] and conns.framers[c].buffered_bytes() == 0
