@@ -16,6 +16,7 @@ Run: python bench.py [--gpus N --steps K --warmup W]
 """
 import argparse
 import json
+import struct
 import os
 import sys
 import time
@@ -287,6 +288,49 @@ def skewed_leg(args, dev, n=1 << 20, reps=10):
             "note": "SURVEY config C5: truncated Pareto unit sizes 64 B..256 KiB, p = zero_thresh/256"}
 
 
+def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
+    """SURVEY §8(f) row 3, RPC framer batching: `conns` connections, each with one socket
+    read holding `msgs` packed 1-segment messages (framed 4096 B, p = zero_thresh/256).
+    PackedConnections.handle_read pops every frame: one read_message_batch per round, one
+    unit per connection, H2D of the buffered bytes and D2H of the frames included (a
+    host-memory path: reported beside `value`, never as it)."""
+    n = conns * msgs
+    words = 511
+    d_fr = cp.generate(n, 4096, seed=0xC0DE0007, zero_thresh=args.zero_thresh, device=dev)
+    hdr = torch.tensor(list(struct.pack("<II", 0, words)), dtype=torch.uint8, device=dev)
+    d_fr.view(n, 4096)[:, :8] = hdr
+    off, ln = cp.uniform_layout(n, 4096, device=dev)
+    slot = cp.encode_bound(4096)
+    pk_off, pk_cap = cp.uniform_layout(n, slot, device=dev)
+    d_pk = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    plen = torch.zeros(n, dtype=torch.int64, device=dev)
+    pst = torch.zeros(n, dtype=torch.int32, device=dev)
+    cp.encode_batch(d_fr, off, ln, d_pk, pk_off, pk_cap, plen, pst)
+    torch.cuda.synchronize()
+    pk_h, pl_h, fr_h = d_pk.cpu().numpy(), plen.cpu().numpy(), d_fr.cpu().numpy()
+    streams = {c: b"".join(pk_h[i * slot:i * slot + int(pl_h[i])].tobytes() for i in range(c * msgs, (c + 1) * msgs))
+               for c in range(conns)}
+    packed_bytes = sum(len(v) for v in streams.values())
+    best, ok = None, True
+    for _ in range(reps):
+        pc = cp.PackedConnections(conns, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = pc.handle_read(streams)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+        for c in (0, conns // 2, conns - 1):
+            fr = res[c]
+            ok &= isinstance(fr, list) and len(fr) == msgs and all(
+                fr[k] == fr_h[(c * msgs + k) * 4096:(c * msgs + k + 1) * 4096].tobytes() for k in range(msgs))
+        ok &= all(isinstance(v, list) and len(v) == msgs for v in res.values())
+    return {"connections": conns, "messages_per_read": msgs, "framed_bytes": 4096, "packed_bytes": packed_bytes,
+            "ms": round(best * 1e3, 2), "framed_GiB_s": round(n * 4096 / best / 2 ** 30, 2),
+            "frames_per_s": round(n / best), "bit_exact": bool(ok),
+            "note": "host buffers in and out (PCIe + host-side framing), rounds of read_message_batch"}
+
+
 def message_leg(args, dev, reps=10, segs=4, seg_words=127):
     """SURVEY §8(f) row 2, framing fused with the codec: 1M messages of 4 segments x
     127 words (framed 4088 B) from a segment pool, packed straight from the segment
@@ -448,6 +492,9 @@ def main():
     if world == 1 and not args.no_skewed:
         torch.cuda.empty_cache()
         extra["c5_skewed"] = skewed_leg(args, dev)
+    if world == 1 and not args.no_read_message:
+        torch.cuda.empty_cache()
+        extra["rpc_framer"] = framer_leg(args, dev)
 
     if rank == 0:
         steps = args.steps

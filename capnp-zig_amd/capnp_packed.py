@@ -423,6 +423,7 @@ class PackedConnections:
         self.framers = [PackedFramer() for _ in range(n_conns)]
         self.closed = [False] * n_conns
         self.frames_before_error = {}
+        self._last = {}  # connection -> its last frame's size (the next round's slot guess)
         self.device = torch.device(device)
 
     def handle_read(self, reads: dict) -> dict:
@@ -441,7 +442,11 @@ class PackedConnections:
         d_in = torch.from_numpy(host.copy()).to(dev) if host.size else torch.zeros(1, dtype=torch.uint8, device=dev)
         used = np.zeros(len(conns), dtype=np.int64)  # packed bytes popped so far, per connection
         live = np.ones(len(conns), dtype=bool)
-        cap = np.maximum(4096, 8 * lens)  # first guess at each frame's size; grown on OutOfSpace
+        # first guess at each frame's size: the connection's last frame (8 KiB at first), at
+        # most 8x its buffered bytes; a round that reports OutOfSpace is redone with the
+        # framed length the reader found
+        cap = np.array([min(self._last.get(c, 8192), max(8, 8 * int(n))) for c, n in zip(conns, lens)],
+                       dtype=np.int64)
         while True:
             idx = np.nonzero(live & (used < lens))[0]
             if idx.size == 0:
@@ -472,6 +477,8 @@ class PackedConnections:
                 if st[j] == OK:
                     result[c].append(out_h[out_off_h[j]:out_off_h[j] + ol[j]].tobytes())
                     used[i] += cons[j]
+                    cap[i] = max(8, int(ol[j]))
+                    self._last[c] = cap[i]
                 elif st[j] == END_OF_STREAM:
                     live[i] = False  # the rest waits for the next read
                 else:
