@@ -69,6 +69,8 @@ constexpr int32_t kStNeedFull = 0x7FFF0001;
 // small device helpers
 // ---------------------------------------------------------------------------
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // Order LDS traffic between lanes of ONE wave (the wave owns its LDS slice).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -535,7 +537,9 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
             if (c < nch_out) {
                 uint32_t cb = 16 * c, ce = cb + 16;
                 if (cb >= lo && ce <= hi) {
-                    *reinterpret_cast<uint4*>(gdst + cb) = *reinterpret_cast<const uint4*>(lds + cb);
+                    // streaming output: non-temporal (nothing re-reads it from L2 in this pass)
+                    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + cb),
+                                                reinterpret_cast<u32x4*>(gdst + cb));
                 } else {
                     uint32_t a = max(cb, lo), e = min(ce, hi);
                     for (uint32_t b = a; b < e; ++b) gdst[b] = lds[b];
@@ -2014,7 +2018,6 @@ __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_
     return !(np <= kFlPieces && cap >= 64 * ((nr + 8) / 8));
 }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // 16 readable bytes for load lanes that have nothing to stage, and 16 writable
 // bytes for the piece-record stores of lanes without a unit.
@@ -2489,8 +2492,10 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                         const uint32_t cc = *reinterpret_cast<const uint32_t*>(code + i);
                         const uint64_t x0 = fill_word(pk, lut, cc & 0xFFFFu);
                         const uint64_t x1 = fill_word(pk, lut, cc >> 16);
-                        if (i + 1 < nw) *reinterpret_cast<uint4*>(dst + W0 + i) =
-                            make_uint4((uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32));
+                        if (i + 1 < nw) {  // streaming output: non-temporal
+                            const u32x4 v = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
+                            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + W0 + i));
+                        }
                         else dst[W0 + i] = x0;
                     }
                     younger += (nw + 2 * kWave - 1) / (2 * kWave);
