@@ -1847,7 +1847,7 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
                             word = gload_u64_unaligned(g + q + 1);
                         }
                     }
-                    o[i] = word;
+                    __builtin_nontemporal_store(word, o + i);  // streaming output (as the fill pass)
                 }
             }
         }
