@@ -129,6 +129,11 @@ SIGNATURES = {
     "capnp_packed_encode_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "capnp_packed_encoded_size_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
     "capnp_packed_decode_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "capnp_packed_batch_workspace_bytes": (_sz, [ctypes.c_uint32]),
+    "capnp_packed_encode_batch_ws": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                    _sz, _vp]),
+    "capnp_packed_decode_batch_ws": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                    _sz, _vp]),
     "capnp_packed_decoded_size_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
     "capnp_packed_read_message_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
                                                        _vp, _vp]),
@@ -519,13 +524,31 @@ def _units(in_off, *per_unit) -> int:
     return n
 
 
-def encode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None) -> None:
+def workspace(n_units: int, device="cuda"):
+    """Device workspace for the *_batch_ws calls (capnp_packed_batch_workspace_bytes):
+    a batch that uses its own workspace shares no library state, so a captured
+    hipGraph of it may replay beside any other work."""
+    nbytes = lib().capnp_packed_batch_workspace_bytes(n_units)
+    return torch.empty((nbytes + 7) // 8, dtype=torch.int64, device=device)
+
+
+def _ws(ws):
+    return (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
+
+
+def encode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None, ws=None) -> None:
     """Batch packPacked: unit i = d_in[in_off[i] : in_off[i]+in_len[i]] -> slot
-    d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit."""
+    d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit.
+    ws: optional workspace() tensor (capnp_packed_encode_batch_ws)."""
     n = _units(in_off, in_len, out_off, out_cap, out_len, status)
-    _raise(lib().capnp_packed_encode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out), _ptr(out_off),
-                                           _ptr(out_cap), _ptr(out_len), _ptr(status), _stream(stream)),
-           "encode_batch")
+    if ws is None:
+        _raise(lib().capnp_packed_encode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
+                                               _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(status),
+                                               _stream(stream)), "encode_batch")
+    else:
+        _raise(lib().capnp_packed_encode_batch_ws(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
+                                                  _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(status),
+                                                  *_ws(ws), _stream(stream)), "encode_batch_ws")
 
 
 def encoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> None:
@@ -534,13 +557,19 @@ def encoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> No
                                                  _ptr(status), _stream(stream)), "encoded_size_batch")
 
 
-def decode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None) -> None:
+def decode_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, status, stream=None, ws=None) -> None:
     """Batch unpackPacked: unit i = d_in[in_off[i] : in_off[i]+in_len[i]] -> slot
-    d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit."""
+    d_out[out_off[i] : out_off[i]+out_cap[i]]; out_len[i], status[i] per unit.
+    ws: optional workspace() tensor (capnp_packed_decode_batch_ws)."""
     n = _units(in_off, in_len, out_off, out_cap, out_len, status)
-    _raise(lib().capnp_packed_decode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out), _ptr(out_off),
-                                           _ptr(out_cap), _ptr(out_len), _ptr(status), _stream(stream)),
-           "decode_batch")
+    if ws is None:
+        _raise(lib().capnp_packed_decode_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
+                                               _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(status),
+                                               _stream(stream)), "decode_batch")
+    else:
+        _raise(lib().capnp_packed_decode_batch_ws(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, _ptr(d_out),
+                                                  _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(status),
+                                                  *_ws(ws), _stream(stream)), "decode_batch_ws")
 
 
 def decoded_size_batch(d_in, in_off, in_len, out_len, status, stream=None) -> None:

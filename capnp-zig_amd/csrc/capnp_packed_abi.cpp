@@ -8,6 +8,7 @@
 // compute entry point returns CAPNP_PACKED_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -84,6 +85,7 @@ struct HostCtx {
     }
     int reserve(uint8_t** p, size_t* cap, size_t need) {
         if (need <= *cap && *p) return CAPNP_PACKED_OK;
+        if (need > (SIZE_MAX / 3) * 2) return fail(CAPNP_PACKED_OUT_OF_SPACE, "workspace size overflows size_t");
         size_t want = need < 4096 ? 4096 : need + need / 2;
         if (*p) (void)hipFree(*p);
         *p = nullptr;
@@ -103,6 +105,7 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
                uint64_t* used_out = nullptr) {
     int st = g_ctx.init();
     if (st) return st;
+    if (n > SIZE_MAX - 16 || slot > SIZE_MAX - 16) return fail(CAPNP_PACKED_OUT_OF_SPACE, "buffer size overflows size_t");
     if ((st = g_ctx.reserve(&g_ctx.d_in, &g_ctx.in_cap, n + 16))) return st;
     const bool write = (kind == 0 || kind == 1 || kind == 4);
     if (write && (st = g_ctx.reserve(&g_ctx.d_out, &g_ctx.out_cap, slot + 16))) return st;
@@ -115,11 +118,13 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
     uint64_t* m = g_ctx.d_meta;
     int32_t* d_status = reinterpret_cast<int32_t*>(m + 5);
     if (kind == 0 || kind == 3)
-        e = cpk::launch_encode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
+        e = cpk::launch_encode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, nullptr, 0,
+                               s);
     else if (kind == 4)
         e = cpk::launch_read_message(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, m + 6, d_status, s);
     else
-        e = cpk::launch_decode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
+        e = cpk::launch_decode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, nullptr, 0,
+                               s);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     e = hipMemcpyAsync(meta, g_ctx.d_meta, sizeof(meta), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -222,15 +227,27 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
     return st;
 }
 
-int capnp_packed_encode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
-                              uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
-                              uint64_t* d_out_len, int32_t* d_status, void* stream) {
+size_t capnp_packed_batch_workspace_bytes(uint32_t n) { return cpk::queue_bytes(n); }
+
+int capnp_packed_encode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                 uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                                 uint64_t* d_out_len, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
+                                 void* stream) {
     int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
     if (st || n == 0) return st;
     if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
+    if (d_workspace && workspace_bytes < cpk::queue_bytes(n))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "workspace smaller than capnp_packed_batch_workspace_bytes(n)");
     hipError_t e = cpk::launch_encode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
-                                      d_status, true, static_cast<hipStream_t>(stream));
+                                      d_status, true, d_workspace, workspace_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "encode launch");
+}
+
+int capnp_packed_encode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                              uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                              uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    return capnp_packed_encode_batch_ws(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, nullptr, 0, stream);
 }
 
 int capnp_packed_encoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
@@ -238,19 +255,29 @@ int capnp_packed_encoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_of
     int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
     if (st || n == 0) return st;
     hipError_t e = cpk::launch_encode(d_in, d_in_off, d_in_len, n, nullptr, nullptr, nullptr, d_out_len, d_status,
-                                      false, static_cast<hipStream_t>(stream));
+                                      false, nullptr, 0, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "encode-size launch");
+}
+
+int capnp_packed_decode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                 uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
+                                 uint64_t* d_out_len, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
+                                 void* stream) {
+    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
+    if (st || n == 0) return st;
+    if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
+    if (d_workspace && workspace_bytes < cpk::queue_bytes(n))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "workspace smaller than capnp_packed_batch_workspace_bytes(n)");
+    hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                                      d_status, true, d_workspace, workspace_bytes, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode launch");
 }
 
 int capnp_packed_decode_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                               uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
                               uint64_t* d_out_len, int32_t* d_status, void* stream) {
-    int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
-    if (st || n == 0) return st;
-    if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
-    hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
-                                      d_status, true, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode launch");
+    return capnp_packed_decode_batch_ws(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, nullptr, 0, stream);
 }
 
 int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
@@ -258,7 +285,7 @@ int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_of
     int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
     if (st || n == 0) return st;
     hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, nullptr, nullptr, nullptr, d_out_len, d_status,
-                                      false, static_cast<hipStream_t>(stream));
+                                      false, nullptr, 0, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode-size launch");
 }
 
@@ -283,8 +310,12 @@ int capnp_packed_read_message(const uint8_t* in, size_t n, uint8_t* out, size_t 
     int st = ensure_device();
     if (st) return st;
     std::lock_guard<std::mutex> lock(g_ctx.mu);
+    // reader.zig can produce at most a 512-segment header (257 words) plus
+    // max_total_words (8 Mi, reader.zig:6) words: a larger cap is clamped, so the
+    // device slot is sized by what the reader can write, not by the caller's buffer
+    const size_t kMaxFramed = (257ull + 8ull * 1024 * 1024) * 8;
     uint64_t len = 0, used = 0;
-    st = run_single(4, in, n, out, cap, &len, &used);
+    st = run_single(4, in, n, out, cap < kMaxFramed ? cap : kMaxFramed, &len, &used);
     *out_len = (size_t)len;
     *consumed = (size_t)used;
     return st;

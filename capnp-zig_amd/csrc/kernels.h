@@ -7,13 +7,18 @@
 
 namespace cpk {
 
+// Batch encode / decode (write = false: sizes only). ws: optional caller workspace of
+// at least queue_bytes(n) bytes for the long-unit queue (nullptr: the caller stream's
+// own queue, kept by the library).
 hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
-                         int32_t* status, bool write, hipStream_t stream);
+                         int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream);
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
-                         int32_t* status, bool write, hipStream_t stream);
+                         int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream);
+
+size_t queue_bytes(uint32_t n);
 
 // Reader.readPackedMessage over a batch of reader streams (reader.zig:84-156).
 hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,

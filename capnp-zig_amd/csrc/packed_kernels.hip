@@ -4,34 +4,31 @@
 //   encode  nullstyle/capnp-zig src/serialization/message.zig:200-271 (packPacked)
 //   decode  message.zig:88-145 (unpackPacked) with the size pass of :152-191
 //
-// Execution model: encode and the wave decoder give one 64-lane
-// wave one unit (one packPacked / unpackPacked call): the unit is staged in the
-// wave's private LDS slice with coalesced 16-B global loads, processed with
-// wave-wide scans and written back with coalesced stores. The stream decoder
-// gives each lane one unit. No MFMA: this is byte compaction.
-//
-//   encode: lane j owns words [8j, 8j+8). Each word's zero-byte tag is formed
-//           with SWAR + a multiply gather; zero/literal runs (greedy, 256-capped)
-//           are resolved with wave max/min scans of break positions; a wave sum
-//           scan gives every lane its output byte offset; each lane appends its
-//           records to a byte stream in LDS (u64 ds_or at 8-B granularity).
-//   decode: the record chain (tag -> record length) is serial. Two decoders:
-//           decode_stream_kernel (default) gives each lane one unit and walks its
-//           chain once, emitting 16-word output rounds through an LDS ring that
-//           the wave stores with coalesced 128-B lines; decode_wave_kernel gives
-//           each wave one unit, resolves the chain through 64 lane chunks with
-//           speculative walks + verification rounds, and stores 64 consecutive
-//           words per instruction.
-//
-// Encode units larger than 4 KiB run a serial per-wave path (lane 0) that reads
-// and writes global memory directly (correct for any size; slow). Both decoders
-// handle any unit size on their fast path.
+// Execution model. No MFMA: this is byte compaction, HBM-bound.
+//   encode  one 64-lane wave per unit of <= 512 words (encode_kernel): the unit is
+//           staged in the wave's LDS slice with coalesced 16-B loads; lane j owns
+//           words [8j, 8j+8); zero-byte tags come from SWAR + a multiply gather;
+//           greedy 256-capped zero / literal runs are resolved with wave max/min
+//           scans of break positions; a wave sum scan gives each lane its output
+//           offset; lanes OR their records into an LDS byte stream that is written
+//           back with coalesced stores. Longer units: encode_tiled_kernel, tile by
+//           tile with run carries, on a side stream beside the main grid.
+//   decode  the record chain (tag -> record length -> next tag) is serial. Pass 1
+//           (decode_index_kernel) walks every unit's chain once, lane per unit,
+//           with quad-coalesced loads into an LDS ring, and leaves one u16 record
+//           per 16-B piece; pass 2 (decode_fill_kernel, wave per unit) starts every
+//           lane at its own pieces' first tag, lists the source of each output word
+//           and expands with coalesced stores. Units the fill pass cannot stage go
+//           to decode_wave_kernel (wave per unit, windowed) on the side stream.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <map>
+#include <memory>
 #include <mutex>
+#include <vector>
 
 #include "capnp_packed.h"
 #include "kernels.h"
@@ -64,6 +61,8 @@ enum : int32_t {
 };
 // internal status between decode passes: the unit goes to a full (fallback) decoder
 constexpr int32_t kStNeedFull = 0x7FFF0001;
+// status of a long unit between its listing and its worker's result
+constexpr int32_t kStPending = CAPNP_PACKED_DEVICE_ERROR;
 
 // ---------------------------------------------------------------------------
 // small device helpers
@@ -667,7 +666,8 @@ __global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restr
                                                           const uint64_t* __restrict__ in_len, uint32_t n,
                                                           uint8_t* __restrict__ out,
                                                           const uint64_t* __restrict__ out_off,
-                                                          const uint64_t* __restrict__ out_cap, uint32_t* q);
+                                                          const uint64_t* __restrict__ out_cap, uint32_t* q,
+                                                          int32_t* __restrict__ status);
 
 // Units longer than one tile (encode_tiled_unit), taken from the long-unit queue
 // and encoded one after another, tile by tile.
@@ -735,12 +735,16 @@ __global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restr
                                                           const uint64_t* __restrict__ in_len, uint32_t n,
                                                           uint8_t* __restrict__ out,
                                                           const uint64_t* __restrict__ out_off,
-                                                          const uint64_t* __restrict__ out_cap, uint32_t* q) {
+                                                          const uint64_t* __restrict__ out_cap, uint32_t* q,
+                                                          int32_t* __restrict__ status) {
     const uint32_t u = blockIdx.x * 256 + threadIdx.x;
     bool p = false;
     if (u < n) {
         p = KIND == 0 ? encode_tiled_unit(in, in_off[u], in_len[u])
                       : decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u]);
+        // sentinel until the long-unit worker writes the unit's outcome: a unit the
+        // worker never reached shows DEVICE_ERROR, not a stale status
+        if (p) status[u] = kStPending;
     }
     const bool huge = p && in_len[u] > kQHuge;
     const uint32_t lane = lane_id();
@@ -1201,167 +1205,8 @@ __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// DECODE, lane per unit, lockstep output rounds (the default decoder)
-// ---------------------------------------------------------------------------
-// Lane l of a wave owns unit wave_base + l and walks its record chain exactly
-// once (input side: per-lane register window, as in decode_lane_kernel). The
-// OUTPUT side is made regular: in every round each live lane emits exactly
-// kRoundWords words (one 128-B line) into its row of an LDS ring; zero runs and
-// literal runs that cross a round boundary carry over as pending counts. After
-// each round the wave stores the ring cooperatively: 8 lanes per 128-B line,
-// 8 lines per store instruction (fully coalesced), instead of 64 scattered
-// 8-byte stores per instruction.
-// ROUND words of output per lane per round (ROUND = 16: one 128-B line); ring rows
-// are ROUND*8 + 16 B (16-B aligned, staggers LDS banks); WAVES waves per block.
-
-template <int ROUND, int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(const uint8_t* __restrict__ in,
-                                                                     const uint64_t* __restrict__ in_off,
-                                                                     const uint64_t* __restrict__ in_len,
-                                                                     uint32_t n, uint8_t* __restrict__ out,
-                                                                     const uint64_t* __restrict__ out_off,
-                                                                     const uint64_t* __restrict__ out_cap,
-                                                                     uint64_t* __restrict__ out_len,
-                                                                     int32_t* __restrict__ status) {
-    constexpr int kRoundWords = ROUND;
-    constexpr int kRingRow = ROUND * 8 + 16;
-    constexpr int kStreamWaves = WAVES;
-    constexpr int kLanesPerRow = ROUND / 2;              // 16 B per lane in the cooperative store
-    constexpr int kRowsPerStep = kWave / kLanesPerRow;
-    constexpr int kSteps = kWave / kRowsPerStep;
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kStreamWaves * kWave * kRingRow];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* ring = ring_all + wave * (kWave * kRingRow);
-    const uint32_t unit = (blockIdx.x * kStreamWaves + wave) * kWave + lane;
-    const bool valid = unit < n;
-
-    // ---- per-lane unit state -------------------------------------------------------
-    const uint8_t* src = in;
-    uint64_t P = 0, capw = 0;
-    uint8_t* dstb = out;
-    int32_t st = ST_OK;
-    if (valid) {
-        src = in + in_off[unit];
-        P = in_len[unit];
-        dstb = out + out_off[unit];
-        capw = out_cap[unit] >> 3;
-        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
-    }
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    const uint64_t end64 = valid ? s + P : 0;
-    const uint8_t* base = src - s;
-    const uint32_t npieces = (uint32_t)((end64 + 15) >> 4);
-    uint64_t q0, q1, q2, q3, n0, n1;
-    uint32_t wb = 0;
-    load_piece(base, npieces, 0, q0, q1);
-    load_piece(base, npieces, 1, q2, q3);
-    load_piece(base, npieces, 2, n0, n1);
-    auto ensure = [&](uint32_t p) {
-        while (p - wb >= 16) {
-            q0 = q2; q1 = q3; q2 = n0; q3 = n1;
-            wb += 16;
-            load_piece(base, npieces, (wb >> 4) + 2, n0, n1);
-        }
-    };
-    uint64_t pos = s;          // next tag
-    uint64_t lit = 0;          // next literal word (valid while pend_lit)
-    uint32_t pend_zero = 0, pend_lit = 0;
-    uint64_t wo = 0;           // words emitted so far
-    bool live = valid && st == ST_OK;
-
-    uint64_t* myrow = reinterpret_cast<uint64_t*>(ring + lane * kRingRow);
-    while (__any(live)) {
-        // ---- one round: each live lane emits up to kRoundWords words -----------------
-        uint32_t nw = 0;
-#pragma unroll 2
-        for (int k = 0; k < kRoundWords; ++k) {
-            if (!live) break;
-            uint64_t word = 0;
-            bool have = true;
-            if (pend_zero) {
-                --pend_zero;
-            } else if (pend_lit) {
-                ensure((uint32_t)lit);
-                word = view_word8(q0, q1, q2, q3, (uint32_t)lit - wb);
-                lit += 8;
-                --pend_lit;
-            } else if (pos < end64) {
-                ensure((uint32_t)pos);
-                const uint32_t o = (uint32_t)pos - wb;
-                const uint32_t t = view_byte(q0, q1, q2, q3, o);
-                if (t == 0x00) {  // message.zig:101-110
-                    if (pos + 2 > end64) { st = ST_EOF; have = false; }
-                    else { pend_zero = view_byte(q0, q1, q2, q3, o + 1); pos += 2; }
-                } else if (t == 0xFF) {  // message.zig:112-128
-                    if (pos + 10 > end64) { st = ST_EOF; have = false; }
-                    else {
-                        const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
-                        if (pos + 10 + 8ULL * c > end64) { st = ST_EOF; have = false; }
-                        else {
-                            word = view_word8(q0, q1, q2, q3, o + 1);
-                            pend_lit = c;
-                            lit = pos + 10;
-                            pos += 10 + 8ULL * c;
-                        }
-                    }
-                } else {  // message.zig:131-141
-                    const uint32_t kk = __popc(t);
-                    if (pos + 1 + kk > end64) { st = ST_EOF; have = false; }
-                    else {
-                        word = expand_word(view_word8(q0, q1, q2, q3, o + 1), t);
-                        pos += 1 + kk;
-                    }
-                }
-            } else {
-                have = false;  // unit finished
-            }
-            if (!have) { live = false; break; }
-            myrow[nw++] = word;
-        }
-        wave_lds_sync();
-        // ---- cooperative store: lane L moves 16 B of unit row (L>>3)+8j ---------------
-        const uint64_t wo_round = wo;
-#pragma unroll
-        for (int j = 0; j < kSteps; ++j) {
-            const uint32_t r = lane / kLanesPerRow + kRowsPerStep * j;  // ring row (= lane of the owning unit)
-            const uint32_t i = lane % kLanesPerRow;                     // 16-B piece within the row
-            const uint32_t rnw = __shfl(nw, r, kWave);
-            const uint64_t rwo = __shfl(wo_round, r, kWave);
-            const uint64_t rcap = __shfl(capw, r, kWave);
-            uint8_t* rdst = reinterpret_cast<uint8_t*>(__shfl(reinterpret_cast<uint64_t>(dstb), r, kWave));
-            const uint32_t w0 = 2 * i;  // first word of this piece
-            if (w0 < rnw) {
-                const uint8_t* rp = ring + r * kRingRow + 16 * i;
-                const uint64_t g = rwo + w0;  // unit word index
-                uint8_t* gp = rdst + 8 * g;
-                const bool both = (w0 + 1 < rnw) && (g + 1 < rcap);
-                if (g < rcap) {
-                    if (both && !(reinterpret_cast<uintptr_t>(gp) & 15)) {
-                        *reinterpret_cast<uint4*>(gp) = *reinterpret_cast<const uint4*>(rp);
-                    } else {
-                        *reinterpret_cast<uint64_t*>(gp) = *reinterpret_cast<const uint64_t*>(rp);
-                        if (both) *reinterpret_cast<uint64_t*>(gp + 8) = *reinterpret_cast<const uint64_t*>(rp + 8);
-                    }
-                }
-            }
-        }
-        wo += nw;
-        wave_lds_sync();
-    }
-    if (!valid) return;
-    if (st != ST_OK) {
-        out_len[unit] = 0;
-        status[unit] = st;
-        return;
-    }
-    out_len[unit] = 8 * wo;
-    status[unit] = (wo > capw) ? ST_SPACE : ST_OK;
-}
-
-// ---------------------------------------------------------------------------
-// DECODE, wave per unit (CPK_DECODE_VARIANT=0; same speed as the stream decoder
-// at p=0.5, exact HBM traffic; see profiles/r01_decode_experiments.md)
+// DECODE fallback, wave per unit (long units of the indexed decoder, marked units
+// of the read-message passes; profiles/r01_decode_experiments.md)
 // ---------------------------------------------------------------------------
 // One wave owns one unit. The unit's packed bytes are processed in windows of
 // up to kWvWin bytes (one window for units up to ~4.5 KiB packed), each staged
@@ -1466,162 +1311,11 @@ __device__ __forceinline__ uint64_t gload_u64_unaligned(const uint8_t* p) {
     return v;
 }
 
-// ---------------------------------------------------------------------------
-// DECODE, checkpoint pass (first half of the two-pass decoder, CPK_DECODE_VARIANT=5)
-// ---------------------------------------------------------------------------
-// Lane l of a wave walks the record chain of unit l (message.zig:152-191) and, for
-// every 64-byte block b of the packed unit, records a checkpoint
-//   ck[b] = (words produced by records whose tag lies before 64b) << 7 | off,
-// off = offset of the first tag in block b (64 = no tag starts in the block).
-// The walk is lockstep by input: in step k every lane consumes the records whose
-// tag lies in its block k, so the wave stages block k+3 of all 64 units with four
-// LDS-DMA instructions per step (16 units x 64 B each) into a 4-slot ring and
-// waits with a fixed vmcnt: the chain reads LDS only, never global memory.
-// Checkpoints are written to the first 4*nblk bytes of the unit's output slot
-// (decode_wave_kernel reads them before it writes a byte of output). The pass
-// also yields the decoded size, EOF and out-of-space statuses. Units it does not
-// take (packed start not 16-B aligned, more than kWvWin packed bytes) get
-// kStNeedFull and are decoded by the wave kernel's full path.
-constexpr uint32_t kCkWaves = 2;
-constexpr uint32_t kCkBlock = kCkWaves * kWave;
-constexpr uint32_t kCkSlot = kWave * 64;        // one 64-B block for every lane of the wave
-constexpr uint32_t kCkNone = 64;
 
-__global__ __launch_bounds__(kCkBlock) void decode_ckpt_kernel(const uint8_t* __restrict__ in,
-                                                               const uint64_t* __restrict__ in_off,
-                                                               const uint64_t* __restrict__ in_len, uint32_t n,
-                                                               uint8_t* __restrict__ out,
-                                                               const uint64_t* __restrict__ out_off,
-                                                               const uint64_t* __restrict__ out_cap,
-                                                               uint64_t* __restrict__ out_len,
-                                                               int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kCkWaves * 4 * kCkSlot];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* const ring = ring_all + wave * 4 * kCkSlot;
-    const uint32_t unit = (blockIdx.x * kCkWaves + wave) * kWave + lane;
-    const bool valid = unit < n;
-
-    const uint8_t* src = in;
-    uint32_t P = 0;
-    uint8_t* dstb = out;
-    uint64_t cap = 0;
-    bool fast = false;
-    int32_t st = ST_OK;
-    if (valid) {
-        src = in + in_off[unit];
-        const uint64_t P64 = in_len[unit];
-        dstb = out + out_off[unit];
-        cap = out_cap[unit];
-        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
-        fast = st == ST_OK && !(reinterpret_cast<uintptr_t>(src) & 15) && P64 <= kWvWin &&
-               cap >= 4 * ((P64 + 63) / 64);
-        P = fast ? (uint32_t)P64 : 0u;
-        if (st == ST_OK && !fast) st = kStNeedFull;
-    }
-    const uint32_t nblk = (P + 63) >> 6;
-    uint32_t maxblk = nblk;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxblk = max(maxblk, (uint32_t)__shfl_xor((int)maxblk, d, kWave));
-    maxblk = __builtin_amdgcn_readfirstlane(maxblk);
-
-    // DMA descriptors: instruction q moves piece (lane & 3) of the block of unit 16q + lane/4
-    const uint8_t* dsrc[4];
-    uint32_t dlast[4];  // last valid 16-B piece of that unit
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t r = 16 * q + lane / 4;
-        const uint32_t rp = __shfl(P, r, kWave);
-        const uint64_t rs = __shfl(reinterpret_cast<uint64_t>(src), r, kWave);
-        // a unit with nothing to stage re-reads 16 B at the start of the in_len array
-        dsrc[q] = rp ? reinterpret_cast<const uint8_t*>(rs) : reinterpret_cast<const uint8_t*>(in_len);
-        dlast[q] = rp ? (rp - 1) >> 4 : 0u;
-    }
-    auto dma = [&](uint32_t k) {  // stage block k of every unit into slot k & 3
-        uint8_t* slot = ring + (k & 3) * kCkSlot;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t piece = min(4 * k + (lane & 3), dlast[q]);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc[q] + 16ull * piece),
-                                             (__attribute__((address_space(3))) void*)(slot + q * 1024), 16, 0, 0);
-        }
-    };
-    auto rb = [&](uint32_t p) -> uint32_t {  // byte p of this lane's unit (its block must be staged)
-        return ring[((p >> 6) & 3) * kCkSlot + lane * 64 + (p & 63)];
-    };
-
-    uint32_t pos = 0;         // next tag
-    uint32_t words = 0;       // words of the records before pos (saturates the checkpoint field)
-    uint32_t total = 0;       // decoded words (<= 4608 / 2 * 256)
-    bool live = fast;
-    uint32_t ck[4];
-    if (maxblk) {
-        dma(0);
-        if (maxblk > 1) dma(1);
-        if (maxblk > 2) dma(2);
-    }
-    for (uint32_t k = 0; k < maxblk; ++k) {
-        // blocks k and k+1 must have landed. Each step ends with [checkpoint stores]
-        // [DMA of block k+3] (when there is one), so the 4 youngest vector-memory
-        // operations are block k+2's DMA; near the end there is none: drain.
-        if (k + 3 <= maxblk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wave_lds_sync();
-        const uint32_t bend = 64 * (k + 1);
-        ck[k & 3] = ((pos < bend) ? (pos & 63) : kCkNone) | (words << 7);
-        for (;;) {  // one record per lane per pass; branch-free body, uniform exit
-            const bool act = live && pos < bend && pos < P;
-            if (!__any(act)) break;
-            uint32_t t = rb(pos);  // any position maps into the ring: inactive lanes read harmlessly
-            uint32_t b1 = rb(pos + 1);
-            uint32_t c9 = rb(pos + 9);
-            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per record
-            const uint32_t len = wv_len(t, c9);
-            const bool eof = act && pos + len > P;  // message.zig:152-191: record runs past the input
-            const bool ok = act && !eof;
-            st = eof ? ST_EOF : st;
-            live = live && !eof;
-            const uint32_t wd = 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
-            total += ok ? wd : 0u;
-            words = ok ? min(words + wd, 0x1FFFFFFu) : words;
-            pos = ok ? pos + len : pos;
-        }
-        if (k < nblk && ((k & 3) == 3 || k + 1 == nblk)) {  // flush up to four checkpoints (16 B)
-            if (fast && st == ST_OK) {
-                uint32_t* cp = reinterpret_cast<uint32_t*>(dstb) + (k & ~3u);
-                const uint32_t nv = min(4u, nblk - (k & ~3u));
-                if (nv == 4 && !(reinterpret_cast<uintptr_t>(cp) & 15)) {
-                    *reinterpret_cast<uint4*>(cp) = make_uint4(ck[0], ck[1], ck[2], ck[3]);
-                } else {
-                    for (uint32_t i = 0; i < nv; ++i) cp[i] = ck[i];
-                }
-            }
-        }
-        wave_lds_sync();
-        if (k + 3 < maxblk) dma(k + 3);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
-    if (!valid) return;
-    if (st == ST_OK && words >= 0x1FFFFFFu) st = kStNeedFull;  // checkpoint word field overflow
-    if (st == ST_OK && 8ull * total > cap) st = ST_SPACE;
-    out_len[unit] = (st == ST_OK || st == ST_SPACE) ? 8ull * total : 0;
-    status[unit] = st;
-}
-
-#ifdef CPK_WV_PROF
-// Phase probe (tools/wv_probe.hip): per unit, cycle stamps after each phase and counters.
-__device__ uint64_t* cpk_wv_prof;
-#define WV_STAMP(k) do { const uint64_t t_ = __builtin_readcyclecounter(); if (lane == 0) cpk_wv_prof[16ull * unit + (k)] = t_; } while (0)
-#define WV_COUNT(k, v) do { if (lane == 0) cpk_wv_prof[16ull * unit + (k)] += (v); } while (0)
-#else
-#define WV_STAMP(k) do { } while (0)
-#define WV_COUNT(k, v) do { } while (0)
-#endif
-
-// SEL: kWvAll every unit (wave per unit); kWvMarked the units a first pass marked
+// SEL: kWvMarked the units a first pass marked
 // kStNeedFull; kWvLong the units decode_long_unit selects (the indexed decoder's
 // fallback, which owns them from the start and may run beside passes 1 and 2).
-constexpr int kWvAll = 0, kWvMarked = 1, kWvLong = 2;
+constexpr int kWvMarked = 1, kWvLong = 2;
 
 template <int SEL>
 __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __restrict__ in,
@@ -1677,7 +1371,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     }
     uint64_t* const dst = reinterpret_cast<uint64_t*>(dstb);
 
-    WV_STAMP(0);
     uint64_t X = 0;   // packed position of the current window (always a tag)
     uint64_t Wb = 0;  // output words before the current window
     int32_t st = ST_OK;
@@ -1695,7 +1388,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         stage_linear<kWvStageK>(pk, g - sh, (sh + nload + 15) >> 4, lane);
         for (uint32_t i = lane * 16; i < Pw; i += 16 * kWave) *reinterpret_cast<uint4*>(mk + i) = make_uint4(0, 0, 0, 0);
         wave_lds_sync();
-        WV_STAMP(1);
 
         uint32_t cs, ce, ent, wbeg, wend, total, xw;
         {
@@ -1708,7 +1400,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         uint32_t hit;
         const uint32_t e1 = wv_walk(pk, mk, sh, rem, cs, ce, 1, hit);
         uint32_t e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0, e7 = 0;
-        WV_STAMP(2);
 
         // ---- walk B: enter where the left neighbour's walk A left off ---------------
         // An entry far past the chunk start (a misread FF run, or a misread record
@@ -1722,7 +1413,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
             if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
             e2 = ex;
         }
-        WV_STAMP(3);
 
         // ---- verification rounds ------------------------------------------------------
         // Lanes before the first disagreeing lane f are verified. A disagreeing lane
@@ -1737,7 +1427,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
             const bool bad = ent != prev;
             const uint64_t bm = __ballot(bad);
             if (!bm) break;
-            WV_COUNT(8, 1);
             const uint32_t f = (uint32_t)__builtin_ctzll(bm);
             const bool left_bad = lane > 0 && ((bm >> (lane - 1)) & 1);
             if (bad && (lane == f || (!left_bad && prev <= cs + kWvSlack))) {
@@ -1753,7 +1442,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
                 ++nid;
             }
         }
-        WV_STAMP(4);
         xw = readlane(ex, kWave - 1);  // window exit = next window start
         if (xw == kEOFX) {
             st = ST_EOF;
@@ -1776,7 +1464,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
         wbeg = incl - words;
         wend = incl;
         }
-        WV_STAMP(5);
 
         // ---- expand, by output word ---------------------------------------------------
         // Output words are produced in passes of kWvList words [W0, W0 + kWvList).
@@ -1851,8 +1538,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
                 }
             }
         }
-        WV_STAMP(6);
-        WV_COUNT(10, 1);
         Wb += total;
         X += xw;
     }
@@ -1862,136 +1547,6 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     }
     }  // marked units
     }  // unit loop
-}
-
-// ---------------------------------------------------------------------------
-// DECODE, expansion pass (second half of the two-pass decoder, CPK_DECODE_VARIANT=5)
-// ---------------------------------------------------------------------------
-// One wave per unit that decode_ckpt_kernel left at ST_OK (16-B aligned, <= kWvWin
-// packed bytes). Lane j owns 64-B blocks [bpl*j, bpl*(j+1)); their checkpoints give
-// its first tag and output word directly, so there is no chain resolution: one
-// fill walk lists the source of each output word (as in decode_wave_kernel) and
-// the wave expands the list with 64 consecutive words per store instruction.
-// The checkpoint loads are issued with the staging loads and all are consumed
-// before the first output store (they live in the output slot).
-constexpr uint32_t kExWaves = 4;
-constexpr uint32_t kExBlock = kExWaves * kWave;
-constexpr uint32_t kExList = 512;  // output words per expand pass
-
-__global__ __launch_bounds__(kExBlock) void decode_expand_kernel(const uint8_t* __restrict__ in,
-                                                                 const uint64_t* __restrict__ in_off,
-                                                                 const uint64_t* __restrict__ in_len, uint32_t n,
-                                                                 uint8_t* __restrict__ out,
-                                                                 const uint64_t* __restrict__ out_off,
-                                                                 const uint64_t* __restrict__ out_len,
-                                                                 const int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kExWaves * kWvPk];
-    __shared__ __attribute__((aligned(16))) uint16_t list_all[kExWaves * kExList];
-    __shared__ uint64_t lut[256];
-    lut[threadIdx.x] = expand_selector(threadIdx.x);
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t unit = blockIdx.x * kExWaves + wave;
-    if (unit >= n || status[unit] != ST_OK) return;  // wave-uniform
-    uint8_t* const pk = pk_all + wave * kWvPk;
-    uint16_t* const list = list_all + wave * kExList;
-
-    const uint8_t* const src = in + in_off[unit];  // 16-B aligned (decode_ckpt_kernel)
-    const uint32_t P = (uint32_t)in_len[unit];     // <= kWvWin
-    uint64_t* const dst = reinterpret_cast<uint64_t*>(out + out_off[unit]);
-    const uint32_t total = (uint32_t)(out_len[unit] >> 3);
-    if (P == 0) return;
-    const uint32_t nblk = (P + 63) >> 6;
-    const uint32_t bpl = (nblk + kWave - 1) / kWave;
-    const uint32_t b0 = min(bpl * lane, nblk), b1 = min(b0 + bpl, nblk);
-
-    // ---- checkpoint loads + staging loads in flight together -----------------------
-    const uint32_t* ckp = reinterpret_cast<const uint32_t*>(dst);
-    uint32_t c0 = ckp[min(b0, nblk - 1)];
-    uint32_t c1 = ckp[min(b0 + 1, nblk - 1)];
-    uint32_t cn = ckp[min(b1, nblk - 1)];
-    stage_linear<kWvStageK>(pk, src, (P + 15) >> 4, lane);
-    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(cn));  // all checkpoints read before any store
-    wave_lds_sync();
-
-    const uint32_t cs = 64 * b0, ce = min(64 * b1, P);
-    uint32_t ent = ce;  // no tag starts in this lane's blocks
-    uint32_t wbeg = (b1 < nblk) ? (cn >> 7) : total;
-    if (b0 < nblk && (c0 & 127) != kCkNone) {
-        ent = cs + (c0 & 127);
-        wbeg = c0 >> 7;
-    } else if (bpl > 1 && b0 + 1 < nblk && (c1 & 127) != kCkNone) {
-        ent = cs + 64 + (c1 & 127);
-        wbeg = c1 >> 7;
-    }
-    const uint32_t wend = (b1 < nblk) ? (cn >> 7) : total;
-
-    for (uint32_t W0 = 0; W0 < total; W0 += kExList) {
-        const uint32_t W1 = min(total, W0 + kExList);
-        wave_lds_sync();
-        for (uint32_t i = lane * 8; i < kExList; i += 8 * kWave)
-            *reinterpret_cast<uint4*>(list + i) = make_uint4(kZero2, kZero2, kZero2, kZero2);
-        wave_lds_sync();
-        // ---- fill: one record per lane per pass, uniform exit ------------------------
-        uint32_t r = ent, w = wbeg;
-        const bool mine = wbeg < W1 && wend > W0;
-        uint32_t pn = 0, ps = 0, pw = 0;  // one long literal run per lane goes to the wave
-        for (;;) {
-            const bool act = mine && r < ce && w < W1;
-            if (!__any(act)) break;
-            const uint32_t rr = act ? r : 0u;
-            uint32_t t = pk[rr];
-            uint32_t b1v = pk[rr + 1];
-            uint32_t c9 = pk[rr + 9];
-            asm volatile("" : "+v"(t), "+v"(b1v), "+v"(c9));
-            const bool z = t == 0, f = t == 0xFFu;
-            if (act) {
-                if (!z && w >= W0) list[w - W0] = (uint16_t)rr;
-                if (f && c9) {  // literal words rr+10 .. rr+10+8c
-                    if (c9 <= kWvExtLane || pn != 0) {
-                        for (uint32_t i = 0; i < c9; ++i) {
-                            const uint32_t wi = w + 1 + i;
-                            if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (rr + 9 + 8 * i));
-                        }
-                    } else {
-                        pn = c9;
-                        ps = rr + 9;
-                        pw = w + 1;
-                    }
-                }
-            }
-            w = act ? w + 1u + (z ? b1v : 0u) + (f ? c9 : 0u) : w;
-            r = act ? r + wv_len(t, c9) : r;
-        }
-        uint64_t pm = __ballot(pn != 0);
-        while (pm) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(pm);
-            pm &= pm - 1;
-            const uint32_t nn = readlane(pn, l), ss = readlane(ps, l), ww = readlane(pw, l);
-            for (uint32_t i = lane; i < nn; i += kWave) {
-                const uint32_t wi = ww + i;
-                if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (ss + 8 * i));
-            }
-        }
-        wave_lds_sync();
-        // ---- expand: lane i -> output word W0 + i (+64k) ---------------------------------
-        for (uint32_t i = W0 + lane; i < W1; i += kWave) {
-            const uint32_t code = list[i - W0];
-            const uint32_t q = code & kPosMask;
-            const bool lit = (code & kLit) != 0;
-            uint64_t word = 0;
-            if (!(code & kZero)) {
-                if (!lit || q + 9 <= P) {
-                    const uint32_t t = lit ? 0xFFu : pk[q];
-                    word = perm64(lds_u64_at(pk, q + 1), lut[t]);
-                } else {
-                    word = gload_u64_unaligned(src + q + 1);
-                }
-            }
-            dst[i] = word;
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2734,111 +2289,126 @@ static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) 
 // from the main kernels and run beside them: a batch whose few long units would
 // otherwise run alone after the main grid (config C5's tail) overlaps them with it.
 // fork(): the side stream waits for everything already on the caller's stream;
-// join(): the caller's stream waits for the side stream's kernel. One side stream
-// and event pair per device, created on first use; the mutex keeps one caller's
-// record/wait pairs together. Both are capturable into a hipGraph.
-struct SideStream {
+// join(): the caller's stream waits for the side stream's kernels.
+//
+// Every (device, caller stream) pair has its own context: side stream, fork/join
+// events and long-unit queue, so batches on independent caller streams never wait
+// on each other, and a graph captured from one stream shares nothing with eager
+// work on another. The context's mutex keeps one caller's record/wait pairs and
+// queue reset together. A queue that has to grow is replaced, never freed (a
+// captured graph may still reference it); growing is refused during a capture.
+// Callers that pass their own workspace (capnp_packed_*_batch_ws) use it as the
+// queue instead, so nothing of the library's is baked into their graphs.
+struct StreamCtx {
+    std::mutex mu;
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    uint32_t* q = nullptr;  // long-unit queue (queue_take): 2 counters + qcap entries
+    uint32_t* q = nullptr;  // long-unit queue (queue_take): kQHead counters + qcap entries
     uint64_t qcap = 0;
+    std::vector<uint32_t*> retired;  // replaced queues (kept: graphs may reference them)
 };
-static std::mutex g_side_mu;
-static SideStream g_side[64];
+static std::mutex g_ctx_mu;
+static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
+
+size_t queue_bytes(uint32_t n) { return (kQHead + (size_t)n) * sizeof(uint32_t); }
 
 class SideLaunch {
   public:
-    explicit SideLaunch(hipStream_t main) : main_(main), lock_(g_side_mu) {
+    SideLaunch(hipStream_t main, void* ws, size_t ws_bytes) : main_(main), ws_(ws), ws_bytes_(ws_bytes) {
         int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
-        SideStream& ss = g_side[dev];
+        if (hipGetDevice(&dev) != hipSuccess) return;
+        {
+            std::lock_guard<std::mutex> g(g_ctx_mu);
+            std::unique_ptr<StreamCtx>& c = g_ctx[{dev, reinterpret_cast<uintptr_t>(main)}];
+            if (!c) c.reset(new StreamCtx());
+            ctx_ = c.get();
+        }
+        lock_ = std::unique_lock<std::mutex>(ctx_->mu);
         static const bool concurrent = [] {  // CPK_SIDE_STREAM=0: long units after the main grid
             const char* e = getenv("CPK_SIDE_STREAM");
             return !(e && e[0] == '0');
         }();
         if (!concurrent) {
-            own_ = ss;
-            own_.s = main_;
-            side_ = &own_;
-            serial_ = &ss;
+            side_ = main_;
+            ok_ = true;
             return;
         }
-        if (!ss.s) {
-            if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) { ss.s = nullptr; return; }
-            if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
-                (void)hipStreamDestroy(ss.s);
-                ss.s = nullptr;
+        if (!ctx_->s) {
+            if (hipStreamCreateWithFlags(&ctx_->s, hipStreamNonBlocking) != hipSuccess) {
+                ctx_->s = nullptr;
+                return;
+            }
+            if (hipEventCreateWithFlags(&ctx_->fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ctx_->join, hipEventDisableTiming) != hipSuccess) {
+                (void)hipStreamDestroy(ctx_->s);
+                ctx_->s = nullptr;
                 return;
             }
         }
-        if (hipEventRecord(ss.fork, main_) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess)
+        if (hipEventRecord(ctx_->fork, main_) != hipSuccess || hipStreamWaitEvent(ctx_->s, ctx_->fork, 0) != hipSuccess)
             return;
-        side_ = &ss;
+        side_ = ctx_->s;
+        forked_ = true;
+        ok_ = true;
     }
     // the stream the long-unit kernels go on (valid once queue() succeeded)
-    hipStream_t stream() const { return side_ ? side_->s : main_; }
+    hipStream_t stream() const { return side_; }
     // The long-unit queue for a batch of n units, its counters cleared on the side
-    // stream; nullptr when the side stream or the queue cannot be set up. Growing it
-    // waits for the side stream's earlier work (a first call inside a hipGraph capture
-    // that needs to grow it fails: run one batch of that size before capturing).
+    // stream; nullptr when the side stream or the queue cannot be set up.
     uint32_t* queue(uint32_t n) {
-        if (!side_) return nullptr;
-        if (side_->qcap < n) {
-            if (side_->q) {
-                if (hipStreamSynchronize(side_->s) != hipSuccess) return nullptr;
-                (void)hipFree(side_->q);
-                side_->q = nullptr;
-                side_->qcap = 0;
+        if (!ok_) return nullptr;
+        uint32_t* q = nullptr;
+        if (ws_) {
+            if (ws_bytes_ < queue_bytes(n)) return nullptr;
+            q = static_cast<uint32_t*>(ws_);
+        } else {
+            if (ctx_->qcap < n) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                if (hipStreamIsCapturing(main_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+                uint32_t* nq = nullptr;
+                if (hipMalloc(reinterpret_cast<void**>(&nq), queue_bytes(n)) != hipSuccess) return nullptr;
+                if (ctx_->q) ctx_->retired.push_back(ctx_->q);
+                ctx_->q = nq;
+                ctx_->qcap = n;
             }
-            if (hipMalloc(reinterpret_cast<void**>(&side_->q), (kQHead + (uint64_t)n) * sizeof(uint32_t)) !=
-                hipSuccess) {
-                side_->q = nullptr;
-                return nullptr;
-            }
-            side_->qcap = n;
+            q = ctx_->q;
         }
-        if (hipMemsetAsync(side_->q, 0, kQHead * sizeof(uint32_t), side_->s) != hipSuccess) return nullptr;
-        return side_->q;
+        if (hipMemsetAsync(q, 0, kQHead * sizeof(uint32_t), side_) != hipSuccess) return nullptr;
+        return q;
     }
     hipError_t join() {
-        if (serial_) {  // the queue may have grown: keep it
-            serial_->q = own_.q;
-            serial_->qcap = own_.qcap;
-            serial_ = nullptr;
-            side_ = nullptr;
-            return hipSuccess;
-        }
-        if (!side_) return hipSuccess;
-        hipError_t e = hipEventRecord(side_->join, side_->s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(main_, side_->join, 0);
-        side_ = nullptr;
+        if (!forked_) return hipSuccess;
+        forked_ = false;
+        hipError_t e = hipEventRecord(ctx_->join, side_);
+        if (e == hipSuccess) e = hipStreamWaitEvent(main_, ctx_->join, 0);
         return e;
     }
     ~SideLaunch() { (void)join(); }
 
   private:
     hipStream_t main_;
-    std::lock_guard<std::mutex> lock_;
-    SideStream* side_ = nullptr;
-    SideStream own_;                // serial mode: the caller's stream, the device's queue
-    SideStream* serial_ = nullptr;
+    void* ws_;
+    size_t ws_bytes_;
+    StreamCtx* ctx_ = nullptr;
+    std::unique_lock<std::mutex> lock_;
+    hipStream_t side_ = nullptr;
+    bool ok_ = false, forked_ = false;
 };
 
 hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
-                         int32_t* status, bool write, hipStream_t stream) {
+                         int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     // units of more than 512 words: encode_tiled_kernel over a grid that strides the batch
     const uint32_t groups = (n + kWave - 1) / kWave;
     // (side stream, launched first so the long units start early; the two kernels own
     // disjoint units: encode_tiled_unit)
     const uint32_t tiled_blocks = min((groups + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
-    SideLaunch side(stream);
+    SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
-    if (!q) return hipErrorOutOfMemory;
+    if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
     const hipStream_t ss = side.stream();
-    select_long_kernel<0><<<(n + 255) / 256, 256, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap, q);
+    select_long_kernel<0><<<(n + 255) / 256, 256, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap, q, status);
     if (write) {
         encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, q);
@@ -2855,22 +2425,11 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     return e != hipSuccess ? e : j;
 }
 
-// Decoder selection, read per launch so tests can exercise every
-// decoder in one process: CPK_DECODE_VARIANT unset = indexed two-pass decoder
-// (decode_index_kernel + decode_fill_kernel), 4 = lane-per-unit stream decoder,
-// 2 = the same with two waves per block, 3 = 8-word rounds, 0 = wave per unit,
-// 5 = checkpoint pass + expansion pass.
-static int decode_variant() {
-    const char* e = getenv("CPK_DECODE_VARIANT");
-    return e ? atoi(e) : 6;
-}
-
 // Persistent grid of the fill pass: as many blocks as are resident at once
 // (hipOccupancy..., LDS/VGPR-bound), each wave striding over the batch with one
 // unit in flight ahead.
 static uint32_t fill_blocks(uint32_t n) {
-    static uint32_t resident = 0;
-    if (resident == 0) {
+    static const uint32_t resident = [] {  // thread-safe one-time init (C++11 static)
         int dev = 0, cus = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -2878,9 +2437,8 @@ static uint32_t fill_blocks(uint32_t n) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decode_fill_kernel, kFlWaves * kWave, 0) !=
                 hipSuccess || per <= 0)
             per = 4;
-        resident = (uint32_t)(cus * per);
-        if (getenv("CPK_DEBUG_GRID")) fprintf(stderr, "fill grid: %d CUs x %d blocks\n", cus, per);
-    }
+        return (uint32_t)(cus * per);
+    }();
     const uint32_t full = (n + kFlWaves - 1) / kFlWaves;
     return full < resident ? full : resident;
 }
@@ -2903,72 +2461,29 @@ static uint32_t fallback_blocks(uint32_t n) {
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
-                         int32_t* status, bool write, hipStream_t stream) {
+                         int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    const int variant = decode_variant();
-    if (!write) {  // size pass
-        if (variant == 6) {
-            launch_index<true>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-            decode_lane_kernel<false, true><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(
-                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
-            return hipGetLastError();
-        }
-        const uint32_t blocks = (n + kBlock - 1) / kBlock;
-        decode_lane_kernel<false><<<blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                  out_len, status);
+    if (!write) {  // size pass: the size-only index walk, then the lane walk for units it declined
+        launch_index<true>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+        decode_lane_kernel<false, true><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(
+            in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
         return hipGetLastError();
     }
-    switch (variant) {
-        case 0: break;  // wave per unit, below
-        case 6: {       // index pass, fill pass, full path for what the first pass declined
-            // the fallback owns the long units from the start (decode_long_unit): it goes
-            // first, on the side stream, beside passes 1 and 2
-            SideLaunch side(stream);
-            uint32_t* const q = side.queue(n);
-            if (!q) return hipErrorOutOfMemory;
-            select_long_kernel<1><<<(n + 255) / 256, 256, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off,
-                                                                             out_cap, q);
-            decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
-                in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
-            launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
-            decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                               out_off, out_len, out_cap, status);
-            const hipError_t e = hipGetLastError();
-            const hipError_t j = side.join();
-            return e != hipSuccess ? e : j;
-        }
-        case 5: {       // checkpoint pass, expansion pass, full path for what the first pass declined
-            decode_ckpt_kernel<<<(n + kCkBlock - 1) / kCkBlock, kCkBlock, 0, stream>>>(
-                in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
-            decode_expand_kernel<<<(n + kExWaves - 1) / kExWaves, kExBlock, 0, stream>>>(
-                in, in_off, in_len, n, out, out_off, out_len, status);
-            decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                                     out_off, out_cap, out_len, status, nullptr);
-            return hipGetLastError();
-        }
-        case 3: {
-            const uint32_t blocks = (n + 2 * kWave - 1) / (2 * kWave);
-            decode_stream_kernel<8, 2><<<blocks, 2 * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                        out_len, status);
-            return hipGetLastError();
-        }
-        case 2: {       // stream, two waves per block
-            const uint32_t blocks = (n + 2 * kWave - 1) / (2 * kWave);
-            decode_stream_kernel<16, 2><<<blocks, 2 * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                         out_len, status);
-            return hipGetLastError();
-        }
-        default: {      // stream, one wave per block
-            const uint32_t blocks = (n + kWave - 1) / kWave;
-            decode_stream_kernel<16, 1><<<blocks, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                     out_len, status);
-            return hipGetLastError();
-        }
-    }
-    const uint32_t blocks = (n + kWvWaves - 1) / kWvWaves;
-    decode_wave_kernel<kWvAll><<<blocks, kWvBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                               out_len, status, nullptr);
-    return hipGetLastError();
+    // index pass, fill pass; the fallback owns the long units from the start
+    // (decode_long_unit): it goes first, on the side stream, beside passes 1 and 2
+    SideLaunch side(stream, ws, ws_bytes);
+    uint32_t* const q = side.queue(n);
+    if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
+    select_long_kernel<1><<<(n + 255) / 256, 256, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                     q, status);
+    decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
+    launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+    decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_len,
+                                                                       out_cap, status);
+    const hipError_t e = hipGetLastError();
+    const hipError_t j = side.join();
+    return e != hipSuccess ? e : j;
 }
 
 hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_len, const uint32_t* seg_first,

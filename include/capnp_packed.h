@@ -18,12 +18,13 @@
  * contract (message.zig:144/270 `toOwnedSlice`).
  *
  * Threading: all functions are thread-safe. The single-buffer host functions
- * serialise on one internal device context; batch functions are reentrant for
- * distinct streams. One-time device init is guarded by std::call_once.
+ * serialise on one internal device context. One-time device init is guarded by
+ * std::call_once. Batch functions keep per-(device, caller stream) state only:
  * encode/encoded_size/decode batches put their long units (more than 4 KiB in;
- * packed units beyond the fast decoder's window) on an internal per-device side
- * stream that is forked from and joined back into `stream` inside the call, so
- * ordering on `stream` is as if everything ran on it.
+ * packed units beyond the fast decoder's window) on a side stream of THAT caller
+ * stream, forked from and joined back into `stream` inside the call, so ordering
+ * on `stream` is as if everything ran on it and batches on different caller
+ * streams never wait on each other.
  */
 #ifndef CAPNP_PACKED_H
 #define CAPNP_PACKED_H
@@ -111,10 +112,16 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
  *
  * `stream` is a hipStream_t (NULL = default stream). Calls are asynchronous:
  * they enqueue kernels and return. The return value reports launch errors only;
- * per-unit results are in d_status / d_out_len. The only allocation is the
- * per-device long-unit queue (4 B per unit), made or grown when a batch is larger
- * than any earlier one on that device: run one batch of the largest size before
- * capturing calls into a hipGraph (capture then works, tests/test_gpu_side_stream.py).
+ * per-unit results are in d_status / d_out_len. A unit whose status is an error
+ * has unspecified slot contents (the reference returns no output for it).
+ *
+ * Workspace: encode / encoded_size / decode batches need a long-unit queue of
+ * capnp_packed_batch_workspace_bytes(n) bytes (4 B per unit + 16). The plain calls
+ * use a queue the library keeps per caller stream (made or grown on a batch larger
+ * than any earlier one on that stream; growing is refused with DEVICE_ERROR inside
+ * a hipGraph capture, and an old queue is never freed, so graphs that captured it
+ * stay valid). The *_ws calls take the caller's device workspace instead: nothing
+ * of the library's is captured, and a graph of them may replay beside any work.
  * ------------------------------------------------------------------------ */
 
 /* Batch packPacked (message.zig:200-271), one unit = one packPacked call. */
@@ -122,6 +129,17 @@ int capnp_packed_encode_batch(const uint8_t* d_in, const uint64_t* d_in_off, con
                               uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
                               const uint64_t* d_out_cap, uint64_t* d_out_len, int32_t* d_status,
                               void* stream);
+
+/* Bytes of device workspace the *_batch_ws calls need for n units. */
+size_t capnp_packed_batch_workspace_bytes(uint32_t n);
+
+/* capnp_packed_encode_batch with a caller-owned device workspace of at least
+ * capnp_packed_batch_workspace_bytes(n) bytes (NULL = the library's per-stream
+ * queue). The workspace must not be used by another batch in flight. */
+int capnp_packed_encode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                 uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                                 const uint64_t* d_out_cap, uint64_t* d_out_len, int32_t* d_status,
+                                 void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Packed sizes only (no output written): the first half of a dense encode
  * (sizes -> exclusive scan -> capnp_packed_encode_batch with dense offsets). */
@@ -133,6 +151,13 @@ int capnp_packed_decode_batch(const uint8_t* d_in, const uint64_t* d_in_off, con
                               uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
                               const uint64_t* d_out_cap, uint64_t* d_out_len, int32_t* d_status,
                               void* stream);
+
+/* capnp_packed_decode_batch with a caller-owned device workspace (as
+ * capnp_packed_encode_batch_ws). */
+int capnp_packed_decode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                 uint32_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                                 const uint64_t* d_out_cap, uint64_t* d_out_len, int32_t* d_status,
+                                 void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Batch estimateUnpackedSize (message.zig:152-191). */
 int capnp_packed_decoded_size_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,

@@ -139,13 +139,11 @@ PAIRS = [("binary", "packed"), ("segmented", "segmented-packed"),
          ("fixture_single.bin", "fixture_single_packed.bin"), ("fixture_far.bin", "fixture_far_packed.bin")]
 
 
-@pytest.fixture(params=["6", "4", "0", "5"], ids=["indexed", "stream", "wave", "ckpt"])
-def decoder(request, monkeypatch):
-    """Run a decode test against every decoder (capnp_packed reads CPK_DECODE_VARIANT
-    per launch: 6 = indexed two-pass (the default), 4 = lane stream, 0 = wave per
-    unit, 5 = checkpoint pass + wave per unit)."""
-    monkeypatch.setenv("CPK_DECODE_VARIANT", request.param)
-    return request.param
+@pytest.fixture
+def decoder():
+    """The production decoder (one path: DESIGN.md §2.3). Kept as a fixture so the
+    decode tests read the same if a decoder variant is ever compared again."""
+    return "production"
 
 
 @pytest.mark.parametrize("unpacked,packed", PAIRS)

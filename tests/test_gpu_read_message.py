@@ -225,3 +225,21 @@ def test_framed_units_at_scale():
     torch.cuda.synchronize()
     assert (st == 0).all() and torch.equal(used, plen) and (olen == ub).all()
     assert torch.equal(d_out, d_in)
+
+
+def test_single_buffer_unbounded_cap():
+    # cap = SIZE_MAX (a C caller's "unbounded" idiom): the device slot is sized by what
+    # reader.zig can produce, so the workspace sums cannot wrap and nothing is written
+    # past the framed message
+    import ctypes
+    segs = [bytes(range(1, 41)), bytes(16)]
+    a = pyref.to_packed_bytes(segs)
+    exp = pyref.frame(segs)
+    src = ctypes.create_string_buffer(a, len(a))
+    out = ctypes.create_string_buffer(len(exp) + 64)
+    ctypes.memset(out, 0xAB, len(exp) + 64)
+    n, used = ctypes.c_size_t(), ctypes.c_size_t()
+    st = cp.lib().capnp_packed_read_message(src, len(a), out, ctypes.c_size_t(-1).value, ctypes.byref(n),
+                                            ctypes.byref(used))
+    assert st == cp.OK and n.value == len(exp) and used.value == len(a)
+    assert out.raw[:len(exp)] == exp and out.raw[len(exp):] == b"\xab" * 64

@@ -1,12 +1,15 @@
 """Long units on the side stream: encode_tiled_kernel and the decode
-fallback take the long units from a device queue on a per-device side stream, joined
-back into the caller's stream. These tests check that the fork/join orders them with
+fallback take the long units from a device queue on a side stream of the caller's
+stream, joined back into it. These tests check that the fork/join orders them with
 the caller's own work:
 - on a caller-created (non-default) stream, with the result read right after a
   synchronisation of that stream only;
 - back-to-back batches of different long-unit mixes, so a later batch's queue reset
   cannot overtake an earlier batch's workers;
-- captured into a hipGraph (torch.cuda.graph) and replayed on new data;
+- captured into a hipGraph (torch.cuda.graph) and replayed on new data, also after a
+  larger eager batch on the capturing stream (the queue grows; the captured one must
+  stay valid), and with a caller workspace while an eager batch runs on another
+  stream;
 - a batch with no long units and one of long units only (the empty-queue and
   all-queue ends).
 Every unit is checked against the oracle (message.zig:200-271 / 88-145) or by
@@ -52,11 +55,17 @@ class Batch:
         self.ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
         self.ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
 
-    def run(self, stream=None):
+    def run(self, stream=None, ws=None):
         cp.encode_batch(self.d_in, self.in_off, self.sizes, self.d_pk, self.pk_off, self.cap, self.plen, self.pst,
-                        stream=stream)
+                        stream=stream, ws=ws)
         cp.decode_batch(self.d_pk, self.pk_off, self.plen, self.d_out, self.in_off, self.sizes, self.ulen, self.ust,
-                        stream=stream)
+                        stream=stream, ws=ws)
+
+    def reset(self, seed):
+        cp.generate(1, self.U, seed=seed, zero_thresh=self.thr, out=self.d_in, device=DEV)
+        self.pst.fill_(-1)
+        self.ust.fill_(-1)
+        self.d_out.zero_()
 
     def check_roundtrip(self):
         assert (self.pst == 0).all().item() and (self.ust == 0).all().item()
@@ -116,19 +125,72 @@ def test_graph_capture_replay():
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        b.run(stream=s)  # warm-up: sizes the device queue before capture
+        b.run(stream=s)  # warm-up: sizes this stream's queue before capture
     s.synchronize()
     b.check_roundtrip()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):
         b.run()
     # new data in the same buffers, then replay the captured encode + decode
-    cp.generate(1, b.U, seed=0xC0DE0402, zero_thresh=128, out=b.d_in, device=DEV)
-    b.pst.fill_(-1)
-    b.ust.fill_(-1)
-    b.d_out.zero_()
+    b.reset(0xC0DE0402)
     g.replay()
     torch.cuda.synchronize()
     b.check_roundtrip()
     long_units = [i for i, x in enumerate(b.sizes.cpu().numpy()) if x > 4096]
     b.check_oracle(long_units[:100])
+
+
+def test_graph_replay_after_larger_eager_batch():
+    # the capturing stream's queue grows for a larger eager batch after the capture:
+    # the old queue, baked into the graph, must stay allocated
+    small = Batch(mixed_sizes(600, 4), seed=0xC0DE0411)
+    big = Batch(mixed_sizes(5000, 5), seed=0xC0DE0412)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        small.run(stream=s)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        small.run()
+    with torch.cuda.stream(s):
+        big.run(stream=s)  # grows s's queue
+    s.synchronize()
+    big.check_roundtrip()
+    small.reset(0xC0DE0413)
+    torch.cuda.empty_cache()
+    g.replay()
+    torch.cuda.synchronize()
+    small.check_roundtrip()
+    long_units = [i for i, x in enumerate(small.sizes.cpu().numpy()) if x > 4096]
+    small.check_oracle(long_units[:60])
+
+
+def test_graph_with_workspace_beside_eager_stream():
+    # a graph captured with its own workspace replays while an eager batch runs on
+    # another stream: nothing of either is shared
+    a = Batch(mixed_sizes(1200, 6), seed=0xC0DE0421)
+    e = Batch(mixed_sizes(2500, 7), seed=0xC0DE0422)
+    ws = cp.workspace(a.n, device=DEV)
+    s, t = torch.cuda.Stream(), torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    t.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        a.run(ws=ws)  # no warm-up needed: the workspace is the queue
+    a.reset(0xC0DE0423)
+    with torch.cuda.stream(s):
+        g.replay()
+    with torch.cuda.stream(t):
+        e.run(stream=t)
+    torch.cuda.synchronize()
+    a.check_roundtrip()
+    e.check_roundtrip()
+    e.check_oracle([i for i, x in enumerate(e.sizes.cpu().numpy()) if x > 4096][:60])
+
+
+def test_workspace_too_small_is_rejected():
+    b = Batch(mixed_sizes(100, 8), seed=0xC0DE0431)
+    ws = cp.workspace(10, device=DEV)
+    with pytest.raises(cp.InvalidArgument):
+        b.run(ws=ws)
