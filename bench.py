@@ -11,13 +11,23 @@ value = sum over ranks of unpacked bytes per step / max-over-ranks step time, in
 Inputs are generated on device before timing (synthetic, counter-based hash:
 DESIGN.md §4). After timing, decode(encode(x)) == x is checked on device.
 
+The headline config is BASELINE config 3 (1M x 4 KiB, zero-byte density sweep
+10/50/90 %): `value` is the p = 0.5 step; `sweep` times every density, each with
+its own encode/decode roofline fraction.
+
 Run: python bench.py [--gpus N --steps K --warmup W]
-     torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU, RCCL)
+     --gpus N without a torchrun environment: this process starts N ranks (one per
+     GPU, RCCL) as child processes before anything touches a GPU, and exits with
+     their status; under torchrun (WORLD_SIZE set) each process is one rank.
+     --dry-run: the same launcher on the CPU (gloo), each rank packing a small shard
+     with the oracle: checks the rank plumbing and the all-gather without a GPU.
 """
 import argparse
 import json
+import socket
 import struct
 import os
+import subprocess
 import sys
 import time
 
@@ -43,9 +53,13 @@ def parse():
     ap.add_argument("--unit-bytes", type=int, default=4096)
     ap.add_argument("--zero-thresh", type=int, default=128, help="zero-byte probability x 256 (128 = 0.5)")
     ap.add_argument("--seed", type=int, default=0xC0DE0003)
-    ap.add_argument("--sweep", action="store_true", help="also time p = 0.1 / 0.9 (extra fields)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the p = 0.1 / 0.9 legs of the density sweep")
+    ap.add_argument("--sweep", action="store_true", help=argparse.SUPPRESS)  # the sweep is the default now
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of each CPU baseline leg")
+    ap.add_argument("--no-dense", action="store_true", help="skip the dense packed-stream decode leg")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 bench-message leg")
+    ap.add_argument("--dry-run", action="store_true", help="CPU (gloo) rehearsal of the multi-rank path")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory leg")
     ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
     ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
@@ -117,40 +131,178 @@ def time_steps(wl, steps, warmup, world, dev):
     return float(elapsed.item()), enc_ms, dec_ms, gathered[0]
 
 
-def cpu_baseline(args, budget_s):
-    """Oracle (C restatement of message.zig:88-271) on the host cores, OpenMP over
-    units, same generator, same unit size/density, bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_native():
+    """The oracle (tests/oracle.py) bound to a -O3 -march=native build of
+    oracle/packed_oracle.c made for THIS host (falls back to the prebuilt
+    x86-64-v2 liboracle.so if gcc fails). Returns (module, march)."""
     sys.path.insert(0, os.path.join(HERE, "tests"))
-    import numpy as np
+    import tempfile
     import oracle
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    src = os.path.join(HERE, "oracle", "packed_oracle.c")
+    out = os.path.join(tempfile.gettempdir(), f"cpk_oracle_native_{os.getpid()}.so")
+    try:
+        subprocess.run(["gcc", "-O3", "-march=native", "-fPIC", "-fopenmp", "-std=c11", "-shared", "-o", out, src],
+                       check=True, capture_output=True, timeout=120)
+        oracle._lib, oracle.LIB_PATH = None, out
+        oracle.lib()
+        return oracle, "native"
+    except Exception:
+        oracle._lib, oracle.LIB_PATH = None, os.path.join(HERE, "oracle", "liboracle.so")
+        return oracle, "x86-64-v2"
+
+
+def _cpu_leg(oracle, args, n, threads, budget_s):
+    import numpy as np
     ub = args.unit_bytes
-    n = 4096
     data = oracle.generate(n, ub, seed=args.seed, zero_thresh=args.zero_thresh, threads=threads)
     in_off = np.arange(0, n * ub + 1, ub, dtype=np.uint64)
     slot = 10 * ub // 8
     pk_off = np.arange(0, n * slot + 1, slot, dtype=np.uint64)
+    out, out_len, st = oracle.pack_batch(data, in_off, pk_off, threads=threads)
+    dense_off = np.zeros(n + 1, dtype=np.uint64)
+    dense_off[1:] = np.cumsum(out_len)
+    dense = np.concatenate([out[int(pk_off[i]):int(pk_off[i]) + int(out_len[i])] for i in range(n)])
     reps, t_total = 0, 0.0
-    packed_dense = None
     while t_total < budget_s and reps < 1000:
         t0 = time.perf_counter()
         out, out_len, st = oracle.pack_batch(data, in_off, pk_off, threads=threads)
-        if packed_dense is None:
-            dense = np.zeros(n + 1, dtype=np.uint64)
-            dense[1:] = np.cumsum(out_len)
-            packed_dense = (np.concatenate([out[int(pk_off[i]):int(pk_off[i]) + int(out_len[i])]
-                                            for i in range(n)]), dense)
-            t0 = time.perf_counter()  # exclude the one-time dense repacking from the timing
-            out, out_len, st = oracle.pack_batch(data, in_off, pk_off, threads=threads)
-        pk, dense = packed_dense
-        dec, dec_len, dst = oracle.unpack_batch(pk, dense, in_off, threads=threads)
+        dec, dec_len, dst = oracle.unpack_batch(dense, dense_off, in_off, threads=threads)
         t_total += time.perf_counter() - t0
         reps += 1
     assert (st == 0).all() and (dst == 0).all() and (dec[:n * ub] == data).all()
-    gib = reps * n * ub / t_total / 2 ** 30
-    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x ({n} units x {ub} B, same generator/seed/density) pack+unpack via "
-                      f"oracle/packed_oracle.c (-O3, OpenMP {threads} threads), {t_total:.1f} s"}
+    return reps * n * ub / t_total / 2 ** 30, reps, t_total
+
+
+def cpu_baseline(args, budget_s):
+    """Oracle (C restatement of message.zig:88-271) on this host's cores, same
+    generator and unit size/density as the GPU, OpenMP over units, bounded samples:
+    an all-core leg on 32K units (128 MiB, past the LLC) and a 1-core leg on 2K
+    units. The oracle is a checker, written byte by byte for clarity (its output
+    sink appends one byte at a time): it is slower than an optimised Zig ReleaseFast
+    codec would be, so the GPU/CPU ratio overstates the gap."""
+    oracle, march = _oracle_native()
+    cores = len(os.sched_getaffinity(0))
+    allc, reps_a, t_a = _cpu_leg(oracle, args, 32768, cores, budget_s)
+    one, reps_1, t_1 = _cpu_leg(oracle, args, 2048, 1, budget_s / 2)
+    return {"value": round(allc, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "one_core_GiB_s": round(one, 4), "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+            "build": f"gcc -O3 -march={march} -fopenmp",
+            "sample": f"pack+unpack of units x {args.unit_bytes} B (same generator/seed/density as the GPU) via "
+                      f"oracle/packed_oracle.c: all-core {reps_a} x 32768 units in {t_a:.1f} s ({cores} threads), "
+                      f"1-core {reps_1} x 2048 units in {t_1:.1f} s",
+            "note": "checker restatement (byte-at-a-time output), not an optimised codec: a lower bound on a "
+                    "ReleaseFast Zig build's rate"}
+
+
+def c1_leg(reps_cpu=300, reps_gpu=100):
+    """BASELINE config 1: the reference bench's own message (bench/packed_unpacked.zig
+    buildMessage, default --payload 4096 --list-len 2048: U = 20,536 B framed,
+    P = 18,463 B packed; tests/pyref.py bench_message_segments), pack / unpack /
+    roundtrip ns/iter in the bench's byte accounting (:350-357): pack U, unpack P,
+    roundtrip U + P. CPU: the oracle, one thread (the bench is single-threaded),
+    toPackedBytes = pack(toBytes) and initPacked = unpack + Message.init. GPU: the
+    single-buffer C-ABI (capnp_packed_encode / _decode: one unit, H2D + kernels +
+    D2H + sync per call). Next to bench/baselines.json:69-183 (Debug build,
+    hardware not recorded)."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import oracle
+    import pyref
+    framed = pyref.frame(pyref.bench_message_segments())
+    st, packed = oracle.pack(framed)
+    assert st == 0 and len(framed) == 20536 and len(packed) == 18463
+    U, P = len(framed), len(packed)
+
+    def t_ns(fn, reps):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return (time.perf_counter() - t0) / reps * 1e9
+
+    def cpu_unpack():
+        s2, out = oracle.unpack(packed)
+        assert s2 == 0 and oracle.message_init(out, 1)[0] == 0
+
+    cpu = {"pack_ns": t_ns(lambda: oracle.pack(framed), reps_cpu), "unpack_ns": t_ns(cpu_unpack, reps_cpu)}
+    cpu["roundtrip_ns"] = cpu["pack_ns"] + cpu["unpack_ns"]
+    assert cp.pack_packed(framed) == packed and cp.unpack_packed(packed) == framed
+    gpu = {"pack_ns": t_ns(lambda: cp.pack_packed(framed), reps_gpu),
+           "unpack_ns": t_ns(lambda: cp.Message.init_packed(packed), reps_gpu)}
+    gpu["roundtrip_ns"] = gpu["pack_ns"] + gpu["unpack_ns"]
+    ref = {"pack_ns": 173923.65, "unpack_ns": 108204.37, "roundtrip_ns": 270675.97}
+    acct = {"pack": U, "unpack": P, "roundtrip": U + P}
+    out = {"unpacked_len": U, "packed_len": P}
+    for name, d in (("cpu_oracle_1core", cpu), ("gpu_single_buffer", gpu), ("reference_debug_ci", ref)):
+        out[name] = {k: round(v, 1) for k, v in d.items()}
+        out[name].update({f"{m}_MiB_s": round(acct[m] / (d[m + "_ns"] * 1e-9) / 2 ** 20, 1) for m in acct})
+    out["note"] = ("ns/iter and MiB/s in the reference bench's accounting (pack U, unpack P, roundtrip U+P); "
+                   "reference_debug_ci = bench/baselines.json:69-183 (Debug build, hardware not recorded)")
+    return out
+
+
+def copy_ceiling(dev, nbytes, reps=5):
+    """Device-copy ceiling: a torch copy of nbytes (read + write), GB/s."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    ev[0].record(stream)
+    for _ in range(reps):
+        b.copy_(a)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    del a, b
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
+def dense_leg(args, dev, reps=10):
+    """Decode from a DENSE packed stream (what arrives off a socket: unit starts at
+    arbitrary byte offsets), headline size: sizes -> scan -> dense encode (untimed),
+    then decode timed with HIP events on the launch stream."""
+    n, ub = args.units, args.unit_bytes
+    stream = torch.cuda.current_stream()
+    d_in = cp.generate(n, ub, seed=args.seed, zero_thresh=args.zero_thresh, device=dev)
+    in_off, in_len = cp.uniform_layout(n, ub, device=dev)
+    lens = torch.empty(n, dtype=torch.int64, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    cp.encoded_size_batch(d_in, in_off, in_len, lens, st)
+    off = cp.lengths_to_offsets(lens)
+    P = int(off[-1].item())
+    dense = torch.empty(P + 16, dtype=torch.uint8, device=dev)
+    pk_off = off[:-1].contiguous()
+    cp.encode_batch(d_in, in_off, in_len, dense, pk_off, lens, lens, st)
+    d_out = torch.empty(n * ub, dtype=torch.uint8, device=dev)
+    ulen = torch.zeros(n, dtype=torch.int64, device=dev)
+    ust = torch.zeros(n, dtype=torch.int32, device=dev)
+    run = lambda: cp.decode_batch(dense, pk_off, lens, d_out, in_off, in_len, ulen, ust, stream=stream)  # noqa: E731
+    run()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    ev[0].record(stream)
+    for _ in range(reps):
+        run()
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    ok = bool((ust == 0).all().item() and torch.equal(d_out, d_in))
+    alg = n * ub + P + META_BYTES_PER_UNIT * n
+    return {"decode_ms": round(ms, 4), "decode_GiB_s": round(n * ub / (ms * 1e-3) / 2 ** 30, 2),
+            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "packed_bytes": P, "bit_exact": ok,
+            "note": "decode of 1M units from one dense packed stream (unaligned unit starts)"}
 
 
 def host_path(args, dev, n_units=1 << 16):
@@ -450,11 +602,75 @@ def load_traffic(config_key):
         return None
 
 
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """One child process per rank (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set), started
+    before this process touches any GPU; rank 0 prints the JSON line. Returns the
+    worst exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal of the multi-rank step (gloo): each rank packs its shard of a small
+    batch with the oracle, then the same all-gather of packed totals as the GPU step."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import oracle
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, ub = args.units, args.unit_bytes
+    data = oracle.generate(n, ub, seed=args.seed, zero_thresh=args.zero_thresh, unit_base=rank * n)
+    t0 = time.perf_counter()
+    local = sum(len(oracle.pack(data[i * ub:(i + 1) * ub].tobytes())[1]) for i in range(n))
+    totals = sharding.gather_packed_totals(local)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (CPU oracle, gloo): per-rank pack + all-gather of packed totals",
+                          "n_gpus": world, "dry_run": True, "units_per_rank": n, "unit_bytes": ub,
+                          "packed_totals": totals.tolist(), "packed_total_all_ranks": int(totals.sum().item()),
+                          "shard_offsets": [sharding.shard_byte_offset(totals, r) for r in range(world)],
+                          "seconds": round(float(el.item()), 4)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def measure(wl, args, steps, warmup, world, dev):
+    """Time `steps` steps of one workload; roofline of encode and decode on their own."""
+    n, ub = wl.n, wl.ub
+    elapsed, enc_ms, dec_ms, gathered = time_steps(wl, steps, warmup, world, dev)
+    P = int(wl.plen.sum().item())
+    alg = n * ub + P + META_BYTES_PER_UNIT * n  # per launch on one GPU, same for encode and decode
+    return {"elapsed": elapsed, "enc_ms": enc_ms, "dec_ms": dec_ms, "gathered": gathered, "P": P, "alg": alg,
+            "ok": wl.verify(),
+            "encode_frac": alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "decode_frac": alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if args.units == 1 << 20:
+            args.units = 64
+        return dry_run(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -463,46 +679,55 @@ def main():
 
     n, ub = args.units, args.unit_bytes
     wl = Workload(n, ub, args.seed, args.zero_thresh, unit_base=rank * n, dev=dev)
-    elapsed, enc_ms, dec_ms, gathered = time_steps(wl, args.steps, args.warmup, world, dev)
-    ok = wl.verify()
-    ok_t = torch.tensor([1 if ok else 0], device=dev)
+    head = measure(wl, args, args.steps, args.warmup, world, dev)
+    ok_t = torch.tensor([1 if head["ok"] else 0], device=dev)
     if world > 1:
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-    packed_local = int(wl.plen.sum().item())
-    packed_all = int(gathered.sum().item())
+    packed_all = int(head["gathered"].sum().item())
+    elapsed, enc_ms, dec_ms = head["elapsed"], head["enc_ms"], head["dec_ms"]
+
+    def sweep_entry(m, thr, steps):
+        return {"zero_thresh": thr, "GiB_s": round(world * n * ub / (m["elapsed"] / steps) / 2 ** 30, 2),
+                "encode_ms": round(m["enc_ms"], 4), "decode_ms": round(m["dec_ms"], 4),
+                "encode_frac": round(m["encode_frac"], 4), "decode_frac": round(m["decode_frac"], 4),
+                "packed_ratio": round(m["P"] / (n * ub), 4), "bit_exact_roundtrip": m["ok"]}
 
     extra = {}
-    if args.sweep:
-        for thr, name in ((26, "p0.1"), (230, "p0.9")):
-            del wl
-            torch.cuda.empty_cache()
-            wl = Workload(n, ub, args.seed, thr, unit_base=rank * n, dev=dev)
-            e, em, dm, g = time_steps(wl, max(3, args.steps // 2), 1, world, dev)
-            extra[name] = {"GiB_s": round(world * n * ub / (e / max(3, args.steps // 2)) / 2 ** 30, 2),
-                           "encode_ms": round(em, 4), "decode_ms": round(dm, 4),
-                           "packed_ratio": round(int(g.sum().item()) / (world * n * ub), 4),
-                           "bit_exact_roundtrip": wl.verify()}
-    if world == 1 and not args.no_read_message:
+    if world == 1:
+        extra["sweep"] = {"p0.5": sweep_entry(head, args.zero_thresh, args.steps)}
+        if not args.no_sweep:
+            for thr, name in ((26, "p0.1"), (230, "p0.9")):
+                del wl
+                torch.cuda.empty_cache()
+                wl = Workload(n, ub, args.seed, thr, unit_base=rank * n, dev=dev)
+                k = max(5, args.steps // 2)
+                extra["sweep"][name] = sweep_entry(measure(wl, args, k, 2, world, dev), thr, k)
         del wl
         torch.cuda.empty_cache()
-        extra["read_message"] = read_message_leg(args, dev)
-    if world == 1 and not args.no_read_message:
-        torch.cuda.empty_cache()
-        extra["message_framing"] = message_leg(args, dev)
-    if world == 1 and not args.no_skewed:
-        torch.cuda.empty_cache()
-        extra["c5_skewed"] = skewed_leg(args, dev)
-    if world == 1 and not args.no_read_message:
-        torch.cuda.empty_cache()
-        extra["rpc_framer"] = framer_leg(args, dev)
+        extra["roofline_copy_ceiling_GBps"] = copy_ceiling(dev, n * ub)
+        if not args.no_dense:
+            torch.cuda.empty_cache()
+            extra["dense_stream"] = dense_leg(args, dev)
+        if not args.no_read_message:
+            torch.cuda.empty_cache()
+            extra["read_message"] = read_message_leg(args, dev)
+            torch.cuda.empty_cache()
+            extra["message_framing"] = message_leg(args, dev)
+        if not args.no_skewed:
+            torch.cuda.empty_cache()
+            extra["c5_skewed"] = skewed_leg(args, dev)
+        if not args.no_read_message:
+            torch.cuda.empty_cache()
+            extra["rpc_framer"] = framer_leg(args, dev)
+        if not args.no_c1:
+            extra["c1_bench_message"] = c1_leg()
 
     if rank == 0:
         steps = args.steps
         ms_per_step = elapsed / steps * 1e3
         U_total = world * n * ub
         value = U_total / (elapsed / steps) / 2 ** 30
-        P = packed_local
-        alg_bytes = n * ub + P + META_BYTES_PER_UNIT * n  # per launch on one GPU, same for enc and dec
+        alg_bytes = head["alg"]
         role, dom_ms = ("decode", dec_ms) if dec_ms >= enc_ms else ("encode", enc_ms)
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
         cfg_key = f"{n}x{ub}_t{args.zero_thresh}"
@@ -528,7 +753,9 @@ def main():
                        "parallelism": f"shard{world}"},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "alg_bytes_per_launch": alg_bytes},
+                         "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                         "encode_frac": round(head["encode_frac"], 4), "decode_frac": round(head["decode_frac"], 4),
+                         "copy_ceiling_GBps": extra.pop("roofline_copy_ceiling_GBps", None)},
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
             "encode_GiB_s": round(n * ub / (enc_ms * 1e-3) / 2 ** 30, 2),

@@ -124,3 +124,27 @@ def frame(segments) -> bytes:
 def to_packed_bytes(segments) -> bytes:
     """message.zig:2175-2179 toPackedBytes = packPacked(toBytes())."""
     return pack(frame(segments))
+
+
+def bench_message_segments(payload_size: int = 4096, list_len: int = 2048):
+    """The message bench/packed_unpacked.zig:128-166 (buildMessage, default config,
+    payload[i] = 'a' + i % 26 at :302-307) builds, as MessageBuilder segments: one
+    segment holding the root pointer, the root struct (2 data words, 2 pointers),
+    the text (payload + NUL, word-padded) and the u64 list, allocated in that order.
+    Standard capnp pointer encoding (struct pointer: offset << 2 | 0, data words,
+    pointer words; list pointer: offset << 2 | 1, element size code | count << 3)."""
+    import struct
+    payload = bytes(ord("a") + (i % 26) for i in range(payload_size))
+    text = payload + b"\x00"
+    text_words = (len(text) + 7) // 8
+    words = []
+    words.append(struct.pack("<IHH", 0 << 2 | 0, 2, 2))                   # root -> struct at word 1
+    words.append(struct.pack("<Q", 0x0123456789ABCDEF))                   # data word 0
+    words.append(struct.pack("<II", payload_size, 0))                     # data word 1: u32 len at byte 8
+    text_at, list_at = 5, 5 + text_words
+    words.append(struct.pack("<II", (text_at - 4) << 2 | 1, 2 | (len(text) << 3)))    # ptr 0 (word 3): bytes
+    words.append(struct.pack("<II", (list_at - 5) << 2 | 1, 5 | (list_len << 3)))     # ptr 1 (word 4): u64
+    seg = b"".join(words) + text + b"\x00" * (8 * text_words - len(text))
+    seg += b"".join(struct.pack("<Q", 0 if i % 4 == 0 else (i + 0x0102030405060708) & (2**64 - 1))
+                    for i in range(list_len))
+    return [seg]

@@ -1,0 +1,39 @@
+"""bench.py's multi-rank launcher on the CPU (gloo): `bench.py --gpus 2 --dry-run`
+starts two rank processes itself (RANK / WORLD_SIZE / MASTER_* set, nothing touches a
+GPU), each packs its shard with the oracle and all-gathers its packed total, exactly
+the collective of the GPU step. The totals must equal a
+single-process computation over the same global units."""
+import json
+import os
+import subprocess
+import sys
+
+import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", *extra], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints the only JSON line
+    return json.loads(lines[0])
+
+
+def test_launcher_two_ranks_all_gather():
+    n, ub, seed, thr = 48, 1024, 0xC0DE0009, 128
+    res = _run("--gpus", "2", "--units", str(n), "--unit-bytes", str(ub), "--seed", str(seed))
+    assert res["n_gpus"] == 2 and res["dry_run"]
+    data = oracle.generate(2 * n, ub, seed=seed, zero_thresh=thr)
+    lens = [len(oracle.pack(data[i * ub:(i + 1) * ub].tobytes())[1]) for i in range(2 * n)]
+    assert res["packed_totals"] == [sum(lens[:n]), sum(lens[n:])]
+    assert res["shard_offsets"] == [0, sum(lens[:n])]
+    assert res["packed_total_all_ranks"] == sum(lens)
+
+
+def test_launcher_single_rank():
+    res = _run("--units", "16", "--unit-bytes", "512")
+    assert res["n_gpus"] == 1 and len(res["packed_totals"]) == 1

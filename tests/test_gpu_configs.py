@@ -111,6 +111,44 @@ def test_c5_skewed_sizes_every_unit(thr):
     assert np.array_equal(d_out.cpu().numpy()[:U], host)
 
 
+def test_c5_full_size_1M_units():
+    """BASELINE configs[4] at its stated size: 1M units of truncated-Pareto sizes
+    64 B..256 KiB (the bench's seed), p = 0.5. decode(encode(x)) == x on device for
+    every unit; every unit over 64 KiB and a strided sample of the rest byte-compared
+    with the oracle."""
+    n = 1 << 20
+    sizes = pareto_sizes(n, seed=0xC0DE0005)
+    off = np.zeros(n + 1, dtype=np.int64)
+    off[1:] = np.cumsum(sizes)
+    U = int(off[-1])
+    d_in = cp.generate(1, U, seed=0xC0DE0005, zero_thresh=128, device=DEV)
+    t_off = torch.from_numpy(off[:-1].copy()).to(DEV)
+    t_len = torch.from_numpy(sizes).to(DEV)
+    caps = (sizes // 8) * 10
+    slots = (caps + 15) // 16 * 16
+    poff = np.zeros(n, dtype=np.int64)
+    poff[1:] = np.cumsum(slots)[:-1]
+    d_pk = torch.zeros(int(slots.sum()) + 16, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    t_poff = torch.from_numpy(poff).to(DEV)
+    cp.encode_batch(d_in, t_off, t_len, d_pk, t_poff, torch.from_numpy(caps).to(DEV), plen, pst)
+    d_out = torch.zeros(U, dtype=torch.uint8, device=DEV)
+    ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.decode_batch(d_pk, t_poff, plen, d_out, t_off, t_len, ulen, ust)
+    torch.cuda.synchronize()
+    assert (pst == 0).all().item() and (ust == 0).all().item()
+    assert torch.equal(ulen, t_len) and torch.equal(d_out, d_in)
+    host = d_in.cpu().numpy()
+    pk, lens = d_pk.cpu().numpy(), plen.cpu().numpy()
+    pick = np.union1d(np.nonzero(sizes > 65536)[0], np.arange(0, n, 521))
+    for i in pick:
+        st, exp = oracle.pack(host[off[i]:off[i + 1]].tobytes())
+        assert st == oracle.OK and lens[i] == len(exp) and pk[poff[i]:poff[i] + lens[i]].tobytes() == exp, \
+            f"unit {i} ({sizes[i]} B)"
+
+
 def _encode_units(units):
     offs, pos = [], 0
     for u in units:

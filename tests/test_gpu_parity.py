@@ -406,3 +406,13 @@ def test_config3_full_size_roundtrip_property(decoder):
     check_sample_vs_oracle(d_in, d_pk, plen, slot, 4096, 1024)
     total = int(plen.sum().item())
     assert 0.55 * (1 << 32) < total < 0.70 * (1 << 32)  # ~0.626 expected at p = 0.5
+
+
+@pytest.mark.parametrize("thr", [26, 230])  # p = 0.1 / 0.9: the rest of the headline density sweep
+def test_config3_full_size_density_sweep(thr, decoder):
+    """BASELINE configs[2] at its stated size, p = 0.1 and 0.9: 1M x 4 KiB,
+    decode(encode(x)) == x on device, 1024 strided units byte-compared with the oracle."""
+    d_in, d_pk, plen, slot = roundtrip_uniform(1 << 20, 4096, 0xC0DE0003, thr)
+    check_sample_vs_oracle(d_in, d_pk, plen, slot, 4096, 1024)
+    ratio = int(plen.sum().item()) / (1 << 32)
+    assert (0.98 < ratio < 1.08) if thr == 26 else (0.18 < ratio < 0.30)  # ~1.033 / ~0.232 (SURVEY §8a)
