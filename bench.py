@@ -192,7 +192,9 @@ def cpu_baseline(args, budget_s):
     sink appends one byte at a time): it is slower than an optimised Zig ReleaseFast
     codec would be, so the GPU/CPU ratio overstates the gap."""
     oracle, march = _oracle_native()
-    cores = len(os.sched_getaffinity(0))
+    # the host's CPU share: OMP_NUM_THREADS where the launcher sets it (the GPU box
+    # exports 16 per GPU while the affinity mask shows every core), else the affinity
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     allc, reps_a, t_a = _cpu_leg(oracle, args, 32768, cores, budget_s)
     one, reps_1, t_1 = _cpu_leg(oracle, args, 2048, 1, budget_s / 2)
     return {"value": round(allc, 4), "unit": "GiB/s", "cores": cores, "kind": "port",

@@ -21,12 +21,12 @@ rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"
 if fatal $rc; then echo "smoke crashed/hung: stopping"; exit $rc; fi
 
 echo "[gpu_check] $(date -u +%T) pytest -m gpu"
-timeout -k 10 900 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider "$@" > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider "$@" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed/hung: stopping"; exit $rc; fi
 
 echo "[gpu_check] $(date -u +%T) bench"
-timeout -k 10 600 python3 bench.py --steps 20 --warmup 3 --sweep > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python3 bench.py --steps 20 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
