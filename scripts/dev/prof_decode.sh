@@ -8,7 +8,7 @@ TAG=${1:-prof}
 shift || true
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-for t in 128 26 230; do
+for t in ${DENS:-128 26 230}; do
   timeout -k 10 120 python3 scripts/microbench.py --zero-thresh $t "$@" > "$OUT/mb_t$t.json" 2> "$OUT/mb_t$t.err"
   rc=$?; echo "microbench t$t rc=$rc"; cat "$OUT/mb_t$t.json"
   [ $rc -ne 0 ] && exit $rc
@@ -20,7 +20,7 @@ for set in \
   "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAVES" ; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$OUT/p$i" -o run -- \
-      python3 scripts/microbench.py --reps 2 --only decode,encode,decoded_size "$@" > "$OUT/p$i.log" 2>&1
+      python3 scripts/microbench.py --reps 2 --only ${ONLY:-decode,encode,decoded_size} "$@" > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$OUT/p$i.log"; exit $rc; }
