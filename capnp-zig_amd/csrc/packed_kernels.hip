@@ -657,12 +657,9 @@ __device__ __forceinline__ bool queue_take(uint32_t* q, uint32_t n, uint32_t lan
 
 __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
                                                  uint64_t out_off, uint64_t cap);
-__device__ __forceinline__ bool stream_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
-                                                 uint64_t out_off);
 
-// KIND 0: units encode_tiled_unit selects; 1: units decode_long_unit selects (the
-// read-message passes); 2: units stream_long_unit selects (the decoder's fallback).
-// One thread per unit; a wave appends its selected units with one atomic.
+// KIND 0: units encode_tiled_unit selects; 1: units decode_long_unit selects. One
+// thread per unit; a wave appends its selected units with one atomic.
 template <int KIND>
 __global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restrict__ in,
                                                           const uint64_t* __restrict__ in_off,
@@ -743,9 +740,8 @@ __global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restr
     const uint32_t u = blockIdx.x * 256 + threadIdx.x;
     bool p = false;
     if (u < n) {
-        p = KIND == 0   ? encode_tiled_unit(in, in_off[u], in_len[u])
-            : KIND == 1 ? decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u])
-                        : stream_long_unit(in, in_off[u], in_len[u], out, out_off[u]);
+        p = KIND == 0 ? encode_tiled_unit(in, in_off[u], in_len[u])
+                      : decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u]);
         // sentinel until the long-unit worker writes the unit's outcome: a unit the
         // worker never reached shows DEVICE_ERROR, not a stale status
         if (p) status[u] = kStPending;
@@ -2083,375 +2079,6 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 }
 
 // ---------------------------------------------------------------------------
-// DECODE, single pass, lane per unit (decode_stream_kernel)
-// ---------------------------------------------------------------------------
-// Lane l of a wave owns unit l and decodes it in one pass (message.zig:88-145):
-// every packed byte is read from HBM once and every output word written once.
-// Input side (as decode_index_kernel): lockstep by 64-B block, quad-coalesced loads
-// issued one round ahead into registers and written to a lane-major LDS ring (block
-// k at +16, block k-1's last piece at +0). Round k takes the records whose tags lie
-// in [64k - 16, 64k + 48) and the literal (FF-run) words whose 8 bytes lie below
-// 64k + 64.
-// Output side: one word per step (a mixed record's expansion through a v_perm
-// selector LUT, an FF record's first word, one literal word, or one zero word of a
-// 00 run), two steps per loop pass from one 28-B window of the ring (the second
-// step's bytes are selected from the window in registers: no second LDS round trip),
-// into the lane's 16-word LDS staging ring. When a lane's staging is full, every
-// lane's complete 64-B half-lines are stored by the whole wave: 4 lanes per
-// half-line, 16 half-lines (of 16 units) per 16-B store instruction.
-// Units of more than kFlPieces pieces go to the fallback (stream_long_unit).
-constexpr uint32_t kSmRing = 84;     // ring row stride in bytes: 80 used; 21 dwords keeps lanes' same-offset dword reads conflict-free
-#ifndef CPK_SM_STAGE
-#define CPK_SM_STAGE 16
-#endif
-constexpr uint32_t kSmStage = CPK_SM_STAGE;    // staging words per lane (16: two 64-B half-lines)
-constexpr uint32_t kSmStageRow = kSmStage + 1; // staging row stride in words (odd dword pairs: fewer bank conflicts)
-constexpr uint32_t kSmWaves = 2;     // waves per block (they share the expand LUT)
-
-// Units decode_stream_kernel leaves to the fallback (decode_wave_kernel<kWvLong>):
-// more packed pieces than the lockstep walk should carry (one long unit would hold
-// its 63 neighbours' wave), with an 8-aligned output slot.
-__device__ __forceinline__ bool stream_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
-                                                 uint64_t out_off) {
-    if (P == 0 || (reinterpret_cast<uintptr_t>(out + out_off) & 7)) return false;
-    const uint64_t s = reinterpret_cast<uintptr_t>(in + in_off) & 15;
-    return ((s + P + 15) >> 4) > kFlPieces;
-}
-
-__device__ __attribute__((aligned(16))) uint8_t cpk_sink_lanes[64 * 16];  // stores of lanes without a unit
-
-// Global-address-space (global_*, not flat_*) loads and stores: flat operations
-// count in lgkmcnt as well and complete out of order, so every wait on them is a
-// full drain; the kernel below counts its global operations exactly instead.
-typedef __attribute__((address_space(1))) u32x4 g_u32x4;
-typedef __attribute__((address_space(1))) uint64_t g_u64;
-// A 16-B load issued as inline asm: the compiler's wait insertion does not see it,
-// so it adds no wait of its own before the value's use (which, with a data-dependent
-// number of stores issued after the load, would be a near-full drain); the caller
-// waits with an exact s_waitcnt vmcnt before using the value.
-__device__ __forceinline__ u32x4 gload16_async(const void* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-
-__device__ __forceinline__ void vmcnt_at_most16(uint32_t c) {
-    switch (c) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
-}
-
-#ifdef CPK_STREAM_PROF
-// Diagnostic build: per-phase cycles and counts of decode_stream_kernel, summed over waves.
-__device__ unsigned long long cpk_stream_prof[8];
-#define SM_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define SM_ACC(i, d) sprof[i] += (d)
-#else
-#define SM_T(v) do { } while (0)
-#define SM_ACC(i, d) do { } while (0)
-#endif
-
-__global__ __launch_bounds__(kSmWaves * kWave) void decode_stream_kernel(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
-    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ out_cap,
-    uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
-    struct WaveLds {
-        uint32_t ring[kWave * kSmRing / 4 + 8];  // + over-read slack
-        uint64_t stage[kWave * kSmStageRow];
-    };
-    __shared__ __attribute__((aligned(16))) WaveLds lds_all[kSmWaves];
-    __shared__ uint64_t lut[256];  // tag -> v_perm selector scattering popc(tag) bytes (00: zero, FF: identity)
-    lut[threadIdx.x] = expand_selector(threadIdx.x);
-    lut[threadIdx.x + 128] = expand_selector(threadIdx.x + 128);
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    WaveLds& L = lds_all[wave];
-    const uint32_t unit = (blockIdx.x * kSmWaves + wave) * kWave + lane;
-    const bool valid = unit < n;
-
-    // ---- per-lane unit ---------------------------------------------------------------
-    const uint8_t* src = cpk_dummy16;
-    uint64_t P64 = 0, capw = 0;
-    uint8_t* dstb = nullptr;
-    int32_t st = ST_OK;
-    bool take = false, mine = false;
-    if (valid) {
-        src = in + in_off[unit];
-        P64 = in_len[unit];
-        dstb = out + out_off[unit];
-        capw = out_cap[unit] >> 3;
-        if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
-        const bool lng = st == ST_OK && stream_long_unit(in, in_off[unit], P64, out, out_off[unit]);
-        take = st == ST_OK && P64 > 0 && !lng;
-        mine = !lng;
-    }
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
-    const uint32_t npieces = (end + 15) >> 4;
-    const uint32_t nr = (end + 63) >> 6;
-    uint32_t maxr = nr;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
-    maxr = __builtin_amdgcn_readfirstlane(maxr);
-    uint8_t* const dst = take ? dstb : cpk_sink_lanes + 16 * lane;
-    // words at or past the slot capacity are counted, not stored (OUT_OF_SPACE)
-    const uint32_t capw32 = take ? (uint32_t)min(capw, (uint64_t)0xFFFFFFFFu) : 0u;
-
-    // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block -------------
-    const uint4* qsrc[4];
-    uint32_t qlast[4];
-#pragma unroll
-    for (uint32_t m = 0; m < 4; ++m) {
-        const uint32_t r = 16 * m + lane / 4;
-        const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
-        const uint32_t rn = __shfl(npieces, r, kWave);
-        qsrc[m] = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16);
-        qlast[m] = rn ? rn - 1 : 0u;
-    }
-    const uint32_t qp = lane & 3;
-    u32x4 d0, d1, d2, d3;
-    auto load = [&](uint32_t k) {  // four loads, waited for with vmcnt_at_most16(younger)
-        d0 = gload16_async(qsrc[0] + min(4 * k + qp, qlast[0]));
-        d1 = gload16_async(qsrc[1] + min(4 * k + qp, qlast[1]));
-        d2 = gload16_async(qsrc[2] + min(4 * k + qp, qlast[2]));
-        d3 = gload16_async(qsrc[3] + min(4 * k + qp, qlast[3]));
-    };
-    uint32_t* const wq = L.ring + (lane / 4) * (kSmRing / 4) + 4 + 4 * qp;  // dword view (ring: 7-dword window reads)
-    uint32_t* const ring = L.ring + lane * (kSmRing / 4);
-    uint64_t* const stage = L.stage + lane * kSmStageRow;
-
-    constexpr uint32_t kDead = 0xFFFFFFF0u;  // position of a lane with nothing (more) to decode
-    uint32_t pos = take ? s : kDead;  // next record / literal word (aligned space)
-    uint32_t w = 0;                   // words produced
-    uint32_t rem = 0;                 // pending words of a 00 run (zero) or an FF run (literal)
-    uint32_t litv = 0;                // 1: the pending words are literal
-    uint32_t younger = 0;             // vector-memory ops issued after the newest loads
-
-    uint32_t fw = 0;  // words stored (a multiple of 8 until the end)
-
-    // Store every lane's complete half-lines [fw, w): instruction (j, g) takes the j-th
-    // half-line of lanes 16g .. 16g+15, 4 lanes x 16 B each. The owners' addresses come
-    // by cross-lane permute, all issued before the staging reads and the stores, so the
-    // latencies overlap. A half-line that crosses the slot capacity goes word by word
-    // from its lane.
-    auto flush = [&]() {
-        const uint32_t nh = (w >> 3) - (fw >> 3);  // complete half-lines: 0 .. kSmStage / 8
-        const uint32_t o = lane >> 2, qq = lane & 3u;
-        const bool f0 = (nh > 0) & (fw + 8 <= capw32), f1 = (kSmStage > 8) & (nh > 1) & (fw + 16 <= capw32);
-        const uint64_t m0 = __builtin_amdgcn_ballot_w64(f0), m1 = __builtin_amdgcn_ballot_w64(f1);
-        const uint32_t passes = m1 ? 2u : (m0 ? 1u : 0u);  // wave-uniform
-        if (passes) {
-            const uint64_t ga = reinterpret_cast<uint64_t>(dst) + 8ull * fw;
-            uint64_t oga[4];
-            uint32_t osl[4];
-#pragma unroll
-            for (uint32_t g = 0; g < 4; ++g) {  // owner 16g + o: address and staging slot of its fw
-                oga[g] = __shfl(ga, 16 * g + o, kWave);
-                osl[g] = __shfl(fw, 16 * g + o, kWave) & (kSmStage - 1);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < 2; ++j) {
-                if (j >= passes) break;
-                const uint64_t m = j ? m1 : m0;
-                u32x4 v[4];
-#pragma unroll
-                for (uint32_t g = 0; g < 4; ++g) {
-                    const uint32_t ow = 16 * g + o;
-                    const uint64_t* const sp =
-                        L.stage + ow * kSmStageRow + ((osl[g] + 8 * j + 2 * qq) & (kSmStage - 1));
-                    const uint64_t a0 = sp[0], a1 = sp[1];
-                    v[g] = u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)};
-                }
-#pragma unroll
-                for (uint32_t g = 0; g < 4; ++g) {
-                    // a group without a half-line issues no store (exec = 0 skips it), so the
-                    // count below is exact either way
-                    if ((m >> (16 * g + o)) & 1ull)
-                        __builtin_nontemporal_store(v[g], (g_u32x4*)(reinterpret_cast<uint8_t*>(oga[g]) + 64 * j + 16 * qq));
-                    younger += ((m >> (16 * g)) & 0xFFFFull) != 0;
-                }
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 2; ++j) {
-            const uint32_t hb = fw + 8 * j;
-            const bool slow = (nh > j) & (hb + 8 > capw32) & (hb < capw32);
-            if (__builtin_amdgcn_ballot_w64(slow)) {
-                for (uint32_t i = 0; i < 8; ++i) {
-                    const bool go = slow & (hb + i < capw32);
-                    if (__builtin_amdgcn_ballot_w64(go)) {
-                        if (go) __builtin_nontemporal_store(stage[(hb + i) & (kSmStage - 1)],
-                                                            (g_u64*)(dst + 8ull * (hb + i)));
-                        ++younger;
-                    }
-                }
-            }
-        }
-        fw = w & ~7u;
-    };
-
-#ifdef CPK_STREAM_PROF
-    uint64_t sprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    SM_T(tstart);
-    if (maxr > 0) load(0);
-    for (uint32_t k = 0; k <= maxr; ++k) {
-        SM_T(tr0);
-        SM_ACC(5, 1);
-        if (k < maxr) vmcnt_at_most16(younger);  // round k's loads landed (younger ops: stores)
-        if (k > 0) {
-            wave_lds_sync();  // every lane is done with round k-1's ring reads
-            const uint32_t m0 = ring[16], m1 = ring[17], m2 = ring[18], m3 = ring[19];
-            ring[0] = m0;
-            ring[1] = m1;
-            ring[2] = m2;
-            ring[3] = m3;
-            wave_lds_sync();
-        }
-        if (k < maxr) {
-            constexpr uint32_t R = kSmRing / 4 * 16;  // 16 units further down the ring
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                wq[e] = d0[e];
-                wq[R + e] = d1[e];
-                wq[2 * R + e] = d2[e];
-                wq[3 * R + e] = d3[e];
-            }
-            if (k + 1 < maxr) {
-                load(k + 1);
-                younger = 0;
-            }
-            wave_lds_sync();
-        }
-        SM_T(tr1);
-        SM_ACC(0, tr1 - tr0);
-        const uint32_t ob = 64 * k - 16;                     // ring offset o = pos - ob
-        const uint32_t tlim = min(ob + 64, end);             // tags of pieces 4k-1 .. 4k+2
-        const uint32_t llim = k < maxr ? ob + 80 : ob + 16;  // literal words: bytes below this
-        for (;;) {
-            // a lane wants a step while this round's window holds its next word (a finished
-            // or failed lane sits at kDead with no pending run); it needs room for two words
-            const bool have = rem != 0;
-            const uint32_t need = have ? (litv ? pos + 8u : 0u) : pos + 1u;
-            const bool want = need <= (have ? llim : tlim);
-            const bool room = w - fw < kSmStage;  // a full ring holds a complete half-line
-            const bool act = want & room;
-            if (__builtin_amdgcn_ballot_w64(want & !room)) {  // a full staging ring: store
-                SM_T(tf0);
-                flush();
-                SM_T(tf1);
-                SM_ACC(2, tf1 - tf0);
-                SM_ACC(4, 1);
-                continue;
-            }
-            if (__builtin_amdgcn_ballot_w64(act) == 0) break;  // nothing left in this round's window
-            SM_ACC(3, 1);
-            // ring bytes o .. o+23 from the 7 aligned dwords that hold them (records: o < 64,
-            // literal words: o <= 72), byte-aligned with v_alignbyte_b32
-            const uint32_t o = act ? pos - ob : 0u;
-            const uint32_t* const rq = ring + (o >> 2);
-            const uint32_t r = o & 3u;
-            uint32_t U[6];
-            {
-                uint32_t v[7];
-#pragma unroll
-                for (int i = 0; i < 7; ++i) v[i] = rq[i];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) U[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], r);
-            }
-            // one step on window bytes b0 (0-3), b1 (4-7), b2 (8-11): returns the bytes it took
-            auto step = [&](bool a, uint32_t b0, uint32_t b1, uint32_t b2) -> uint32_t {
-                const uint32_t p0 = __builtin_amdgcn_alignbyte(b1, b0, 1), p1 = __builtin_amdgcn_alignbyte(b2, b1, 1);
-                const uint32_t c9 = (b2 >> 8) & 0xFFu;
-                const uint32_t t = b0 & 0xFFu;
-                const bool hv = rem != 0;
-                const bool rec = !hv;
-                const bool z = t == 0u, f = t == 0xFFu;
-                // message.zig:97-142: 00 -> c+1 zero words; FF -> 8 bytes + c literal words;
-                // other tags -> the nonzero bytes scattered by the tag. Truncation
-                // (message.zig:152-191).
-                const uint32_t len = 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u);
-                const bool eof = a & rec & (pos + len > end);
-                const uint64_t sel = lut[rec ? t : 0u];  // 00 / zero-run word: all-zero selector
-                const bool lw = hv & (litv != 0);        // a literal word of an FF run
-                const uint32_t x0 = lw ? b0 : __builtin_amdgcn_perm(p1, p0, (uint32_t)sel);
-                const uint32_t x1 = lw ? b1 : __builtin_amdgcn_perm(p1, p0, (uint32_t)(sel >> 32));
-                const bool put = a & !eof;
-                if (put) stage[w & (kSmStage - 1)] = (uint64_t)x0 | ((uint64_t)x1 << 32);
-                if (eof) st = ST_EOF;
-                // next state, as selects on masks (no branches): records start runs, runs count down
-                const uint32_t mz = 0u - (uint32_t)z, mf = 0u - (uint32_t)f;
-                const uint32_t runw = ((p0 & 0xFFu) & mz) | (c9 & mf);  // words of the run after this word
-                const uint32_t adv = rec ? ((10u & mf) | (len & ~mf)) : (lw ? 8u : 0u);
-                const uint32_t nrem = rec ? runw : rem - 1u;
-                const uint32_t nlit = rec ? (f ? 1u : 0u) : litv;
-                pos = eof ? kDead : (a ? pos + adv : pos);
-                rem = eof ? 0u : (a ? nrem : rem);
-                litv = a ? nlit : litv;
-                w += (uint32_t)put;
-                return put ? adv : 0u;
-            };
-            const uint32_t d = step(act, U[0], U[1], U[2]);
-            // second step: same window, bytes d .. d+11 (d <= 10)
-            const bool have2 = rem != 0;
-            const uint32_t need2 = have2 ? (litv ? pos + 8u : 0u) : pos + 1u;
-            const bool act2 = act & (need2 <= (have2 ? llim : tlim)) & (w - fw < kSmStage);
-            const uint32_t qb = d >> 2, rb = d & 3u;
-            const uint32_t V0 = qb == 0 ? U[0] : (qb == 1 ? U[1] : U[2]);
-            const uint32_t V1 = qb == 0 ? U[1] : (qb == 1 ? U[2] : U[3]);
-            const uint32_t V2 = qb == 0 ? U[2] : (qb == 1 ? U[3] : U[4]);
-            const uint32_t V3 = qb == 0 ? U[3] : (qb == 1 ? U[4] : U[5]);
-            (void)step(act2, __builtin_amdgcn_alignbyte(V1, V0, rb), __builtin_amdgcn_alignbyte(V2, V1, rb),
-                       __builtin_amdgcn_alignbyte(V3, V2, rb));
-        }
-    }
-    // the complete half-lines still staged, then the last, partial one (words below
-    // the capacity)
-    flush();
-    {
-        const uint32_t h = w & ~7u;
-        for (uint32_t j = 0; j < 7; ++j) {
-            const bool go = (h + j < w) & (h + j < capw32);
-            if (__builtin_amdgcn_ballot_w64(go)) {
-                if (go) __builtin_nontemporal_store(stage[(h + j) & (kSmStage - 1)], (g_u64*)(dst + 8ull * (h + j)));
-                ++younger;
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef CPK_STREAM_PROF
-    SM_T(tend);
-    sprof[6] += tend - tstart;
-    if (lane == 0)
-        for (int i = 0; i < 7; ++i) atomicAdd(&cpk_stream_prof[i], (unsigned long long)sprof[i]);
-#endif
-    if (!mine) return;  // the fallback's unit
-    if (st != ST_OK) {
-        out_len[unit] = 0;
-        status[unit] = st;
-        return;
-    }
-    out_len[unit] = 8ull * w;
-    status[unit] = (uint64_t)w > capw ? ST_SPACE : ST_OK;
-}
-
-// ---------------------------------------------------------------------------
 // Reader.readPackedMessage, batched (reader.zig:84-156)
 // ---------------------------------------------------------------------------
 // Unit i is one reader's buffered packed stream; one message is decoded from its
@@ -2842,17 +2469,18 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
             in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
         return hipGetLastError();
     }
-    // single-pass decoder; the fallback owns the long units from the start
-    // (stream_long_unit): it goes first, on the side stream, beside the main grid
+    // index pass, fill pass; the fallback owns the long units from the start
+    // (decode_long_unit): it goes first, on the side stream, beside passes 1 and 2
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-    select_long_kernel<2><<<(n + 255) / 256, 256, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off, out_cap,
+    select_long_kernel<1><<<(n + 255) / 256, 256, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      q, status);
     decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
         in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
-    decode_stream_kernel<<<(n + kSmWaves * kWave - 1) / (kSmWaves * kWave), kSmWaves * kWave, 0, stream>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
+    launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+    decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_len,
+                                                                       out_cap, status);
     const hipError_t e = hipGetLastError();
     const hipError_t j = side.join();
     return e != hipSuccess ? e : j;
@@ -2935,15 +2563,6 @@ hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t*
 }
 
 }  // namespace cpk
-
-#ifdef CPK_STREAM_PROF
-// Diagnostic build only: read and clear the single-pass decoder's phase sums.
-extern "C" int capnp_packed_debug_stream_prof(unsigned long long* out8) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_stream_prof), sizeof(z)) != hipSuccess) return 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(cpk::cpk_stream_prof), z, sizeof(z)) != hipSuccess;
-}
-#endif
 
 #ifdef CPK_FILL_PROF
 // Diagnostic build only: read and clear the fill-kernel phase cycle sums.
