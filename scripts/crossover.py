@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Single-buffer crossover for the Zig drop-in: latency of one
+packPacked / unpackPacked call through the C-ABI single-buffer entry points
+(capnp_packed_encode / capnp_packed_decode: H2D, kernels, D2H, sync) against the CPU
+oracle on one core (oracle/packed_oracle.c, a restatement of message.zig:88-271), for one
+unit of 64 B .. 16 MiB of the bench's byte distribution (p = 0.5). Prints one JSON
+object; the threshold is the smallest size from which the GPU call is faster."""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "capnp-zig_amd"))
+sys.path.insert(0, os.path.join(HERE, "..", "tests"))
+
+import capnp_packed as cp  # noqa: E402
+import oracle  # noqa: E402
+
+
+def t_us(fn, budget=0.3, max_reps=2000):
+    fn()
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or (time.perf_counter() - t0 < budget and reps < max_reps):
+        fn()
+        reps += 1
+    return (time.perf_counter() - t0) / reps * 1e6
+
+
+def main():
+    thr = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    rows = []
+    size = 64
+    while size <= 16 << 20:
+        data = oracle.generate(1, size, seed=0xC0DE0008, zero_thresh=thr).tobytes()
+        st, packed = oracle.pack(data)
+        assert st == 0
+        assert cp.pack_packed(data) == packed and cp.unpack_packed(packed) == data
+        row = {"bytes": size, "packed": len(packed),
+               "cpu_pack_us": t_us(lambda: oracle.pack(data)),
+               "cpu_unpack_us": t_us(lambda: oracle.unpack(packed)),
+               "gpu_pack_us": t_us(lambda: cp.pack_packed(data)),
+               "gpu_unpack_us": t_us(lambda: cp.unpack_packed(packed))}
+        rows.append({k: (round(v, 2) if isinstance(v, float) else v) for k, v in row.items()})
+        print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+        size *= 4
+    out = {"zero_thresh": thr, "rows": rows}
+    for op in ("pack", "unpack"):
+        win = [r["bytes"] for r in rows if r[f"gpu_{op}_us"] < r[f"cpu_{op}_us"]]
+        out[f"{op}_gpu_faster_from_bytes"] = min(win) if win else None
+    out["note"] = ("one unit per call; GPU = single-buffer C-ABI (pageable host buffers, one device "
+                   "context, H2D + launches + D2H + sync); CPU = oracle, one thread")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
