@@ -48,6 +48,16 @@ MESSAGE_TOO_LARGE = 11
 INVALID_PACKED_MESSAGE = 12
 # Message.init (message.zig:341-394)
 TRUNCATED_MESSAGE = 13
+# Message.validate (message.zig:699-969)
+EMPTY_MESSAGE = 14
+NESTING_LIMIT_EXCEEDED = 15
+INVALID_SEGMENT_ID = 16
+INVALID_POINTER = 17
+OUT_OF_BOUNDS = 18
+TRAVERSAL_LIMIT_EXCEEDED = 19
+INVALID_FAR_POINTER = 20
+INVALID_INLINE_COMPOSITE_POINTER = 21
+LIST_TOO_LARGE = 22
 
 
 class PackedError(Exception):
@@ -107,10 +117,49 @@ class TruncatedMessage(PackedError):  # message.zig:353/380
     status = TRUNCATED_MESSAGE
 
 
+# Message.validate (message.zig:699-969)
+class EmptyMessage(PackedError):  # :700
+    status = EMPTY_MESSAGE
+
+
+class NestingLimitExceeded(PackedError):  # :717
+    status = NESTING_LIMIT_EXCEEDED
+
+
+class InvalidSegmentId(PackedError):  # :718 / :421 / :739
+    status = INVALID_SEGMENT_ID
+
+
+class InvalidPointer(PackedError):  # :731
+    status = INVALID_POINTER
+
+
+class OutOfBounds(PackedError):  # bounds.zig:10-13
+    status = OUT_OF_BOUNDS
+
+
+class TraversalLimitExceeded(PackedError):  # :711
+    status = TRAVERSAL_LIMIT_EXCEEDED
+
+
+class InvalidFarPointer(PackedError):  # :752-758
+    status = INVALID_FAR_POINTER
+
+
+class InvalidInlineCompositePointer(PackedError):  # :600-612 / :944
+    status = INVALID_INLINE_COMPOSITE_POINTER
+
+
+class ListTooLarge(PackedError):  # :949
+    status = LIST_TOO_LARGE
+
+
 _ERRORS = {c.status: c for c in (InvalidMessageSize, UnexpectedEof, Overflow, OutOfSpace,
                                  InvalidArgument, DeviceError, NoDevice, EndOfStream, InvalidSegmentCount,
                                  SegmentCountLimitExceeded, MessageTooLarge, InvalidPackedMessage,
-                                 TruncatedMessage)}
+                                 TruncatedMessage, EmptyMessage, NestingLimitExceeded, InvalidSegmentId,
+                                 InvalidPointer, OutOfBounds, TraversalLimitExceeded, InvalidFarPointer,
+                                 InvalidInlineCompositePointer, ListTooLarge)}
 
 
 _lib = None
@@ -142,6 +191,8 @@ SIGNATURES = {
                                                          _vp, _vp]),
     "capnp_packed_message_init_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp,
                                                        _vp, _vp, _vp]),
+    "capnp_packed_validate_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint64,
+                                                   ctypes.c_uint64, ctypes.c_uint32, _vp, _vp, _vp]),
     "capnp_packed_scan_scratch_bytes": (_sz, [ctypes.c_uint32]),
     "capnp_packed_lengths_to_offsets": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp,
                                                        _sz, _vp]),
@@ -309,6 +360,25 @@ class Message:
         msg = cls.init(unpacked)
         msg.backing_data = unpacked
         return msg
+
+    def validate(self, segment_count_limit=None, traversal_limit_words=None, nesting_limit=None,
+                 device="cuda") -> int:
+        """message.zig:699-969 Message.validate(options), run by validate_batch on the
+        device over this message's segments (re-framed: header + segments, the bytes
+        Message.init parsed). Raises the reference's error; returns the traversal words
+        consumed. Arguments left None take ValidationOptions' defaults (:331-335)."""
+        framed = np.frombuffer(frame_segments(self.segments), dtype=np.uint8)
+        d_in = torch.from_numpy(framed.copy()).to(device)
+        off = torch.zeros(1, dtype=torch.int64, device=device)
+        ln = torch.full((1,), framed.size, dtype=torch.int64, device=device)
+        st = torch.full((1,), -1, dtype=torch.int32, device=device)
+        words = torch.zeros(1, dtype=torch.int64, device=device)
+        validate_batch(d_in, off, ln, st, words,
+                       DEFAULT_SEGMENT_COUNT_LIMIT if segment_count_limit is None else segment_count_limit,
+                       DEFAULT_TRAVERSAL_LIMIT_WORDS if traversal_limit_words is None else traversal_limit_words,
+                       DEFAULT_NESTING_LIMIT if nesting_limit is None else nesting_limit)
+        _raise(int(st.item()), "Message.validate")
+        return int(words.item())
 
     def deinit(self) -> None:
         self.segments = []
@@ -612,6 +682,24 @@ def message_init_batch(d_in, in_off, in_len, max_segs, seg_count, seg_off, seg_l
     _raise(lib().capnp_packed_message_init_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, max_segs,
                                                  _ptr(seg_count), _ptr(seg_off), _ptr(seg_len), _ptr(status),
                                                  _stream(stream)), "message_init_batch")
+
+
+# Message.ValidationOptions defaults (message.zig:331-335)
+DEFAULT_SEGMENT_COUNT_LIMIT = MAX_SEGMENT_COUNT
+DEFAULT_TRAVERSAL_LIMIT_WORDS = 8 * 1024 * 1024
+DEFAULT_NESTING_LIMIT = 64
+
+
+def validate_batch(d_in, in_off, in_len, status, words=None, segment_count_limit=DEFAULT_SEGMENT_COUNT_LIMIT,
+                   traversal_limit_words=DEFAULT_TRAVERSAL_LIMIT_WORDS, nesting_limit=DEFAULT_NESTING_LIMIT,
+                   stream=None) -> None:
+    """Message.validate (message.zig:699-969) of a batch of framed messages (the bytes
+    Message.init takes): status[i] = 0 or the reference's first error for message i;
+    words[i] (optional int64) = traversal words the walk consumed (0 on error)."""
+    n = _units(in_off, in_len, status, words)
+    _raise(lib().capnp_packed_validate_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, segment_count_limit,
+                                             traversal_limit_words, nesting_limit, _ptr(status), _ptr(words),
+                                             _stream(stream)), "validate_batch")
 
 
 def lengths_to_offsets(lengths, base: int = 0, out=None, stream=None):

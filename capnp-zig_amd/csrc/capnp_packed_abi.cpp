@@ -173,6 +173,15 @@ const char* capnp_packed_status_name(int status) {
         case CAPNP_PACKED_MESSAGE_TOO_LARGE: return "MessageTooLarge";
         case CAPNP_PACKED_INVALID_PACKED_MESSAGE: return "InvalidPackedMessage";
         case CAPNP_PACKED_TRUNCATED_MESSAGE: return "TruncatedMessage";
+        case CAPNP_PACKED_EMPTY_MESSAGE: return "EmptyMessage";
+        case CAPNP_PACKED_NESTING_LIMIT_EXCEEDED: return "NestingLimitExceeded";
+        case CAPNP_PACKED_INVALID_SEGMENT_ID: return "InvalidSegmentId";
+        case CAPNP_PACKED_INVALID_POINTER: return "InvalidPointer";
+        case CAPNP_PACKED_OUT_OF_BOUNDS: return "OutOfBounds";
+        case CAPNP_PACKED_TRAVERSAL_LIMIT_EXCEEDED: return "TraversalLimitExceeded";
+        case CAPNP_PACKED_INVALID_FAR_POINTER: return "InvalidFarPointer";
+        case CAPNP_PACKED_INVALID_INLINE_COMPOSITE_POINTER: return "InvalidInlineCompositePointer";
+        case CAPNP_PACKED_LIST_TOO_LARGE: return "ListTooLarge";
         default: return "Unknown";
     }
 }
@@ -348,6 +357,20 @@ int capnp_packed_message_init_batch(const uint8_t* d_in, const uint64_t* d_in_of
     hipError_t e = cpk::launch_message_init(d_in, d_in_off, d_in_len, n, max_segs, d_seg_count, d_seg_off, d_seg_len,
                                             d_status, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "message-init launch");
+}
+
+int capnp_packed_validate_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                uint32_t n, uint64_t segment_count_limit, uint64_t traversal_limit_words,
+                                uint32_t nesting_limit, int32_t* d_status, uint64_t* d_words, void* stream) {
+    if (n == 0) return CAPNP_PACKED_OK;
+    if (!d_in_off || !d_in_len || !d_status) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null batch pointer");
+    if (nesting_limit > 64)
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "nesting_limit above 64 (the device stack depth)");
+    int st = ensure_device();
+    if (st) return st;
+    hipError_t e = cpk::launch_validate(d_in, d_in_off, d_in_len, n, segment_count_limit, traversal_limit_words,
+                                        nesting_limit, d_status, d_words, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "validate launch");
 }
 
 size_t capnp_packed_scan_scratch_bytes(uint32_t n) { return cpk::scan_scratch_bytes(n); }

@@ -36,6 +36,11 @@ hipError_t launch_message_init(const uint8_t* in, const uint64_t* in_off, const 
                                uint32_t max_segs, uint32_t* seg_count, uint64_t* seg_off, uint64_t* seg_len,
                                int32_t* status, hipStream_t stream);
 
+// Message.validate (message.zig:699-969) of framed messages.
+hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                           uint64_t seg_limit, uint64_t trav_limit, uint32_t nest_limit, int32_t* status,
+                           uint64_t* words, hipStream_t stream);
+
 hipError_t launch_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
                            uint64_t seed, uint32_t thr, hipStream_t stream);
 

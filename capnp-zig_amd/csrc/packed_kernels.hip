@@ -58,6 +58,16 @@ enum : int32_t {
     ST_TOOLARGE = CAPNP_PACKED_MESSAGE_TOO_LARGE,
     ST_OVERSHOOT = CAPNP_PACKED_INVALID_PACKED_MESSAGE,
     ST_TRUNC = CAPNP_PACKED_TRUNCATED_MESSAGE,  // Message.init (message.zig:353/380)
+    // Message.validate (message.zig:699-969)
+    ST_EMPTY = CAPNP_PACKED_EMPTY_MESSAGE,
+    ST_NEST = CAPNP_PACKED_NESTING_LIMIT_EXCEEDED,
+    ST_SEGID = CAPNP_PACKED_INVALID_SEGMENT_ID,
+    ST_PTR = CAPNP_PACKED_INVALID_POINTER,
+    ST_OOB = CAPNP_PACKED_OUT_OF_BOUNDS,
+    ST_TRAV = CAPNP_PACKED_TRAVERSAL_LIMIT_EXCEEDED,
+    ST_FAR = CAPNP_PACKED_INVALID_FAR_POINTER,
+    ST_ICP = CAPNP_PACKED_INVALID_INLINE_COMPOSITE_POINTER,
+    ST_LIST = CAPNP_PACKED_LIST_TOO_LARGE,
 };
 // internal status between decode passes: the unit goes to a full (fallback) decoder
 constexpr int32_t kStNeedFull = 0x7FFF0001;
@@ -2079,6 +2089,235 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 }
 
 // ---------------------------------------------------------------------------
+// Message.validate, batched (message.zig:699-969)
+// ---------------------------------------------------------------------------
+// Lane per framed message: Message.init's segment-table parse (message.zig:341-394),
+// then the reference's recursive depth-first traversal (validatePointer and the
+// struct / list / far / inline-composite validators) as a loop over an explicit
+// stack of pointer runs in LDS. A frame is one run of pointer words still to visit:
+// the current element's remaining pointers (pleft of pw, from byte `cur` of segment
+// `seg`) and the elements after it (eleft, each dw data words then pw pointers), at
+// the nesting value the reference passes to validatePointer for them. Pushing a
+// frame always spends a nesting level, so the stack never holds more than the
+// nesting limit (<= kVdDepth) frames. Visiting order, limit consumption and every
+// check follow the reference line by line, so the first error is the one it raises.
+constexpr uint32_t kVdDepth = 64;  // supported nesting limit (the reference default)
+
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t* p) {  // unaligned-safe 8-B load
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+__device__ __forceinline__ int64_t ptr_offset_words(uint64_t w) {  // message.zig:11-18
+    const uint32_t raw = (uint32_t)((w >> 2) & 0x3FFFFFFFu);
+    return (raw & 0x20000000u) ? (int64_t)raw - ((int64_t)1 << 30) : (int64_t)raw;
+}
+
+__global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restrict__ in,
+                                                         const uint64_t* __restrict__ in_off,
+                                                         const uint64_t* __restrict__ in_len, uint32_t n,
+                                                         uint64_t seg_limit, uint64_t trav_limit, uint32_t nest_limit,
+                                                         int32_t* __restrict__ status, uint64_t* __restrict__ words) {
+    __shared__ uint4 stack_all[kVdDepth * kWave];  // frame f of lane l at [f * 64 + l]
+    const uint32_t lane = lane_id();
+    const uint32_t msg = blockIdx.x * kWave + lane;
+    if (msg >= n) return;
+    const uint8_t* const d = in + in_off[msg];
+    const uint64_t len = in_len[msg];
+    auto u32at = [&](uint64_t o) { return (uint32_t)d[o] | ((uint32_t)d[o + 1] << 8) | ((uint32_t)d[o + 2] << 16) |
+                                          ((uint32_t)d[o + 3] << 24); };
+    int32_t st = ST_OK;
+    uint64_t rem = trav_limit;
+    // ---- Message.init (message.zig:341-394) --------------------------------------------
+    uint32_t nseg = 0;
+    uint64_t header = 0;
+    if (len >= 0x100000000ull) st = ST_ARG;  // byte offsets in the frames are u32
+    else if (len < 4) st = ST_EOS;
+    else {
+        const uint32_t m1 = u32at(0);
+        if (m1 == 0xFFFFFFFFu) st = ST_SEGCOUNT;
+        else if ((uint64_t)m1 + 1 > kMsgMaxSegs) st = ST_SEGLIMIT;
+        else {
+            nseg = m1 + 1;
+            header = 4ull * (1 + nseg + ((nseg & 1) ? 0 : 1));
+            if (header > len) st = ST_TRUNC;
+            uint64_t o = header;
+            for (uint32_t i = 0; st == ST_OK && i < nseg; ++i) {
+                o += 8ull * u32at(4 + 4 * i);
+                if (o > len) st = ST_TRUNC;
+            }
+        }
+    }
+    // ---- validate (:699-708) ---------------------------------------------------------
+    uint32_t cseg = 0;  // cached segment: byte offset in the message and length
+    uint64_t coff = header, clen = 0;
+    if (st == ST_OK) {
+        clen = 8ull * u32at(4);
+        if (nseg > seg_limit) st = ST_SEGLIMIT;
+        else if (clen < 8) st = ST_TRUNC;
+    }
+    auto seg_at = [&](uint32_t id) {  // caller guarantees id < nseg
+        if (id != cseg) {
+            uint64_t o = header;
+            for (uint32_t i = 0; i < id; ++i) o += 8ull * u32at(4 + 4 * i);
+            cseg = id;
+            coff = o;
+            clen = 8ull * u32at(4 + 4 * id);
+        }
+    };
+    auto word_at = [&](uint32_t seg, uint64_t pos) { seg_at(seg); return ld_u64(d + coff + pos); };
+    auto in_bounds = [&](uint32_t seg, uint64_t off, uint64_t size) {  // bounds.zig:10-13
+        seg_at(seg);
+        return off + size >= off && off + size <= clen;
+    };
+    uint4* const stk = stack_all + lane;
+    uint32_t depth = 0;
+    auto push = [&](uint32_t seg, uint64_t cur, uint32_t pleft, uint32_t pw, uint32_t eleft, uint32_t dw,
+                    uint32_t nest) {
+        stk[kWave * depth] = make_uint4((uint32_t)cur, eleft, pleft | (pw << 16), dw | (seg << 16) | (nest << 26));
+        ++depth;
+    };
+    auto consume = [&](uint64_t w) {  // :710-713
+        if (w > rem) return false;
+        rem -= w;
+        return true;
+    };
+    // the pending pointer (validatePointer's arguments); the root first
+    bool pend = st == ST_OK;
+    uint32_t pseg = 0, pnest = nest_limit;
+    uint64_t ppos = 0, pword = pend ? word_at(0, 0) : 0;
+    while (st == ST_OK) {
+        if (!pend) {  // next pointer of the top run, or pop it
+            if (depth == 0) break;
+            uint4 f = stk[kWave * (depth - 1)];
+            const uint32_t pleft = f.z & 0xFFFFu, pw = f.z >> 16, dw = f.w & 0xFFFFu;
+            const uint32_t seg = (f.w >> 16) & 0x3FFu, nest = f.w >> 26;
+            if (pleft) {
+                pseg = seg;
+                ppos = f.x;
+                pword = word_at(seg, f.x);
+                pnest = nest;
+                pend = true;
+                f.x += 8;
+                f.z -= 1;
+            } else if (f.y) {
+                f.y -= 1;
+                f.x += 8 * dw;  // the next element's pointer section
+                f.z |= pw;
+            } else {
+                --depth;
+                continue;
+            }
+            stk[kWave * (depth - 1)] = f;
+            continue;
+        }
+        pend = false;
+        // ---- validatePointer (:715-732) ------------------------------------------------
+        if (pword == 0) continue;
+        if (pnest == 0) { st = ST_NEST; break; }
+        if (pseg >= nseg) { st = ST_SEGID; break; }
+        const uint32_t type = (uint32_t)pword & 3u;
+        if (type == 3) { st = ST_PTR; break; }
+        const uint32_t nest = pnest - 1;
+        // a list or inline-composite run to validate: (seg, content offset, pointer word,
+        // content given (double far), layout B tag position)
+        uint32_t lseg = pseg;
+        uint64_t lword = pword, lov = 0;
+        bool has_ov = false;
+        if (type == 2) {  // ---- validateFarPointer (:734-759) ------------------------------
+            const bool dbl = (pword >> 2) & 1u;
+            const uint64_t landing = ((pword >> 3) & 0x1FFFFFFFu) * 8;
+            const uint32_t fseg = (uint32_t)(pword >> 32);
+            if (fseg >= nseg) { st = ST_SEGID; break; }
+            if (!in_bounds(fseg, landing, dbl ? 16 : 8)) { st = ST_OOB; break; }
+            if (!dbl) {  // the landing word is the pointer: validatePointer at the same nesting
+                pseg = fseg;
+                ppos = landing;
+                pword = word_at(fseg, landing);
+                pnest = nest;
+                pend = true;
+                continue;
+            }
+            const uint64_t lw = word_at(fseg, landing), tw = word_at(fseg, landing + 8);
+            if ((lw & 3) != 2 || ((lw >> 2) & 1u)) { st = ST_FAR; break; }
+            const uint32_t s2 = (uint32_t)(lw >> 32);
+            if (s2 >= nseg) { st = ST_SEGID; break; }
+            const uint64_t eo = ((lw >> 3) & 0x1FFFFFFFu) * 8;
+            if ((tw & 3) == 0) {  // validateInlineCompositeTag (:940-969)
+                const int64_t cs = ptr_offset_words(tw);
+                if (cs < 0) { st = ST_ICP; break; }
+                const uint64_t count = (uint64_t)cs, dw = (tw >> 32) & 0xFFFFu, pw = tw >> 48;
+                const uint64_t tot = count * (dw + pw);
+                seg_at(s2);
+                if (eo > clen || tot * 8 > clen - eo) { st = ST_OOB; break; }
+                if (!consume(tot)) { st = ST_TRAV; break; }
+                if (pw && count) push(s2, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest);
+                continue;
+            }
+            if ((tw & 3) != 1) { st = ST_FAR; break; }
+            lseg = s2;  // validateListPointer(landing seg, 0, tag, elements offset)
+            lword = tw;
+            lov = eo;
+            has_ov = true;
+        }
+        if (type == 0) {  // ---- validateStructPointer (:761-799) -----------------------------
+            const uint64_t ds = (pword >> 32) & 0xFFFFu, pc = pword >> 48;
+            const int64_t so_s = (int64_t)ppos + 8 + ptr_offset_words(pword) * 8;
+            if (so_s < 0) { st = ST_OOB; break; }
+            const uint64_t so = (uint64_t)so_s;
+            seg_at(pseg);
+            if (so > clen || (ds + pc) * 8 > clen - so) { st = ST_OOB; break; }
+            if (!consume(ds + pc)) { st = ST_TRAV; break; }
+            if (pc) push(pseg, so + 8 * ds, (uint32_t)pc, (uint32_t)pc, 0, 0, nest);
+            continue;
+        }
+        // ---- validateListPointer (:801-893) ---------------------------------------------
+        const uint32_t es = (uint32_t)(lword >> 32) & 7u;
+        const uint64_t wc = lword >> 35;  // element count, or word count for inline composite
+        if (es == 7) {
+            // inline composite: the tag at the pointer's target (:586-627, validated by
+            // :895-923) or, behind a double far, at the landing pad's target (:815-857)
+            uint64_t tag_pos;
+            if (has_ov) {
+                tag_pos = lov;
+            } else {
+                const int64_t tp = (int64_t)ppos + 8 + ptr_offset_words(lword) * 8;
+                if (tp < 0) { st = ST_OOB; break; }
+                tag_pos = (uint64_t)tp;
+            }
+            if (!in_bounds(lseg, tag_pos, 8)) { st = ST_OOB; break; }
+            const uint64_t tag = word_at(lseg, tag_pos);
+            if ((tag & 3) != 0) { st = ST_ICP; break; }
+            const int64_t cs = ptr_offset_words(tag);
+            if (cs < 0) { st = ST_ICP; break; }
+            const uint64_t count = (uint64_t)cs, dw = (tag >> 32) & 0xFFFFu, pw = tag >> 48;
+            if (count * (dw + pw) > wc) { st = ST_ICP; break; }
+            const uint64_t eo = tag_pos + 8;
+            if (!in_bounds(lseg, eo, wc * 8)) { st = ST_OOB; break; }
+            if (!consume(wc)) { st = ST_TRAV; break; }
+            if (pw && count) push(lseg, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest);
+            continue;
+        }
+        uint64_t co;
+        if (has_ov) {
+            co = lov;
+        } else {
+            const int64_t c = (int64_t)ppos + 8 + ptr_offset_words(lword) * 8;
+            if (c < 0) { st = ST_OOB; break; }
+            co = (uint64_t)c;
+        }
+        const uint64_t bytes = es == 0 ? 0 : es == 1 ? (wc + 7) / 8 : es == 2 ? wc : es == 3 ? 2 * wc
+                             : es == 4 ? 4 * wc : 8 * wc;  // listContentBytes (:65-79)
+        seg_at(lseg);
+        if (co > clen || bytes > clen - co) { st = ST_OOB; break; }
+        if (!consume((bytes + 7) / 8)) { st = ST_TRAV; break; }  // listContentWords (:81-86)
+        if (es == 6 && wc) push(lseg, co, 1, 1, (uint32_t)(wc - 1), 0, nest);
+    }
+    status[msg] = st;
+    if (words) words[msg] = st == ST_OK ? trav_limit - rem : 0ull;
+}
+
+// ---------------------------------------------------------------------------
 // Reader.readPackedMessage, batched (reader.zig:84-156)
 // ---------------------------------------------------------------------------
 // Unit i is one reader's buffered packed stream; one message is decoded from its
@@ -2532,6 +2771,15 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                                                        out_len, out_cap, status);
     decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
                                                                         out_cap, out_len, status, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                           uint64_t seg_limit, uint64_t trav_limit, uint32_t nest_limit, int32_t* status,
+                           uint64_t* words, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    validate_kernel<<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(in, in_off, in_len, n, seg_limit, trav_limit,
+                                                                  nest_limit, status, words);
     return hipGetLastError();
 }
 

@@ -58,7 +58,17 @@ enum capnp_packed_status {
     CAPNP_PACKED_MESSAGE_TOO_LARGE = 11,        /* more than 8 Mi words (reader.zig:140) */
     CAPNP_PACKED_INVALID_PACKED_MESSAGE = 12,   /* the last record overshoots the framed length (reader.zig:151-153) */
     /* Message.init (message.zig:341-394) only: */
-    CAPNP_PACKED_TRUNCATED_MESSAGE = 13         /* header or a segment runs past the data (message.zig:353/380) */
+    CAPNP_PACKED_TRUNCATED_MESSAGE = 13,        /* header or a segment runs past the data (message.zig:353/380) */
+    /* Message.validate (message.zig:699-969) only: */
+    CAPNP_PACKED_EMPTY_MESSAGE = 14,            /* no segments (:700) */
+    CAPNP_PACKED_NESTING_LIMIT_EXCEEDED = 15,   /* a non-null pointer below the nesting limit (:724) */
+    CAPNP_PACKED_INVALID_SEGMENT_ID = 16,       /* a far pointer names a missing segment (:421/:428/:749) */
+    CAPNP_PACKED_INVALID_POINTER = 17,          /* pointer type 3 (capability) where data is validated (:731) */
+    CAPNP_PACKED_OUT_OF_BOUNDS = 18,            /* an object runs past its segment (bounds.zig:10-13) */
+    CAPNP_PACKED_TRAVERSAL_LIMIT_EXCEEDED = 19, /* more words than traversal_limit_words (:711) */
+    CAPNP_PACKED_INVALID_FAR_POINTER = 20,      /* malformed double-far landing pad (:746-757) */
+    CAPNP_PACKED_INVALID_INLINE_COMPOSITE_POINTER = 21, /* bad inline-composite tag (:608-621, :822-832) */
+    CAPNP_PACKED_LIST_TOO_LARGE = 22            /* list size overflows (:944) */
 };
 
 /* Version / capability query (precedent: src/wasm/capnp_host_abi.zig:60-70). */
@@ -211,6 +221,19 @@ int capnp_packed_encode_message_batch(const uint64_t* d_seg_ptr, const uint64_t*
 int capnp_packed_message_init_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                     uint32_t n, uint32_t max_segs, uint32_t* d_seg_count, uint64_t* d_seg_off,
                                     uint64_t* d_seg_len, int32_t* d_status, void* stream);
+
+/* Message.validate (message.zig:699-969, ValidationOptions :331-335) of n framed
+ * messages d_in[d_in_off[i] .. + d_in_len[i]): Message.init's segment-table parse
+ * (its errors: END_OF_STREAM, INVALID_SEGMENT_COUNT, SEGMENT_COUNT_LIMIT_EXCEEDED,
+ * TRUNCATED_MESSAGE), then the depth-first pointer traversal with the reference's
+ * limits and error order. d_status[i] = the first error the reference's recursion
+ * would raise, or OK; d_words[i] (may be NULL) = traversal words consumed (OK only).
+ * The reference defaults are segment_count_limit 512, traversal_limit_words 8 Mi,
+ * nesting_limit 64; nesting limits above 64 and messages of 4 GiB or more give
+ * INVALID_ARGUMENT. */
+int capnp_packed_validate_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
+                                uint32_t n, uint64_t segment_count_limit, uint64_t traversal_limit_words,
+                                uint32_t nesting_limit, int32_t* d_status, uint64_t* d_words, void* stream);
 
 /* Exclusive scan of n lengths into n+1 offsets (d_off[0] = base, d_off[n] =
  * base + total), on device.

@@ -230,6 +230,241 @@ int oracle_message_init(const uint8_t* data, size_t n, uint32_t max_segs,
     return 0;
 }
 
+/* ------------------------------------------------------------------------
+ * message.zig:699-969 Message.validate (and the helpers it calls, :11-18
+ * decodeOffsetWords, :65-86 listContentBytes/Words, :279-285 decodeFarPointer,
+ * :420-444 readWord/resolveFarLandingPad, :586-697 resolveInlineCompositeList,
+ * message/bounds.zig:10-13 checkBounds), recursive as in the reference.
+ * ------------------------------------------------------------------------ */
+enum {
+    V_OK = 0, V_EOS = 8, V_SEGCOUNT = 9, V_SEGLIMIT = 10, V_TRUNC = 13, V_EMPTY = 14, V_NEST = 15, V_SEGID = 16,
+    V_PTR = 17, V_OOB = 18, V_TRAV = 19, V_FAR = 20, V_ICP = 21, V_LIST = 22
+};
+
+typedef struct {
+    const uint8_t* data;
+    uint32_t nseg;
+    const uint64_t* off; /* segment byte offsets in data */
+    const uint64_t* len; /* segment byte lengths */
+    uint64_t remaining;
+} vmsg_t;
+
+static int64_t v_offset_words(uint64_t w) { /* :11-18 */
+    uint32_t raw = (uint32_t)((w >> 2) & 0x3FFFFFFFu);
+    return (raw & 0x20000000u) ? (int64_t)raw - ((int64_t)1 << 30) : (int64_t)raw;
+}
+static uint64_t v_word(const vmsg_t* m, uint32_t seg, uint64_t pos) { return load_le64(m->data + m->off[seg] + pos); }
+static int v_bounds(const vmsg_t* m, uint32_t seg, uint64_t off, uint64_t size) { /* bounds.zig:10-13 */
+    uint64_t end = off + size;
+    if (end < off) return V_OOB;
+    return end > m->len[seg] ? V_OOB : V_OK;
+}
+static int v_read(const vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t* w) { /* :420-425 readWord */
+    if (seg >= m->nseg) return V_SEGID;
+    int e = v_bounds(m, seg, pos, 8);
+    if (e) return e;
+    *w = v_word(m, seg, pos);
+    return V_OK;
+}
+static int v_consume(vmsg_t* m, uint64_t words) { /* :710-713 */
+    if (words > m->remaining) return V_TRAV;
+    m->remaining -= words;
+    return V_OK;
+}
+
+static int v_pointer(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint64_t nesting);
+
+/* pointers of `count` elements of (dw + pw) words at elements_offset (:846-859, :956-967) */
+static int v_elements(vmsg_t* m, uint32_t seg, uint64_t elements_offset, uint64_t count, uint64_t dw, uint64_t pw,
+                      uint64_t nesting) {
+    if (pw == 0 || count == 0) return V_OK;
+    uint64_t stride = (dw + pw) * 8;
+    for (uint64_t e = 0; e < count; ++e) {
+        uint64_t ps = elements_offset + e * stride + dw * 8;
+        for (uint64_t p = 0; p < pw; ++p) {
+            uint64_t pp = ps + p * 8;
+            int r = v_pointer(m, seg, pp, v_word(m, seg, pp), nesting);
+            if (r) return r;
+        }
+    }
+    return V_OK;
+}
+
+/* :940-969 validateInlineCompositeTag */
+static int v_ic_tag(vmsg_t* m, uint32_t seg, uint64_t elements_offset, uint64_t tag, uint64_t nesting) {
+    int64_t cs = v_offset_words(tag);
+    if (cs < 0) return V_ICP;
+    uint64_t count = (uint64_t)cs, dw = (tag >> 32) & 0xFFFF, pw = tag >> 48;
+    uint64_t total_words = count * (dw + pw);
+    if (total_words > UINT64_MAX / 8) return V_LIST; /* > maxInt(usize) / 8 (unreachable: < 2^46) */
+    uint64_t total_bytes = total_words * 8;
+    if (elements_offset > m->len[seg]) return V_OOB;
+    if (total_bytes > m->len[seg] - elements_offset) return V_OOB;
+    int r = v_consume(m, total_words);
+    if (r) return r;
+    return v_elements(m, seg, elements_offset, count, dw, pw, nesting);
+}
+
+/* :761-799 validateStructPointer */
+static int v_struct(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, int has_ov, uint64_t ov, uint64_t nesting) {
+    uint64_t ds = (word >> 32) & 0xFFFF, pc = word >> 48, so;
+    if (has_ov) {
+        so = ov;
+    } else {
+        int64_t s = (int64_t)pos + 8 + v_offset_words(word) * 8;
+        if (s < 0) return V_OOB;
+        so = (uint64_t)s;
+    }
+    uint64_t total_words = ds + pc, total_bytes = total_words * 8;
+    if (so > m->len[seg]) return V_OOB;
+    if (total_bytes > m->len[seg] - so) return V_OOB;
+    int r = v_consume(m, total_words);
+    if (r) return r;
+    for (uint64_t i = 0; i < pc; ++i) {
+        uint64_t pp = so + ds * 8 + i * 8;
+        r = v_pointer(m, seg, pp, v_word(m, seg, pp), nesting);
+        if (r) return r;
+    }
+    return V_OK;
+}
+
+static int v_list_bytes(uint64_t es, uint64_t count, uint64_t* bytes) { /* :65-79 */
+    switch (es) {
+        case 0: *bytes = 0; return V_OK;
+        case 1: *bytes = (count + 7) / 8; return V_OK;
+        case 2: *bytes = count; return V_OK;
+        case 3: *bytes = count * 2; return V_OK;
+        case 4: *bytes = count * 4; return V_OK;
+        case 5: case 6: *bytes = count * 8; return V_OK;
+        default: return V_PTR;
+    }
+}
+
+/* :586-627 resolveInlineCompositeList, list-pointer case (the only one validate reaches) */
+static int v_ic_list(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint64_t nesting) {
+    int64_t t = (int64_t)pos + 8 + v_offset_words(word) * 8;
+    if (t < 0) return V_OOB;
+    uint64_t tag_pos = (uint64_t)t, word_count = word >> 35, tag = 0;
+    int r = v_read(m, seg, tag_pos, &tag);
+    if (r) return r;
+    if ((tag & 3) != 0) return V_ICP;
+    int64_t cs = v_offset_words(tag);
+    if (cs < 0) return V_ICP;
+    uint64_t count = (uint64_t)cs, dw = (tag >> 32) & 0xFFFF, pw = tag >> 48;
+    if (count * (dw + pw) > word_count) return V_ICP;
+    uint64_t elements_offset = tag_pos + 8;
+    r = v_bounds(m, seg, elements_offset, word_count * 8);
+    if (r) return r;
+    r = v_consume(m, word_count); /* :910-912 */
+    if (r) return r;
+    return v_elements(m, seg, elements_offset, count, dw, pw, nesting);
+}
+
+/* :801-893 validateListPointer */
+static int v_list(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, int has_ov, uint64_t ov, uint64_t nesting) {
+    uint64_t es = (word >> 32) & 7;
+    if (es == 7 && !has_ov) return v_ic_list(m, seg, pos, word, nesting);
+    if (es == 7) { /* layout B double-far inline composite (:815-857) */
+        uint64_t word_count = word >> 35, tag_pos = ov, tag = 0;
+        int r = v_read(m, seg, tag_pos, &tag);
+        if (r) return r;
+        if ((tag & 3) != 0) return V_ICP;
+        int64_t cs = v_offset_words(tag);
+        if (cs < 0) return V_ICP;
+        uint64_t count = (uint64_t)cs, dw = (tag >> 32) & 0xFFFF, pw = tag >> 48;
+        if (count * (dw + pw) > word_count) return V_ICP;
+        uint64_t elements_offset = tag_pos + 8, total_bytes = word_count * 8;
+        if (elements_offset > m->len[seg]) return V_OOB;
+        if (total_bytes > m->len[seg] - elements_offset) return V_OOB;
+        r = v_consume(m, word_count);
+        if (r) return r;
+        return v_elements(m, seg, elements_offset, count, dw, pw, nesting);
+    }
+    uint64_t count = word >> 35, co, bytes = 0;
+    if (has_ov) {
+        co = ov;
+    } else {
+        int64_t c = (int64_t)pos + 8 + v_offset_words(word) * 8;
+        if (c < 0) return V_OOB;
+        co = (uint64_t)c;
+    }
+    int r = v_list_bytes(es, count, &bytes);
+    if (r) return r;
+    if (co > m->len[seg]) return V_OOB;
+    if (bytes > m->len[seg] - co) return V_OOB;
+    r = v_consume(m, bytes ? (bytes + 7) / 8 : 0); /* listContentWords :81-86 */
+    if (r) return r;
+    if (es != 6 || count == 0) return V_OK;
+    for (uint64_t i = 0; i < count; ++i) {
+        uint64_t pp = co + 8 * i;
+        r = v_pointer(m, seg, pp, v_word(m, seg, pp), nesting);
+        if (r) return r;
+    }
+    return V_OK;
+}
+
+/* :734-759 validateFarPointer (with :427-435 resolveFarLandingPad) */
+static int v_far(vmsg_t* m, uint64_t word, uint64_t nesting) {
+    int dbl = (word >> 2) & 1;
+    uint64_t pad_off = (word >> 3) & 0x1FFFFFFF;
+    uint32_t fseg = (uint32_t)(word >> 32);
+    if (fseg >= m->nseg) return V_SEGID;
+    uint64_t landing = pad_off * 8;
+    int r = v_bounds(m, fseg, landing, dbl ? 16 : 8);
+    if (r) return r;
+    uint64_t lw = 0, tw = 0;
+    if (!dbl) {
+        r = v_read(m, fseg, landing, &lw);
+        if (r) return r;
+        return v_pointer(m, fseg, landing, lw, nesting);
+    }
+    r = v_read(m, fseg, landing, &lw);
+    if (r) return r;
+    r = v_read(m, fseg, landing + 8, &tw);
+    if (r) return r;
+    if ((lw & 3) != 2) return V_FAR;
+    if ((lw >> 2) & 1) return V_FAR;
+    uint32_t lseg = (uint32_t)(lw >> 32);
+    if (lseg >= m->nseg) return V_SEGID;
+    uint64_t eo = ((lw >> 3) & 0x1FFFFFFF) * 8;
+    if ((tw & 3) == 0) return v_ic_tag(m, lseg, eo, tw, nesting);
+    if ((tw & 3) == 1) return v_list(m, lseg, 0, tw, 1, eo, nesting);
+    return V_FAR;
+}
+
+/* :715-732 validatePointer */
+static int v_pointer(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint64_t nesting) {
+    if (word == 0) return V_OK;
+    if (nesting == 0) return V_NEST;
+    if (seg >= m->nseg) return V_SEGID;
+    switch (word & 3) {
+        case 0: return v_struct(m, seg, pos, word, 0, 0, nesting - 1);
+        case 1: return v_list(m, seg, pos, word, 0, 0, nesting - 1);
+        case 2: return v_far(m, word, nesting - 1);
+        default: return V_PTR;
+    }
+}
+
+int oracle_validate(const uint8_t* data, size_t n, uint64_t segment_count_limit, uint64_t traversal_limit_words,
+                    uint64_t nesting_limit, uint64_t* words) {
+    uint64_t off[512], len[512];
+    uint32_t nseg = 0;
+    *words = 0;
+    int r = oracle_message_init(data, n, 512, off, len, &nseg);
+    if (r == -1) return V_EOS;
+    if (r == -2) return V_SEGCOUNT;
+    if (r == -3) return V_SEGLIMIT;
+    if (r) return V_TRUNC;
+    /* :699-708 validate */
+    if (nseg == 0) return V_EMPTY;
+    if (nseg > segment_count_limit) return V_SEGLIMIT;
+    if (len[0] < 8) return V_TRUNC;
+    vmsg_t m = {data, nseg, off, len, traversal_limit_words};
+    r = v_pointer(&m, 0, 0, v_word(&m, 0, 0), nesting_limit);
+    if (r == V_OK) *words = traversal_limit_words - m.remaining;
+    return r;
+}
+
 /* reader.zig:84-156 Reader.readPackedMessage */
 int oracle_read_packed_message(const uint8_t* in, size_t n, uint8_t* out, size_t cap,
                                size_t* out_len, size_t* consumed) {

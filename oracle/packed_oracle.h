@@ -52,6 +52,17 @@ int oracle_message_init(const uint8_t* data, size_t n, uint32_t max_segs,
 int oracle_read_packed_message(const uint8_t* in, size_t n, uint8_t* out, size_t cap,
                                size_t* out_len, size_t* consumed);
 
+/* message.zig:699-969 Message.validate over a framed message (Message.init first,
+ * message.zig:341-394). Returns a capnp_packed_status code (include/capnp_packed.h):
+ * 0 OK; Message.init: 8 EndOfStream, 9 InvalidSegmentCount, 10
+ * SegmentCountLimitExceeded, 13 TruncatedMessage; validate: 14 EmptyMessage, 10
+ * SegmentCountLimitExceeded, 13 TruncatedMessage, 15 NestingLimitExceeded, 16
+ * InvalidSegmentId, 17 InvalidPointer, 18 OutOfBounds, 19 TraversalLimitExceeded, 20
+ * InvalidFarPointer, 21 InvalidInlineCompositePointer, 22 ListTooLarge. *words =
+ * traversal words consumed (valid when OK). */
+int oracle_validate(const uint8_t* data, size_t n, uint64_t segment_count_limit, uint64_t traversal_limit_words,
+                    uint64_t nesting_limit, uint64_t* words);
+
 /* Batch drivers over independent units (same layout as the device batch ABI);
  * OpenMP over units with `threads` threads (<= 0: all). */
 void oracle_pack_batch(const uint8_t* in, const uint64_t* in_off, uint32_t n,

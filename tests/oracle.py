@@ -44,6 +44,8 @@ def lib():
         L.oracle_mix64.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         L.oracle_mix64.restype = ctypes.c_uint64
         L.oracle_word_has_zero_byte.argtypes = [ctypes.c_uint64]
+        L.oracle_validate.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_uint64, _u64p]
         _lib = L
     return _lib
 
@@ -99,6 +101,16 @@ def read_packed_message(p: bytes, cap=1 << 20):
     used = ctypes.c_size_t()
     rc = lib().oracle_read_packed_message(src, len(p), dst, cap, ctypes.byref(n), ctypes.byref(used))
     return rc, dst.raw[:n.value], used.value
+
+
+def validate(data: bytes, segment_count_limit=512, traversal_limit_words=8 * 1024 * 1024, nesting_limit=64):
+    """(status, traversal words consumed) — message.zig:699-969 Message.validate of a
+    framed message (Message.init first); status codes are include/capnp_packed.h's."""
+    src = _buf(data)
+    words = ctypes.c_uint64()
+    st = lib().oracle_validate(src, len(data), segment_count_limit, traversal_limit_words, nesting_limit,
+                               ctypes.byref(words))
+    return st, words.value
 
 
 def _ptr(a: np.ndarray):
