@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory leg")
     ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
     ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
+    ap.add_argument("--no-validate", action="store_true", help="skip the Message.validate leg")
+    ap.add_argument("--only-validate", action="store_true", help=argparse.SUPPRESS)  # dev: validate leg only
     return ap.parse_args()
 
 
@@ -593,6 +595,90 @@ def read_message_leg(args, dev, reps=10):
             "note": "GiB/s of framed (unpacked) bytes; header pass + framed-length walk + indexed decode"}
 
 
+def validate_leg(args, dev, reps=10, n=1 << 20, distinct=4096, cpu_s=3.0):
+    """SURVEY §8(f) row 4, Message.validate (message.zig:699-969) batched, with the
+    default ValidationOptions (:331-335), on two device-resident corpora:
+      trees: 1M framed messages, `distinct` random valid trees (tests/msggen.py: 1-4
+             segments, structs, lists of every element size, pointer lists, inline-
+             composite lists, single and double far pointers, depth <= 6) repeated;
+      c1:    256K copies of the reference bench's own 20,536-B message.
+    Algorithmic bytes = the words the walk reads (pointer slots, landing pads, tags:
+    msggen's per-tree count) x 8 + the segment table + 24 B of per-message metadata.
+    CPU side: the oracle's recursive restatement, one thread, on the distinct trees."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import numpy as np
+    import msggen
+    import pyref
+    stream = torch.cuda.current_stream()
+    rng = np.random.default_rng(0xC0DE0008)
+    trees = [msggen.RandomTree(rng) for _ in range(distinct)]
+    msgs = [t.framed() for t in trees]
+    lens = np.array([len(m) for m in msgs], dtype=np.int64)
+    alg_one = np.array([8 * t.reads + msggen.header_bytes(m) + 24 for t, m in zip(trees, msgs)], dtype=np.int64)
+    base = torch.from_numpy(np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()).to(dev)
+    reps_n = n // distinct
+    d_in = base.repeat(reps_n)
+    off1 = np.zeros(distinct, dtype=np.int64)
+    off1[1:] = np.cumsum(lens)[:-1]
+    offs = (torch.from_numpy(off1).to(dev)[None, :] + (torch.arange(reps_n, device=dev) * int(lens.sum()))[:, None])
+    in_off = offs.reshape(-1).contiguous()
+    in_len = torch.from_numpy(lens).to(dev).repeat(reps_n)
+    st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    words = torch.zeros(n, dtype=torch.int64, device=dev)
+
+    def timed(fn):
+        fn()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        for _ in range(reps):
+            fn()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) / reps
+
+    ms = timed(lambda: cp.validate_batch(d_in, in_off, in_len, st, words, stream=stream))
+    w2 = words.view(reps_n, distinct)
+    ok = bool((st == 0).all().item() and (w2 == w2[0:1]).all().item())
+    alg = int(alg_one.sum()) * reps_n
+    reads = sum(t.reads for t in trees) * reps_n
+    out = {"trees": {"messages": n, "distinct": distinct, "framed_bytes": int(lens.sum()) * reps_n,
+                     "pointer_words_read": reads, "ms": round(ms, 4),
+                     "messages_per_s": round(n / (ms * 1e-3)), "words_read_per_s": round(reads / (ms * 1e-3)),
+                     "alg_GB_s": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "all_valid": ok}}
+    del d_in, in_off, in_len, st, words, offs
+    torch.cuda.empty_cache()
+    # the reference bench's message (one segment: root struct -> text + u64 list)
+    c1 = pyref.frame(pyref.bench_message_segments())
+    n1 = 1 << 18
+    d1 = torch.from_numpy(np.frombuffer(c1, dtype=np.uint8).copy()).to(dev).repeat(n1)
+    o1, l1 = cp.uniform_layout(n1, len(c1), device=dev)
+    s1 = torch.full((n1,), -1, dtype=torch.int32, device=dev)
+    wd1 = torch.zeros(n1, dtype=torch.int64, device=dev)
+    ms1 = timed(lambda: cp.validate_batch(d1, o1, l1, s1, wd1, stream=stream))
+    ok1 = bool((s1 == 0).all().item() and (wd1 == wd1[0]).all().item())
+    out["c1"] = {"messages": n1, "framed_bytes": len(c1), "ms": round(ms1, 4),
+                 "messages_per_s": round(n1 / (ms1 * 1e-3)),
+                 "validated_GiB_s": round(n1 * len(c1) / (ms1 * 1e-3) / 2 ** 30, 1),
+                 "traversal_words": int(wd1[0].item()), "all_valid": ok1}
+    del d1
+    torch.cuda.empty_cache()
+    # CPU: the oracle walk on the distinct trees, one thread
+    import oracle
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < cpu_s:
+        for m in msgs:
+            oracle.validate(m)
+        done += len(msgs)
+    el = time.perf_counter() - t0
+    out["cpu_oracle_1core_trees"] = {"messages_per_s": round(done / el), "sample": f"{done} tree validations",
+                                     "note": "includes a ctypes call per message (~1 us)"}
+    out["note"] = ("device: lane per message, LDS stack of pointer runs; alg bytes = walked words x 8 + "
+                   "segment table + 24 B metadata per message")
+    return out
+
+
 def load_traffic(config_key):
     """PMC HBM bytes per launch for this config (scripts/pmc_traffic.py output)."""
     path = os.environ.get("CPK_TRAFFIC_JSON") or os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -679,6 +765,9 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
+    if args.only_validate:
+        print(json.dumps({"validate": validate_leg(args, dev)}), flush=True)
+        return
     n, ub = args.units, args.unit_bytes
     wl = Workload(n, ub, args.seed, args.zero_thresh, unit_base=rank * n, dev=dev)
     head = measure(wl, args, args.steps, args.warmup, world, dev)
@@ -721,6 +810,9 @@ def main():
         if not args.no_read_message:
             torch.cuda.empty_cache()
             extra["rpc_framer"] = framer_leg(args, dev)
+        if not args.no_validate:
+            torch.cuda.empty_cache()
+            extra["validate"] = validate_leg(args, dev)
         if not args.no_c1:
             extra["c1_bench_message"] = c1_leg()
 

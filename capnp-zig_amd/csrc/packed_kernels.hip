@@ -2091,21 +2091,56 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 // ---------------------------------------------------------------------------
 // Message.validate, batched (message.zig:699-969)
 // ---------------------------------------------------------------------------
-// Lane per framed message: Message.init's segment-table parse (message.zig:341-394),
-// then the reference's recursive depth-first traversal (validatePointer and the
-// struct / list / far / inline-composite validators) as a loop over an explicit
-// stack of pointer runs in LDS. A frame is one run of pointer words still to visit:
-// the current element's remaining pointers (pleft of pw, from byte `cur` of segment
-// `seg`) and the elements after it (eleft, each dw data words then pw pointers), at
-// the nesting value the reference passes to validatePointer for them. Pushing a
-// frame always spends a nesting level, so the stack never holds more than the
-// nesting limit (<= kVdDepth) frames. Visiting order, limit consumption and every
-// check follow the reference line by line, so the first error is the one it raises.
+// Lane per framed message. Each lane runs Message.init's segment-table parse
+// (message.zig:341-394) and then the reference's recursive depth-first walk
+// (validatePointer and the struct / list / far / inline-composite validators) as a
+// state machine over an explicit stack of pointer runs:
+// - The walk is a chain of dependent reads, and lanes of a wave sit in different
+//   states. So every turn of the wave's loop issues at most ONE read per lane (the
+//   4/8/16 bytes its walk needs next) and then advances each lane through all the work
+//   that needs no memory. No turn serialises several round trips for the wave.
+// - A persistent grid: each wave owns a contiguous range of messages and its lanes take
+//   the next one as they finish (a wave-uniform cursor, no atomics), so a long message
+//   does not idle the other 63 lanes.
+// - A frame is one run of pointer words still to visit: the current element's remaining
+//   pointers (pleft of pw, from byte `cur` of segment `seg`) and the elements after it
+//   (eleft, each dw data words then pw pointers), at the nesting value the reference
+//   passes to validatePointer for them. Pushing a frame spends a nesting level, so a lane
+//   never holds more than nesting_limit (<= kVdDepth) frames. The first kVdLds live in
+//   LDS, deeper ones in the lane's private scratch.
+// - Segment offsets: the first kVdSegs segments' byte offsets are kept in LDS from the
+//   header parse; one more (the last sought) in registers; any other is sought again by
+//   reading the segment table.
+// Visiting order, limit consumption and every check follow the reference line by line,
+// so a message's status is the first error the reference raises.
 constexpr uint32_t kVdDepth = 64;  // supported nesting limit (the reference default)
+#ifndef CPK_VD_LDS
+#define CPK_VD_LDS 8
+#endif
+constexpr uint32_t kVdLds = CPK_VD_LDS;  // stack frames per lane held in LDS
+constexpr uint32_t kVdSegs = 4;          // segments per lane whose offsets are held in LDS
+
+enum : uint32_t {
+    VK_IDLE,     // no message: take the next one
+    VK_EXIT,     // the wave's range is done
+    VK_META,     // read in_off / in_len
+    VK_COUNT,    // read the segment count (and segment 0's size)
+    VK_SIZES,    // read segment sizes (Message.init's truncation check)
+    VK_PTR,      // read a pointer word: validatePointer (also a single far's landing pad)
+    VK_LAND2,    // read a double far's 16-B landing pad
+    VK_TAG,      // read an inline-composite tag word
+    VK_SEEK,     // read segment sizes to find a segment's offset
+    VK_REQ_PTR,  // (no read) issue the read of the next pointer word
+};
 
 __device__ __forceinline__ uint64_t ld_u64(const uint8_t* p) {  // unaligned-safe 8-B load
     uint64_t v;
     __builtin_memcpy(&v, p, 8);
+    return v;
+}
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
     return v;
 }
 __device__ __forceinline__ int64_t ptr_offset_words(uint64_t w) {  // message.zig:11-18
@@ -2116,205 +2151,341 @@ __device__ __forceinline__ int64_t ptr_offset_words(uint64_t w) {  // message.zi
 __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restrict__ in,
                                                          const uint64_t* __restrict__ in_off,
                                                          const uint64_t* __restrict__ in_len, uint32_t n,
-                                                         uint64_t seg_limit, uint64_t trav_limit, uint32_t nest_limit,
-                                                         int32_t* __restrict__ status, uint64_t* __restrict__ words) {
-    __shared__ uint4 stack_all[kVdDepth * kWave];  // frame f of lane l at [f * 64 + l]
+                                                         uint32_t per_wave, uint64_t seg_limit, uint64_t trav_limit,
+                                                         uint32_t nest_limit, int32_t* __restrict__ status,
+                                                         uint64_t* __restrict__ words) {
+    __shared__ uint4 stack_all[kVdLds * kWave];         // frame f < kVdLds of lane l at [f * 64 + l]
+    __shared__ uint32_t segp_all[(kVdSegs + 1) * kWave];  // segment i's start (i <= kVdSegs) at [i * 64 + l]
+    uint4 deep[kVdDepth - kVdLds];                       // frames kVdLds.. (private scratch)
     const uint32_t lane = lane_id();
-    const uint32_t msg = blockIdx.x * kWave + lane;
-    if (msg >= n) return;
-    const uint8_t* const d = in + in_off[msg];
-    const uint64_t len = in_len[msg];
-    auto u32at = [&](uint64_t o) { return (uint32_t)d[o] | ((uint32_t)d[o + 1] << 8) | ((uint32_t)d[o + 2] << 16) |
-                                          ((uint32_t)d[o + 3] << 24); };
-    int32_t st = ST_OK;
-    uint64_t rem = trav_limit;
-    // ---- Message.init (message.zig:341-394) --------------------------------------------
-    uint32_t nseg = 0;
-    uint64_t header = 0;
-    if (len >= 0x100000000ull) st = ST_ARG;  // byte offsets in the frames are u32
-    else if (len < 4) st = ST_EOS;
-    else {
-        const uint32_t m1 = u32at(0);
-        if (m1 == 0xFFFFFFFFu) st = ST_SEGCOUNT;
-        else if ((uint64_t)m1 + 1 > kMsgMaxSegs) st = ST_SEGLIMIT;
-        else {
-            nseg = m1 + 1;
-            header = 4ull * (1 + nseg + ((nseg & 1) ? 0 : 1));
-            if (header > len) st = ST_TRUNC;
-            uint64_t o = header;
-            for (uint32_t i = 0; st == ST_OK && i < nseg; ++i) {
-                o += 8ull * u32at(4 + 4 * i);
-                if (o > len) st = ST_TRUNC;
-            }
-        }
-    }
-    // ---- validate (:699-708) ---------------------------------------------------------
-    uint32_t cseg = 0;  // cached segment: byte offset in the message and length
-    uint64_t coff = header, clen = 0;
-    if (st == ST_OK) {
-        clen = 8ull * u32at(4);
-        if (nseg > seg_limit) st = ST_SEGLIMIT;
-        else if (clen < 8) st = ST_TRUNC;
-    }
-    auto seg_at = [&](uint32_t id) {  // caller guarantees id < nseg
-        if (id != cseg) {
-            uint64_t o = header;
-            for (uint32_t i = 0; i < id; ++i) o += 8ull * u32at(4 + 4 * i);
-            cseg = id;
-            coff = o;
-            clen = 8ull * u32at(4 + 4 * id);
-        }
-    };
-    auto word_at = [&](uint32_t seg, uint64_t pos) { seg_at(seg); return ld_u64(d + coff + pos); };
-    auto in_bounds = [&](uint32_t seg, uint64_t off, uint64_t size) {  // bounds.zig:10-13
-        seg_at(seg);
-        return off + size >= off && off + size <= clen;
-    };
     uint4* const stk = stack_all + lane;
-    uint32_t depth = 0;
+    uint32_t* const segp = segp_all + lane;
+    const uint64_t first = (uint64_t)blockIdx.x * per_wave;
+    const uint64_t last = first + per_wave < n ? first + per_wave : n;
+    uint64_t cursor = first;  // wave-uniform
+
+    uint32_t kind = VK_IDLE;
+    uint64_t msg = 0;
+    const uint8_t* d = in;
+    const uint8_t* laddr = in;  // the pending read
+    uint32_t lsz = 0;
+    uint64_t len = 0, rem = 0;
+    uint32_t nseg = 0, si = 0, depth = 0;
+    uint64_t acc = 0;
+    uint32_t xseg = 0xFFFFFFFFu;  // the sought segment cached in registers
+    uint64_t xoff = 0, xlen = 0;
+    uint32_t sk_target = 0, sk_i = 0, sk_ret = 0;
+    uint64_t sk_acc = 0, sva = 0, svb = 0;
+    uint32_t pseg = 0, pnest = 0;  // the pending pointer, or the pending tag's nesting
+    uint64_t ppos = 0;
+    uint32_t tseg = 0;  // the pending inline-composite tag: segment, position, list word count
+    uint64_t tpos = 0, twc = 0;
+
+    auto frame_store = [&](uint32_t i, uint4 f) {
+        if (i < kVdLds) stk[kWave * i] = f;
+        else deep[i - kVdLds] = f;
+    };
+    auto frame_load = [&](uint32_t i) { return i < kVdLds ? stk[kWave * i] : deep[i - kVdLds]; };
     auto push = [&](uint32_t seg, uint64_t cur, uint32_t pleft, uint32_t pw, uint32_t eleft, uint32_t dw,
                     uint32_t nest) {
-        stk[kWave * depth] = make_uint4((uint32_t)cur, eleft, pleft | (pw << 16), dw | (seg << 16) | (nest << 26));
+        frame_store(depth, make_uint4((uint32_t)cur, eleft, pleft | (pw << 16), dw | (seg << 16) | (nest << 26)));
         ++depth;
+    };
+    auto finish = [&](int32_t st) {
+        status[msg] = st;
+        if (words) words[msg] = st == ST_OK ? trav_limit - rem : 0ull;
+        kind = VK_IDLE;
     };
     auto consume = [&](uint64_t w) {  // :710-713
         if (w > rem) return false;
         rem -= w;
         return true;
     };
-    // the pending pointer (validatePointer's arguments); the root first
-    bool pend = st == ST_OK;
-    uint32_t pseg = 0, pnest = nest_limit;
-    uint64_t ppos = 0, pword = pend ? word_at(0, 0) : 0;
-    while (st == ST_OK) {
-        if (!pend) {  // next pointer of the top run, or pop it
-            if (depth == 0) break;
-            uint4 f = stk[kWave * (depth - 1)];
-            const uint32_t pleft = f.z & 0xFFFFu, pw = f.z >> 16, dw = f.w & 0xFFFFu;
-            const uint32_t seg = (f.w >> 16) & 0x3FFu, nest = f.w >> 26;
-            if (pleft) {
-                pseg = seg;
+    auto seg_lookup = [&](uint32_t s, uint64_t& off, uint64_t& slen) {  // s < nseg
+        const uint32_t lim = nseg < kVdSegs ? nseg : kVdSegs;
+        if (s < lim) {
+            off = segp[kWave * s];
+            slen = segp[kWave * (s + 1)] - off;
+            return true;
+        }
+        if (s == xseg) {
+            off = xoff;
+            slen = xlen;
+            return true;
+        }
+        return false;
+    };
+    auto request = [&](uint32_t k, const uint8_t* a, uint32_t size) {
+        kind = k;
+        laddr = a;
+        lsz = size;
+    };
+    auto seek_next = [&]() { request(VK_SEEK, d + 4 + 4ull * sk_i, sk_i < sk_target ? 8u : 4u); };
+    // find segment s (>= kVdSegs) in the segment table, then re-run state `ret` on (va, vb)
+    auto start_seek = [&](uint32_t s, uint32_t ret, uint64_t va, uint64_t vb) {
+        sk_target = s;
+        sk_i = kVdSegs;
+        sk_acc = segp[kWave * kVdSegs];
+        sk_ret = ret;
+        sva = va;
+        svb = vb;
+        seek_next();
+    };
+    auto load_ptr = [&]() {  // read the pointer word at (pseg, ppos)
+        uint64_t off, slen;
+        if (!seg_lookup(pseg, off, slen)) start_seek(pseg, VK_REQ_PTR, 0, 0);
+        else request(VK_PTR, d + off + ppos, 8);
+    };
+    auto next = [&]() {  // the next pointer of the walk, or the end of the message
+        while (depth) {
+            uint4 f = frame_load(depth - 1);
+            if (f.z & 0xFFFFu) {
+                pseg = (f.w >> 16) & 0x3FFu;
                 ppos = f.x;
-                pword = word_at(seg, f.x);
-                pnest = nest;
-                pend = true;
+                pnest = f.w >> 26;
                 f.x += 8;
                 f.z -= 1;
-            } else if (f.y) {
+                frame_store(depth - 1, f);
+                load_ptr();
+                return;
+            }
+            if (f.y) {
                 f.y -= 1;
-                f.x += 8 * dw;  // the next element's pointer section
-                f.z |= pw;
-            } else {
-                --depth;
+                f.x += 8 * (f.w & 0xFFFFu);  // the next element's pointer section
+                f.z |= f.z >> 16;
+                frame_store(depth - 1, f);
                 continue;
             }
-            stk[kWave * (depth - 1)] = f;
-            continue;
+            --depth;
         }
-        pend = false;
-        // ---- validatePointer (:715-732) ------------------------------------------------
-        if (pword == 0) continue;
-        if (pnest == 0) { st = ST_NEST; break; }
-        if (pseg >= nseg) { st = ST_SEGID; break; }
-        const uint32_t type = (uint32_t)pword & 3u;
-        if (type == 3) { st = ST_PTR; break; }
-        const uint32_t nest = pnest - 1;
-        // a list or inline-composite run to validate: (seg, content offset, pointer word,
-        // content given (double far), layout B tag position)
-        uint32_t lseg = pseg;
-        uint64_t lword = pword, lov = 0;
-        bool has_ov = false;
-        if (type == 2) {  // ---- validateFarPointer (:734-759) ------------------------------
-            const bool dbl = (pword >> 2) & 1u;
-            const uint64_t landing = ((pword >> 3) & 0x1FFFFFFFu) * 8;
-            const uint32_t fseg = (uint32_t)(pword >> 32);
-            if (fseg >= nseg) { st = ST_SEGID; break; }
-            if (!in_bounds(fseg, landing, dbl ? 16 : 8)) { st = ST_OOB; break; }
-            if (!dbl) {  // the landing word is the pointer: validatePointer at the same nesting
-                pseg = fseg;
-                ppos = landing;
-                pword = word_at(fseg, landing);
-                pnest = nest;
-                pend = true;
-                continue;
-            }
-            const uint64_t lw = word_at(fseg, landing), tw = word_at(fseg, landing + 8);
-            if ((lw & 3) != 2 || ((lw >> 2) & 1u)) { st = ST_FAR; break; }
-            const uint32_t s2 = (uint32_t)(lw >> 32);
-            if (s2 >= nseg) { st = ST_SEGID; break; }
-            const uint64_t eo = ((lw >> 3) & 0x1FFFFFFFu) * 8;
-            if ((tw & 3) == 0) {  // validateInlineCompositeTag (:940-969)
-                const int64_t cs = ptr_offset_words(tw);
-                if (cs < 0) { st = ST_ICP; break; }
-                const uint64_t count = (uint64_t)cs, dw = (tw >> 32) & 0xFFFFu, pw = tw >> 48;
-                const uint64_t tot = count * (dw + pw);
-                seg_at(s2);
-                if (eo > clen || tot * 8 > clen - eo) { st = ST_OOB; break; }
-                if (!consume(tot)) { st = ST_TRAV; break; }
-                if (pw && count) push(s2, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest);
-                continue;
-            }
-            if ((tw & 3) != 1) { st = ST_FAR; break; }
-            lseg = s2;  // validateListPointer(landing seg, 0, tag, elements offset)
-            lword = tw;
-            lov = eo;
-            has_ov = true;
+        finish(ST_OK);
+    };
+    auto sizes_next = [&]() {  // after segment si - 1: the next sizes, or validate's preamble (:699-708)
+        if (si < nseg) {
+            request(VK_SIZES, d + 4 + 4ull * si, si + 1 < nseg ? 8u : 4u);
+            return;
         }
-        if (type == 0) {  // ---- validateStructPointer (:761-799) -----------------------------
-            const uint64_t ds = (pword >> 32) & 0xFFFFu, pc = pword >> 48;
-            const int64_t so_s = (int64_t)ppos + 8 + ptr_offset_words(pword) * 8;
-            if (so_s < 0) { st = ST_OOB; break; }
-            const uint64_t so = (uint64_t)so_s;
-            seg_at(pseg);
-            if (so > clen || (ds + pc) * 8 > clen - so) { st = ST_OOB; break; }
-            if (!consume(ds + pc)) { st = ST_TRAV; break; }
-            if (pc) push(pseg, so + 8 * ds, (uint32_t)pc, (uint32_t)pc, 0, 0, nest);
-            continue;
-        }
-        // ---- validateListPointer (:801-893) ---------------------------------------------
-        const uint32_t es = (uint32_t)(lword >> 32) & 7u;
-        const uint64_t wc = lword >> 35;  // element count, or word count for inline composite
-        if (es == 7) {
-            // inline composite: the tag at the pointer's target (:586-627, validated by
-            // :895-923) or, behind a double far, at the landing pad's target (:815-857)
-            uint64_t tag_pos;
-            if (has_ov) {
-                tag_pos = lov;
-            } else {
-                const int64_t tp = (int64_t)ppos + 8 + ptr_offset_words(lword) * 8;
-                if (tp < 0) { st = ST_OOB; break; }
-                tag_pos = (uint64_t)tp;
-            }
-            if (!in_bounds(lseg, tag_pos, 8)) { st = ST_OOB; break; }
-            const uint64_t tag = word_at(lseg, tag_pos);
-            if ((tag & 3) != 0) { st = ST_ICP; break; }
-            const int64_t cs = ptr_offset_words(tag);
-            if (cs < 0) { st = ST_ICP; break; }
-            const uint64_t count = (uint64_t)cs, dw = (tag >> 32) & 0xFFFFu, pw = tag >> 48;
-            if (count * (dw + pw) > wc) { st = ST_ICP; break; }
-            const uint64_t eo = tag_pos + 8;
-            if (!in_bounds(lseg, eo, wc * 8)) { st = ST_OOB; break; }
-            if (!consume(wc)) { st = ST_TRAV; break; }
-            if (pw && count) push(lseg, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest);
-            continue;
-        }
-        uint64_t co;
-        if (has_ov) {
-            co = lov;
-        } else {
-            const int64_t c = (int64_t)ppos + 8 + ptr_offset_words(lword) * 8;
-            if (c < 0) { st = ST_OOB; break; }
-            co = (uint64_t)c;
-        }
+        if (nseg > seg_limit) return finish(ST_SEGLIMIT);
+        if (segp[kWave] - segp[0] < 8) return finish(ST_TRUNC);
+        pseg = 0;
+        ppos = 0;
+        pnest = nest_limit;
+        load_ptr();
+    };
+    auto add_size = [&](uint32_t words_) {  // Message.init :376-383
+        acc += 8ull * words_;
+        if (acc > len) return false;
+        ++si;
+        if (si <= kVdSegs) segp[kWave * si] = (uint32_t)acc;
+        return true;
+    };
+    // list content (non-composite) at co of segment s: listContentBytes / bounds / consume (:871-896)
+    auto plain_list = [&](uint32_t s, uint64_t co, uint64_t w, uint32_t nest) {
+        const uint32_t es = (uint32_t)(w >> 32) & 7u;
+        const uint64_t wc = w >> 35;
         const uint64_t bytes = es == 0 ? 0 : es == 1 ? (wc + 7) / 8 : es == 2 ? wc : es == 3 ? 2 * wc
                              : es == 4 ? 4 * wc : 8 * wc;  // listContentBytes (:65-79)
-        seg_at(lseg);
-        if (co > clen || bytes > clen - co) { st = ST_OOB; break; }
-        if (!consume((bytes + 7) / 8)) { st = ST_TRAV; break; }  // listContentWords (:81-86)
-        if (es == 6 && wc) push(lseg, co, 1, 1, (uint32_t)(wc - 1), 0, nest);
+        uint64_t off, slen;
+        seg_lookup(s, off, slen);
+        if (co > slen || bytes > slen - co) return finish(ST_OOB);
+        if (!consume((bytes + 7) / 8)) return finish(ST_TRAV);  // listContentWords (:81-86)
+        if (es == 6 && wc) push(s, co, 1, 1, (uint32_t)(wc - 1), 0, nest);
+        next();
+    };
+    // inline-composite elements from a tag (:940-968 with layout A, :846-868, :911-926)
+    auto composite = [&](uint32_t s, uint64_t eo, uint64_t tag, uint64_t total_words, uint32_t nest) {
+        const uint64_t count = (uint64_t)ptr_offset_words(tag), dw = (tag >> 32) & 0xFFFFu, pw = tag >> 48;
+        uint64_t off, slen;
+        seg_lookup(s, off, slen);
+        if (eo > slen || total_words * 8 > slen - eo) return finish(ST_OOB);
+        if (!consume(total_words)) return finish(ST_TRAV);
+        if (pw && count) push(s, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest);
+        next();
+    };
+
+    for (;;) {
+        // ---- take new messages ---------------------------------------------------------------
+        const uint64_t idle = __ballot(kind == VK_IDLE);
+        if (idle) {
+            if (cursor < last) {
+                if (kind == VK_IDLE) {
+                    const uint64_t id = cursor + __popcll(idle & ((1ull << lane) - 1));
+                    if (id < last) {
+                        msg = id;
+                        kind = VK_META;
+                    } else {
+                        kind = VK_EXIT;
+                    }
+                }
+                cursor += __popcll(idle);
+            } else if (kind == VK_IDLE) {
+                kind = VK_EXIT;
+            }
+        }
+        if (__ballot(kind != VK_EXIT) == 0) break;
+        // ---- the one read of this turn -----------------------------------------------------------
+        uint64_t va = 0, vb = 0;
+        if (kind == VK_META) {
+            va = in_off[msg];
+            vb = in_len[msg];
+        } else if (kind >= VK_COUNT && kind <= VK_SEEK) {
+            if (lsz == 4) va = ld_u32(laddr);
+            else va = ld_u64(laddr);
+            if (lsz == 16) vb = ld_u64(laddr + 8);
+        }
+        // ---- advance the lane to its next read --------------------------------------------------
+        for (bool go = true; go;) {
+            go = false;
+            switch (kind) {
+            case VK_META:
+                d = in + va;
+                len = vb;
+                rem = trav_limit;
+                depth = 0;
+                xseg = 0xFFFFFFFFu;
+                if (len >= 0x100000000ull) finish(ST_ARG);  // byte offsets in the frames are u32
+                else if (len < 4) finish(ST_EOS);
+                else request(VK_COUNT, d, len >= 8 ? 8u : 4u);
+                break;
+            case VK_COUNT: {  // Message.init :341-371
+                const uint32_t m1 = (uint32_t)va;
+                if (m1 == 0xFFFFFFFFu) { finish(ST_SEGCOUNT); break; }
+                if ((uint64_t)m1 + 1 > kMsgMaxSegs) { finish(ST_SEGLIMIT); break; }
+                nseg = m1 + 1;
+                acc = 4ull * (1 + nseg + ((nseg & 1) ? 0 : 1));
+                if (acc > len) { finish(ST_TRUNC); break; }
+                segp[0] = (uint32_t)acc;
+                si = 0;
+                if (lsz == 8 && !add_size((uint32_t)(va >> 32))) { finish(ST_TRUNC); break; }
+                sizes_next();
+                break;
+            }
+            case VK_SIZES:
+                if (!add_size((uint32_t)va) || (lsz == 8 && !add_size((uint32_t)(va >> 32)))) {
+                    finish(ST_TRUNC);
+                    break;
+                }
+                sizes_next();
+                break;
+            case VK_SEEK: {
+                bool found = false;
+                for (uint32_t h = 0; h < lsz / 4 && !found; ++h) {
+                    const uint32_t sz = (uint32_t)(va >> (32 * h));
+                    if (sk_i == sk_target) {
+                        xseg = sk_target;
+                        xoff = sk_acc;
+                        xlen = 8ull * sz;
+                        found = true;
+                    } else {
+                        sk_acc += 8ull * sz;
+                        ++sk_i;
+                    }
+                }
+                if (!found) {
+                    seek_next();
+                    break;
+                }
+                kind = sk_ret;  // re-run the state that needed the segment
+                va = sva;
+                vb = svb;
+                go = true;
+                break;
+            }
+            case VK_REQ_PTR:
+                load_ptr();
+                break;
+            case VK_PTR: {  // validatePointer (:715-734) on the word at (pseg, ppos)
+                const uint64_t w = va;
+                if (w == 0) { next(); break; }
+                if (pnest == 0) { finish(ST_NEST); break; }
+                if (pseg >= nseg) { finish(ST_SEGID); break; }
+                const uint32_t type = (uint32_t)w & 3u;
+                if (type == 3) { finish(ST_PTR); break; }
+                const uint32_t nest = pnest - 1;
+                if (type == 0) {  // validateStructPointer (:774-812)
+                    const uint64_t ds = (w >> 32) & 0xFFFFu, pc = w >> 48;
+                    const int64_t so_s = (int64_t)ppos + 8 + ptr_offset_words(w) * 8;
+                    uint64_t off, slen;
+                    seg_lookup(pseg, off, slen);
+                    if (so_s < 0 || (uint64_t)so_s > slen || (ds + pc) * 8 > slen - (uint64_t)so_s) {
+                        finish(ST_OOB);
+                        break;
+                    }
+                    if (!consume(ds + pc)) { finish(ST_TRAV); break; }
+                    if (pc) push(pseg, (uint64_t)so_s + 8 * ds, (uint32_t)pc, (uint32_t)pc, 0, 0, nest);
+                    next();
+                    break;
+                }
+                if (type == 1) {  // validateListPointer (:814-897)
+                    const int64_t c = (int64_t)ppos + 8 + ptr_offset_words(w) * 8;
+                    if (c < 0) { finish(ST_OOB); break; }
+                    if (((w >> 32) & 7u) != 7) { plain_list(pseg, (uint64_t)c, w, nest); break; }
+                    // inline composite: resolveInlineCompositeList (:563-609) reads the tag at c
+                    uint64_t off, slen;
+                    seg_lookup(pseg, off, slen);
+                    if ((uint64_t)c + 8 > slen) { finish(ST_OOB); break; }
+                    tseg = pseg;
+                    tpos = (uint64_t)c;
+                    twc = w >> 35;
+                    pnest = nest;
+                    request(VK_TAG, d + off + tpos, 8);
+                    break;
+                }
+                // validateFarPointer (:736-772) + resolveFarLandingPad (:430-437)
+                const bool dbl = (w >> 2) & 1u;
+                const uint64_t landing = ((w >> 3) & 0x1FFFFFFFu) * 8;
+                const uint32_t fseg = (uint32_t)(w >> 32);
+                if (fseg >= nseg) { finish(ST_SEGID); break; }
+                uint64_t off, slen;
+                if (!seg_lookup(fseg, off, slen)) { start_seek(fseg, VK_PTR, va, vb); break; }
+                if (landing + (dbl ? 16 : 8) > slen) { finish(ST_OOB); break; }
+                pnest = nest;
+                if (!dbl) {  // the landing word is validatePointer'd at the same nesting
+                    pseg = fseg;
+                    ppos = landing;
+                    request(VK_PTR, d + off + landing, 8);
+                } else {
+                    request(VK_LAND2, d + off + landing, 16);
+                }
+                break;
+            }
+            case VK_LAND2: {  // :754-771 (nesting: pnest)
+                const uint64_t lw = va, tw = vb;
+                if ((lw & 3) != 2 || ((lw >> 2) & 1u)) { finish(ST_FAR); break; }
+                const uint32_t s2 = (uint32_t)(lw >> 32);
+                if (s2 >= nseg) { finish(ST_SEGID); break; }
+                uint64_t off, slen;
+                if (!seg_lookup(s2, off, slen)) { start_seek(s2, VK_LAND2, va, vb); break; }
+                const uint64_t eo = ((lw >> 3) & 0x1FFFFFFFu) * 8;
+                if ((tw & 3) == 0) {  // validateInlineCompositeTag (:929-968), layout A
+                    if (ptr_offset_words(tw) < 0) { finish(ST_ICP); break; }
+                    const uint64_t tot = (uint64_t)ptr_offset_words(tw) * (((tw >> 32) & 0xFFFFu) + (tw >> 48));
+                    composite(s2, eo, tw, tot, pnest);
+                    break;
+                }
+                if ((tw & 3) != 1) { finish(ST_FAR); break; }
+                if (((tw >> 32) & 7u) != 7) { plain_list(s2, eo, tw, pnest); break; }
+                // layout B (:827-869): the tag is at the landing pad's target
+                if (eo + 8 > slen) { finish(ST_OOB); break; }
+                tseg = s2;
+                tpos = eo;
+                twc = tw >> 35;
+                request(VK_TAG, d + off + eo, 8);
+                break;
+            }
+            case VK_TAG: {  // the tag checks of :583-600 / :833-851, then the elements
+                const uint64_t tag = va;
+                if ((tag & 3) != 0 || ptr_offset_words(tag) < 0) { finish(ST_ICP); break; }
+                const uint64_t count = (uint64_t)ptr_offset_words(tag);
+                if (count * (((tag >> 32) & 0xFFFFu) + (tag >> 48)) > twc) { finish(ST_ICP); break; }
+                composite(tseg, tpos + 8, tag, twc, pnest);
+                break;
+            }
+            default:
+                break;
+            }
+        }
     }
-    status[msg] = st;
-    if (words) words[msg] = st == ST_OK ? trav_limit - rem : 0ull;
 }
 
 // ---------------------------------------------------------------------------
@@ -2778,8 +2949,21 @@ hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint
                            uint64_t seg_limit, uint64_t trav_limit, uint32_t nest_limit, int32_t* status,
                            uint64_t* words, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    validate_kernel<<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(in, in_off, in_len, n, seg_limit, trav_limit,
-                                                                  nest_limit, status, words);
+    // persistent grid: the resident waves, each owning a contiguous range of messages
+    static const uint32_t resident = [] {  // thread-safe one-time init (C++11 static)
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, validate_kernel, kWave, 0) != hipSuccess || per <= 0)
+            per = 8;
+        return (uint32_t)(cus * per);
+    }();
+    const uint32_t full = (n + kWave - 1) / kWave;
+    const uint32_t blocks = full < resident ? full : resident;
+    const uint32_t per_wave = (uint32_t)(((uint64_t)n + blocks - 1) / blocks);
+    validate_kernel<<<blocks, kWave, 0, stream>>>(in, in_off, in_len, n, per_wave, seg_limit, trav_limit, nest_limit,
+                                                 status, words);
     return hipGetLastError();
 }
 

@@ -67,6 +67,8 @@ class RandomTree:
         self.max_count = max_count
         self.far_rate = far_rate
         self.null_rate = null_rate
+        self.reads = 1  # words Message.validate reads: pointer slots, landing pads, tags
+        self.live = True  # is the pointer being built reached by the walk?
         self.b.alloc(0, 1)
         self.value(0, 0, 0)
 
@@ -93,10 +95,13 @@ class RandomTree:
             dw, pw = int(rng.integers(0, 4)), int(rng.integers(0, 4))
             content = self.b.alloc(t, dw + pw)
             self._data(t, content, dw)
-            self.link(seg, pos, t, content, lambda off: struct_ptr(off, dw, pw),
-                      ("struct", dw, pw))
+            live = self.live
+            self.live = self.link(seg, pos, t, content, lambda off: struct_ptr(off, dw, pw), ("struct", dw, pw)) \
+                and live
+            self.reads += pw if self.live else 0
             for i in range(pw):
                 self.value(t, content + dw + i, depth + 1)
+            self.live = live
         elif kind == "list":
             es = int(rng.integers(0, 6))
             count = int(rng.integers(0, 4 * mc))
@@ -109,6 +114,7 @@ class RandomTree:
             count = int(rng.integers(0, mc))
             content = self.b.alloc(t, count)
             self.link(seg, pos, t, content, lambda off: list_ptr(off, 6, count), ("list", 6, count))
+            self.reads += count if self.live else 0
             for i in range(count):
                 self.value(t, content + i, depth + 1)
         else:
@@ -124,11 +130,14 @@ class RandomTree:
                 self.b.set(pad_seg, pad, far_ptr(False, content, t))
                 self.b.set(pad_seg, pad + 1, tag)
                 self.b.set(seg, pos, far_ptr(True, pad, pad_seg))
+                self.reads += 2 if self.live else 0
             else:
+                self.reads += 1 if self.live else 0
                 tag_at = self.b.alloc(t, 1 + wc)
                 self.b.set(t, tag_at, struct_ptr(count, dw, pw))
                 content = tag_at + 1
                 self.link(seg, pos, t, tag_at, lambda off: list_ptr(off, 7, wc), ("list", 7, wc))
+            self.reads += count * pw if self.live else 0
             for e in range(count):
                 base = content + e * (dw + pw)
                 self._data(t, base, dw)
@@ -137,21 +146,27 @@ class RandomTree:
 
     def link(self, seg, pos, t, content, near, far_tag):
         """Point (seg, pos) at `content` in segment t: near pointer, single far (landing
-        pad = near pointer before the content) or double far (pad = far + tag)."""
+        pad = near pointer before the content) or double far (pad = far + tag). Returns
+        whether Message.validate goes on into the content's pointers."""
         if t == seg:
             self.b.set(seg, pos, near(content - pos - 1))
-            return
+            return True
         if self.rng.random() < 0.5:
             pad = self.b.alloc(t, 1)
             self.b.set(t, pad, near(content - pad - 1))
             self.b.set(seg, pos, far_ptr(False, pad, t))
-            return
+            self.reads += 1 if self.live else 0
+            return True
+        self.reads += 2 if self.live else 0
         pad_seg = int(self.rng.integers(0, len(self.b.segs)))
         pad = self.b.alloc(pad_seg, 2)
         self.b.set(pad_seg, pad, far_ptr(False, content, t))
         kind, a, c = far_tag
         self.b.set(pad_seg, pad + 1, struct_ptr(0, a, c) if kind == "struct" else list_ptr(0, a, c))
         self.b.set(seg, pos, far_ptr(True, pad, pad_seg))
+        # a struct tag behind a double far is read as an inline-composite tag of count 0
+        # (its offset field, validateFarPointer :765-767): the walk stops there
+        return kind != "struct"
 
     def framed(self) -> bytes:
         return self.b.framed()

@@ -95,3 +95,23 @@ def test_valid_trees_validate():
         m = msggen.random_message(rng)
         st, words = oracle.validate(m)
         assert st == 0 and words <= len(m) // 8
+
+
+def test_generator_read_count_matches_walk():
+    # msggen's per-tree count of the words the walk reads (bench.py's algorithmic bytes
+    # for the validate leg) equals the restatement's own count of word reads
+    class Counting(pyref._Validator):
+        n = 0
+
+        def word(self, seg, pos):
+            Counting.n += 1
+            return super().word(seg, pos)
+
+    rng = np.random.default_rng(11)
+    for _ in range(200):
+        t = msggen.RandomTree(rng)
+        segs = pyref.message_segments(t.framed())
+        Counting.n = 0
+        v = Counting(segs, 1 << 40)
+        v.pointer(0, 0, v.word(0, 0), 64)
+        assert Counting.n == t.reads
