@@ -61,14 +61,14 @@ enum capnp_packed_status {
     CAPNP_PACKED_TRUNCATED_MESSAGE = 13,        /* header or a segment runs past the data (message.zig:353/380) */
     /* Message.validate (message.zig:699-969) only: */
     CAPNP_PACKED_EMPTY_MESSAGE = 14,            /* no segments (:700) */
-    CAPNP_PACKED_NESTING_LIMIT_EXCEEDED = 15,   /* a non-null pointer below the nesting limit (:724) */
-    CAPNP_PACKED_INVALID_SEGMENT_ID = 16,       /* a far pointer names a missing segment (:421/:428/:749) */
-    CAPNP_PACKED_INVALID_POINTER = 17,          /* pointer type 3 (capability) where data is validated (:731) */
+    CAPNP_PACKED_NESTING_LIMIT_EXCEEDED = 15,   /* a non-null pointer past the nesting limit (:724) */
+    CAPNP_PACKED_INVALID_SEGMENT_ID = 16,       /* a pointer or landing pad names a missing segment (:421/:431/:725/:761) */
+    CAPNP_PACKED_INVALID_POINTER = 17,          /* pointer type 3 (capability) where data is validated (:732) */
     CAPNP_PACKED_OUT_OF_BOUNDS = 18,            /* an object runs past its segment (bounds.zig:10-13) */
     CAPNP_PACKED_TRAVERSAL_LIMIT_EXCEEDED = 19, /* more words than traversal_limit_words (:711) */
-    CAPNP_PACKED_INVALID_FAR_POINTER = 20,      /* malformed double-far landing pad (:746-757) */
-    CAPNP_PACKED_INVALID_INLINE_COMPOSITE_POINTER = 21, /* bad inline-composite tag (:608-621, :822-832) */
-    CAPNP_PACKED_LIST_TOO_LARGE = 22            /* list size overflows (:944) */
+    CAPNP_PACKED_INVALID_FAR_POINTER = 20,      /* malformed double-far landing pad (:758-760, :771) */
+    CAPNP_PACKED_INVALID_INLINE_COMPOSITE_POINTER = 21, /* bad inline-composite tag (:585-596, :835-845, :938) */
+    CAPNP_PACKED_LIST_TOO_LARGE = 22            /* list size overflows (:945; unreachable: sizes < 2^46 words) */
 };
 
 /* Version / capability query (precedent: src/wasm/capnp_host_abi.zig:60-70). */
@@ -229,8 +229,9 @@ int capnp_packed_message_init_batch(const uint8_t* d_in, const uint64_t* d_in_of
  * limits and error order. d_status[i] = the first error the reference's recursion
  * would raise, or OK; d_words[i] (may be NULL) = traversal words consumed (OK only).
  * The reference defaults are segment_count_limit 512, traversal_limit_words 8 Mi,
- * nesting_limit 64; nesting limits above 64 and messages of 4 GiB or more give
- * INVALID_ARGUMENT. */
+ * nesting_limit 64; nesting limits above 64 (the device stack depth) fail the
+ * call with INVALID_ARGUMENT, and a message of 4 GiB or more gets INVALID_ARGUMENT
+ * as its status. Allocates nothing; capturable in a hipGraph. */
 int capnp_packed_validate_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                 uint32_t n, uint64_t segment_count_limit, uint64_t traversal_limit_words,
                                 uint32_t nesting_limit, int32_t* d_status, uint64_t* d_words, void* stream);

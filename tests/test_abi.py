@@ -83,3 +83,38 @@ def test_no_cpu_fallback_without_device():
         cp.pack_packed(bytes(16))
     with pytest.raises(cp.NoDevice):
         cp.unpack_packed(b"\x00\x00")
+
+
+def header_statuses():
+    text = open(HEADER).read()
+    return {name: int(v) for name, v in re.findall(r"CAPNP_PACKED_(\w+)\s*=\s*(\d+)", text)
+            if name != "ABI_VERSION"}
+
+
+def test_status_tables_agree():
+    # header enum == Python constants / error classes == library names == Zig binding enum
+    st = header_statuses()
+    assert len(st) == 23 and sorted(st.values()) == list(range(23))
+    for name, v in st.items():
+        assert getattr(cp, name) == v, name
+        if v:
+            assert cp._ERRORS[v].status == v
+        assert cp.lib().capnp_packed_status_name(v).decode() != "Unknown"
+    zig = open(os.path.join(REPO, "zig", "packed_ffi.zig")).read()
+    zig_enum = dict((n, int(v)) for n, v in re.findall(r"^\s+(\w+) = (\d+),$", zig, flags=re.M))
+    assert {k.lower(): v for k, v in st.items()} == zig_enum
+
+
+def test_zig_binding_declares_only_header_symbols():
+    zig = open(os.path.join(REPO, "zig", "packed_ffi.zig")).read()
+    externs = set(re.findall(r'extern "capnp_packed" fn (capnp_packed_\w+)', zig))
+    assert externs <= set(declared_functions()), externs - set(declared_functions())
+    assert "capnp_packed_validate_batch" in externs
+
+
+def test_validate_argument_errors_without_device():
+    L = cp.lib()
+    st = L.capnp_packed_validate_batch(None, None, None, 0, 512, 1 << 23, 64, None, None, None)
+    assert st == cp.OK  # n = 0: nothing to do
+    st = L.capnp_packed_validate_batch(None, None, None, 4, 512, 1 << 23, 64, None, None, None)
+    assert st == cp.INVALID_ARGUMENT

@@ -31,6 +31,16 @@ pub const Status = enum(c_int) {
     message_too_large = 11,
     invalid_packed_message = 12,
     truncated_message = 13,
+    // Message.validate (message.zig:699-969)
+    empty_message = 14,
+    nesting_limit_exceeded = 15,
+    invalid_segment_id = 16,
+    invalid_pointer = 17,
+    out_of_bounds = 18,
+    traversal_limit_exceeded = 19,
+    invalid_far_pointer = 20,
+    invalid_inline_composite_pointer = 21,
+    list_too_large = 22,
     _,
 };
 
@@ -79,6 +89,25 @@ pub extern "capnp_packed" fn capnp_packed_message_init_batch(
     d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32, max_segs: u32,
     d_seg_count: [*]u32, d_seg_off: [*]u64, d_seg_len: [*]u64, d_status: [*]i32, stream: ?*anyopaque,
 ) c_int;
+/// Message.validate (message.zig:699-969) of n framed messages; ValidationOptions as
+/// arguments (:331-335). d_status[i]: 0 or the first error; d_words (nullable): words consumed.
+pub extern "capnp_packed" fn capnp_packed_validate_batch(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    segment_count_limit: u64, traversal_limit_words: u64, nesting_limit: u32,
+    d_status: [*]i32, d_words: ?[*]u64, stream: ?*anyopaque,
+) c_int;
+/// Long-unit workspace for the *_batch_ws calls (graph-safe batches with no shared state).
+pub extern "capnp_packed" fn capnp_packed_batch_workspace_bytes(n: u32) usize;
+pub extern "capnp_packed" fn capnp_packed_encode_batch_ws(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
+    d_out_len: [*]u64, d_status: [*]i32, d_ws: ?*anyopaque, ws_bytes: usize, stream: ?*anyopaque,
+) c_int;
+pub extern "capnp_packed" fn capnp_packed_decode_batch_ws(
+    d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
+    d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
+    d_out_len: [*]u64, d_status: [*]i32, d_ws: ?*anyopaque, ws_bytes: usize, stream: ?*anyopaque,
+) c_int;
 pub extern "capnp_packed" fn capnp_packed_scan_scratch_bytes(n: u32) usize;
 pub extern "capnp_packed" fn capnp_packed_lengths_to_offsets(
     d_len: [*]const u64, n: u32, base: u64, d_off: [*]u64,
@@ -113,6 +142,16 @@ pub const Error = error{
     InvalidPackedMessage,
     // Message.init (message.zig:341-394)
     TruncatedMessage,
+    // Message.validate (message.zig:699-969)
+    EmptyMessage,
+    NestingLimitExceeded,
+    InvalidSegmentId,
+    InvalidPointer,
+    OutOfBounds,
+    TraversalLimitExceeded,
+    InvalidFarPointer,
+    InvalidInlineCompositePointer,
+    ListTooLarge,
 };
 
 fn check(status: c_int) Error!void {
@@ -129,6 +168,15 @@ fn check(status: c_int) Error!void {
         .message_too_large => error.MessageTooLarge,
         .invalid_packed_message => error.InvalidPackedMessage,
         .truncated_message => error.TruncatedMessage,
+        .empty_message => error.EmptyMessage,
+        .nesting_limit_exceeded => error.NestingLimitExceeded,
+        .invalid_segment_id => error.InvalidSegmentId,
+        .invalid_pointer => error.InvalidPointer,
+        .out_of_bounds => error.OutOfBounds,
+        .traversal_limit_exceeded => error.TraversalLimitExceeded,
+        .invalid_far_pointer => error.InvalidFarPointer,
+        .invalid_inline_composite_pointer => error.InvalidInlineCompositePointer,
+        .list_too_large => error.ListTooLarge,
         else => {
             std.log.err("capnp_packed: {s}", .{capnp_packed_last_error()});
             return error.PackedDeviceError;
@@ -190,6 +238,11 @@ pub fn readPackedMessageBuffered(allocator: std.mem.Allocator, buffered: []const
         };
         return .{ .framed = try allocator.realloc(buf, len), .consumed = used };
     }
+}
+
+/// A validate_batch per-message status as the error Message.validate would return.
+pub fn validateBatchStatus(status: i32) Error!void {
+    return check(status);
 }
 
 pub fn abiVersion() u32 {
