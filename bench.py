@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
     ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
     ap.add_argument("--no-validate", action="store_true", help="skip the Message.validate leg")
-    ap.add_argument("--only-validate", action="store_true", help=argparse.SUPPRESS)  # dev: validate leg only
+    ap.add_argument("--only", default="", help=argparse.SUPPRESS)  # dev: run one side leg (validate, c5, ...)
     return ap.parse_args()
 
 
@@ -765,8 +765,10 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    if args.only_validate:
-        print(json.dumps({"validate": validate_leg(args, dev)}), flush=True)
+    if args.only:
+        legs = {"validate": validate_leg, "c5": skewed_leg, "dense": dense_leg, "read_message": read_message_leg,
+                "framing": message_leg}
+        print(json.dumps({args.only: legs[args.only](args, dev)}), flush=True)
         return
     n, ub = args.units, args.unit_bytes
     wl = Workload(n, ub, args.seed, args.zero_thresh, unit_base=rank * n, dev=dev)

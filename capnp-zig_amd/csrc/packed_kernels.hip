@@ -566,27 +566,16 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
     return P;
 }
 
+// One unit of encode_kernel (wave-uniform `unit`).
 template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint64_t* __restrict__ in_len,
-                                                        uint32_t n, uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        const uint64_t* __restrict__ out_cap,
-                                                        uint64_t* __restrict__ out_len,
-                                                        int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint64_t lut[256];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WRITE) {
-        lut[threadIdx.x] = compact_selector(threadIdx.x);
-        __syncthreads();
-    }
-    const uint32_t unit = blockIdx.x * kWavesPerBlock + wave;
-    if (unit >= n) return;
-    uint8_t* lds = smem + wave * kEncLds;
-
+__device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
+                                                      const uint64_t* __restrict__ in_off,
+                                                      const uint64_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                      const uint64_t* __restrict__ out_off,
+                                                      const uint64_t* __restrict__ out_cap,
+                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+                                                      uint32_t unit, uint8_t* lds, const uint64_t* lut,
+                                                      uint32_t lane) {
     const uint64_t b0 = in_off[unit];
     const uint64_t nbytes = in_len[unit];
     uint64_t ob = 0, cap = 0;
@@ -617,6 +606,7 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     }
     const uint32_t words = (uint32_t)(nbytes >> 3);
     if (words <= kEncMaxWords) {  // one tile (the headline 4-KiB units)
+        wave_lds_sync();          // the previous unit's write-back read the slice
         encode_stage(lds, src, words, lane);
         wave_lds_sync();
         uint32_t cz = 0, cf = 0;
@@ -625,12 +615,41 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
             out_len[unit] = P;
             status[unit] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
         }
-        return;
     }
     // longer units belong to encode_tiled_kernel, which selects them by the same test
     // (encode_tiled_unit) and may be running beside this kernel on the side stream:
     // nothing of theirs is written here (a separate kernel keeps this one at its
     // register budget)
+}
+
+// A wave per unit: the class list's units (launch_encode: the mid units), or the batch.
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint64_t* __restrict__ in_len,
+                                                        uint32_t n, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint64_t* __restrict__ out_cap,
+                                                        uint64_t* __restrict__ out_len,
+                                                        int32_t* __restrict__ status,
+                                                        const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ list_count) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    uint8_t* lds = smem + wave * kEncLds;
+    // a wave per list entry; a list as long as the batch is the identity (class lists keep
+    // batch order), so the headline's all-mid batches skip the list read
+    const uint32_t count = list ? *list_count : n;
+    const uint32_t slot = blockIdx.x * kWavesPerBlock + wave;
+    if (slot >= count) return;
+    const uint32_t unit = (list && count != n) ? __builtin_amdgcn_readfirstlane(list[slot]) : slot;
+    encode_unit<WRITE>(in, in_off, in_len, out, out_off, out_cap, out_len, status, unit, lds, lut, lane);
 }
 
 // The units encode_tiled_kernel owns: valid word streams (8-aligned start, whole
@@ -642,14 +661,14 @@ __device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t of
            (len >> 3) <= 0xFFFFF000ull;
 }
 
-// Long-unit work queue (device memory, filled by select_long_kernel on the side
-// stream) for a batch of n units: q[0] = long units listed, q[1] = next entry to
-// take, q[2] = huge units listed (more than kQHuge bytes in), q[3] unused; the long
-// units at q[4 ..] upwards, the huge ones from q[4 + n - 1] downwards. A worker wave
+// Long-unit work queue (device memory, filled by the class kernels below) for a batch
+// of n units: q[0] = long units listed, q[1] = next entry to take, q[2] = huge units
+// listed (more than kQHuge bytes in); the long units at q[kQHead ..] upwards, the huge
+// ones from q[kQHead + n - 1] downwards. A worker wave
 // takes entries one at a time (a lane-0 vector atomic), huge units first, so the
 // units that set the tail start first and the rest spread over every worker wave.
 constexpr uint64_t kQHuge = 65536;
-constexpr uint32_t kQHead = 4;
+constexpr uint32_t kQHead = 8;
 __device__ __forceinline__ uint32_t queue_listed(const uint32_t* q) { return q[0] + q[2]; }
 __device__ __forceinline__ bool queue_take(uint32_t* q, uint32_t n, uint32_t lane, uint32_t& unit) {
     uint32_t i = 0;
@@ -667,17 +686,6 @@ __device__ __forceinline__ bool queue_take(uint32_t* q, uint32_t n, uint32_t lan
 
 __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
                                                  uint64_t out_off, uint64_t cap);
-
-// KIND 0: units encode_tiled_unit selects; 1: units decode_long_unit selects. One
-// thread per unit; a wave appends its selected units with one atomic.
-template <int KIND>
-__global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restrict__ in,
-                                                          const uint64_t* __restrict__ in_off,
-                                                          const uint64_t* __restrict__ in_len, uint32_t n,
-                                                          uint8_t* __restrict__ out,
-                                                          const uint64_t* __restrict__ out_off,
-                                                          const uint64_t* __restrict__ out_cap, uint32_t* q,
-                                                          int32_t* __restrict__ status);
 
 // Units longer than one tile (encode_tiled_unit), taken from the long-unit queue
 // and encoded one after another, tile by tile.
@@ -737,39 +745,6 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
         status[unit] = (WRITE && !fits) ? ST_SPACE : ST_OK;
     }
     }  // queued units
-}
-
-template <int KIND>
-__global__ __launch_bounds__(256) void select_long_kernel(const uint8_t* __restrict__ in,
-                                                          const uint64_t* __restrict__ in_off,
-                                                          const uint64_t* __restrict__ in_len, uint32_t n,
-                                                          uint8_t* __restrict__ out,
-                                                          const uint64_t* __restrict__ out_off,
-                                                          const uint64_t* __restrict__ out_cap, uint32_t* q,
-                                                          int32_t* __restrict__ status) {
-    const uint32_t u = blockIdx.x * 256 + threadIdx.x;
-    bool p = false;
-    if (u < n) {
-        p = KIND == 0 ? encode_tiled_unit(in, in_off[u], in_len[u])
-                      : decode_long_unit(in, in_off[u], in_len[u], out, out_off[u], out_cap[u]);
-        // sentinel until the long-unit worker writes the unit's outcome: a unit the
-        // worker never reached shows DEVICE_ERROR, not a stale status
-        if (p) status[u] = kStPending;
-    }
-    const bool huge = p && in_len[u] > kQHuge;
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // long units, then huge units (list layout: queue_take)
-        const bool mine = h ? huge : (p && !huge);
-        const uint64_t m = __ballot(mine);
-        if (m == 0) continue;  // wave-uniform
-        const uint32_t first = (uint32_t)__builtin_ctzll(m);
-        uint32_t base = 0;
-        if (lane == first) base = atomicAdd(q + (h ? 2 : 0), (uint32_t)__popcll(m));
-        base = (uint32_t)__shfl((int)base, (int)first, kWave);
-        const uint32_t i = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (mine) q[h ? kQHead + n - 1 - i : kQHead + i] = u;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1628,14 +1603,19 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-    uint64_t* __restrict__ consumed) {
+    uint64_t* __restrict__ consumed, const uint32_t* __restrict__ list = nullptr,
+    const uint32_t* __restrict__ list_count = nullptr) {
     static_assert(RD != kRdWalk || SIZE_ONLY, "the read walk writes no output");
     static_assert(RD != kRdGate || !SIZE_ONLY, "the gated pass is the write pass");
     constexpr uint32_t kRing = 80;  // [0, 16): block k-1's last piece, [16, 80): block k
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWave * kRing];
     const uint32_t lane = lane_id();
-    const uint32_t unit = blockIdx.x * kWave + lane;
-    const bool valid = unit < n;
+    // with a class list (launch_decode: the mid units), lane l takes list entry 64b + l
+    const uint32_t count = list ? *list_count : n;
+    if (blockIdx.x * kWave >= count) return;  // wave-uniform
+    const uint32_t slot = blockIdx.x * kWave + lane;
+    const bool valid = slot < count;
+    const uint32_t unit = valid ? ((list && count != n) ? list[slot] : slot) : 0u;
 
     // ---- per-lane unit ---------------------------------------------------------------
     const uint8_t* src = cpk_dummy16;
@@ -1893,7 +1873,9 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                                                                        const uint64_t* __restrict__ out_off,
                                                                        const uint64_t* __restrict__ out_len,
                                                                        const uint64_t* __restrict__ out_cap,
-                                                                       const int32_t* __restrict__ status) {
+                                                                       const int32_t* __restrict__ status,
+                                                                       const uint32_t* __restrict__ list = nullptr,
+                                                                       const uint32_t* __restrict__ list_count = nullptr) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFlWaves * kFlPk];
     __shared__ __attribute__((aligned(16))) uint16_t code_all[kFlWaves * (kFlOut + 8)];  // + a dummy slot
     __shared__ uint64_t lut[256];  // tag -> v_perm selector scattering popc(tag) packed bytes
@@ -1903,24 +1885,30 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     __syncthreads();
     uint8_t* const pk = pk_all + wave * kFlPk;
     uint16_t* const code = code_all + wave * (kFlOut + 8);
-    const uint32_t G = gridDim.x * kFlWaves;  // persistent: the wave takes units u0, u0+G, u0+2G, ...
+    // persistent: the wave takes units u0, u0+G, u0+2G, ... (entries of the class list, if any)
+    const uint32_t G = gridDim.x * kFlWaves;
     const uint32_t u0 = blockIdx.x * kFlWaves + wave;
+    const uint32_t n_all = n;
+    const bool listed = list != nullptr;  // class list: none of its units is the fallback's
+    if (list) n = *list_count;
     if (u0 >= n) return;
+    if (n == n_all) list = nullptr;  // a list as long as the batch is the identity (batch order)
 
     uint64_t m_in = 0, m_out = 0;
     uint32_t m_P = 0, m_T = 0;
     int32_t m_st = -1;
     auto load_batch = [&](uint32_t k0) {  // meta of the wave's units k0 .. k0+63
-        const uint64_t uu = (uint64_t)u0 + (uint64_t)(k0 + lane) * G;
+        const uint64_t slot = (uint64_t)u0 + (uint64_t)(k0 + lane) * G;
         m_st = -1;
-        if (uu < n) {
+        if (slot < n) {
+            const uint32_t uu = list ? list[slot] : (uint32_t)slot;
             m_in = in_off[uu];
             const uint64_t P = in_len[uu];
             m_P = (uint32_t)P;
             m_out = out_off[uu];
             // the fallback's units (it may be writing their status right now) are skipped
-            // without reading what pass 1 left for them
-            if (!decode_long_unit(in, m_in, P, out, m_out, out_cap[uu])) {
+            // without reading what pass 1 left for them (a class list holds none)
+            if (listed || !decode_long_unit(in, m_in, P, out, m_out, out_cap[uu])) {
                 m_T = (uint32_t)(out_len[uu] >> 3);
                 m_st = status[uu];
             }
@@ -2086,6 +2074,506 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
         for (int i = 0; i < 5; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- size classes ------------------------------------------------
+// A batch's units are split by size before the coding kernels run, so each kernel gets
+// units of the shape it is built for:
+//   small: lane per unit (encode_small_kernel / decode_small_kernel): units so short that
+//          a wave per unit would leave most of its 64 lanes idle (config C5: median 15 words);
+//   mid:   a wave per unit (encode_kernel) / the indexed decoder (decode_index_kernel,
+//          64 units per wave, then decode_fill_kernel, a wave per unit);
+//   long, huge: a wave per unit walking it tile by tile / window by window
+//          (encode_tiled_kernel / decode_wave_kernel<kWvLong>), on the side stream.
+// Workspace q (queue_bytes(n)): q[0] long, q[1] take cursor, q[2] huge, q[3] small and
+// q[4] mid counts; the long list at q[kQHead ..] upwards and the huge list from
+// q[kQHead + n - 1] downwards (queue_take), the small list at q[kQHead + n ..], the mid
+// list at q[kQHead + 2n ..], then kClassK counts per class block. Count, scan, scatter:
+// each list keeps batch order, and no atomic is contended.
+constexpr uint32_t kClassBlock = 1024;
+constexpr uint32_t kClassK = 4;
+enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3 };
+constexpr uint64_t kSmEncWords = 64;  // encode: units of at most 64 words are small
+constexpr uint64_t kSmDecP = 512;     // decode: small = at most 512 packed bytes ...
+constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
+
+__device__ __forceinline__ uint32_t* q_blocks(uint32_t* q, uint32_t n) { return q + kQHead + 3ull * n; }
+
+template <int KIND>  // 0: encode, 1: decode
+__device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                                               uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                                               uint32_t u) {
+    const uint64_t off = in_off[u], len = in_len[u];
+    if (KIND == 0) {
+        if (encode_tiled_unit(in, off, len)) return len > kQHuge ? CL_HUGE : CL_LONG;
+        const bool valid = !(reinterpret_cast<uintptr_t>(in + off) & 7) && !(len & 7);
+        return (!valid || (len >> 3) <= kSmEncWords) ? CL_SMALL : CL_MID;
+    }
+    const uint64_t cap = out_cap[u];
+    if (len <= kSmDecP && cap <= kSmDecCap) return CL_SMALL;
+    if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
+    return CL_MID;
+}
+
+// Pass 1: units per class in each block of kClassBlock units; long units get the
+// kStPending sentinel until their worker writes their outcome (a unit the worker never
+// reached shows DEVICE_ERROR, not a stale status).
+template <int KIND>
+__global__ __launch_bounds__(kClassBlock) void class_count_kernel(const uint8_t* __restrict__ in,
+                                                                  const uint64_t* __restrict__ in_off,
+                                                                  const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                  uint8_t* __restrict__ out,
+                                                                  const uint64_t* __restrict__ out_off,
+                                                                  const uint64_t* __restrict__ out_cap, uint32_t* q,
+                                                                  int32_t* __restrict__ status) {
+    __shared__ uint32_t cnt[kClassK];
+    if (threadIdx.x < kClassK) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t u = blockIdx.x * kClassBlock + threadIdx.x;
+    const uint32_t c = u < n ? unit_class<KIND>(in, in_off, in_len, out, out_off, out_cap, u) : kClassK;
+    if (c <= CL_HUGE) status[u] = kStPending;
+#pragma unroll
+    for (uint32_t k = 0; k < kClassK; ++k) {
+        const uint64_t m = __ballot(c == k);
+        if (m && lane_id() == 0) atomicAdd(&cnt[k], (uint32_t)__popcll(m));  // LDS
+    }
+    __syncthreads();
+    if (threadIdx.x < kClassK) q_blocks(q, n)[blockIdx.x * kClassK + threadIdx.x] = cnt[threadIdx.x];
+}
+
+// Pass 2 (one block): exclusive scan of the block counts per class, and the totals.
+__global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t n, uint32_t nb) {
+    __shared__ uint32_t wsum[16][kClassK];
+    __shared__ uint32_t carry[kClassK];
+    uint32_t* const bl = q_blocks(q, n);
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x < kClassK) carry[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+        const uint32_t b = b0 + threadIdx.x;
+        uint32_t v[kClassK], incl[kClassK];
+#pragma unroll
+        for (uint32_t k = 0; k < kClassK; ++k) {
+            v[k] = b < nb ? bl[b * kClassK + k] : 0u;
+            incl[k] = wave_incl_sum(v[k], lane);
+            if (lane == 63) wsum[w][k] = incl[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kClassK; ++k) {
+            uint32_t pre = carry[k];
+            for (uint32_t j = 0; j < w; ++j) pre += wsum[j][k];
+            if (b < nb) bl[b * kClassK + k] = pre + incl[k] - v[k];
+        }
+        __syncthreads();
+        if (threadIdx.x < kClassK) {
+            uint32_t t = 0;
+            for (uint32_t j = 0; j < 16; ++j) t += wsum[j][threadIdx.x];
+            carry[threadIdx.x] += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        q[0] = carry[CL_LONG];
+        q[2] = carry[CL_HUGE];
+        q[3] = carry[CL_SMALL];
+        q[4] = carry[CL_MID];
+    }
+}
+
+// Pass 3: every unit to its place in its class list (batch order within a class).
+template <int KIND>
+__global__ __launch_bounds__(kClassBlock) void class_scatter_kernel(const uint8_t* __restrict__ in,
+                                                                    const uint64_t* __restrict__ in_off,
+                                                                    const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                    uint8_t* __restrict__ out,
+                                                                    const uint64_t* __restrict__ out_off,
+                                                                    const uint64_t* __restrict__ out_cap, uint32_t* q) {
+    __shared__ uint32_t wcnt[16][kClassK];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t u = blockIdx.x * kClassBlock + threadIdx.x;
+    const uint32_t c = u < n ? unit_class<KIND>(in, in_off, in_len, out, out_off, out_cap, u) : kClassK;
+    uint32_t rank = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kClassK; ++k) {
+        const uint64_t m = __ballot(c == k);
+        if (lane == 0) wcnt[w][k] = (uint32_t)__popcll(m);
+        if (c == k) rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();
+    if (c >= kClassK) return;
+    uint32_t idx = q_blocks(q, n)[blockIdx.x * kClassK + c] + rank;
+    for (uint32_t j = 0; j < w; ++j) idx += wcnt[j][c];
+    if (c == CL_LONG) q[kQHead + idx] = u;
+    else if (c == CL_HUGE) q[kQHead + n - 1 - idx] = u;
+    else q[kQHead + (c == CL_SMALL ? 1ull : 2ull) * n + idx] = u;
+}
+
+// ---- small units, lane per unit -----------------------------------------------------------
+// A persistent grid: each wave owns a contiguous range of the small list and its lanes
+// take the range's next unit as they finish (a wave-uniform cursor, as in
+// validate_kernel), so one longer unit does not idle the rest of its wave. Every turn
+// of the wave's loop issues at most one read per lane (the unit's metadata, or its next
+// 16 B) and then codes the 16 B read one turn earlier: the read's latency overlaps the
+// work.
+constexpr uint32_t kSmBlock = 256;
+enum : uint32_t { SM_IDLE, SM_EXIT, SM_META, SM_FIRST, SM_RUN };
+
+// Zig encoder rules (message.zig:200-271) as a word-at-a-time state machine: a zero run
+// (00 n-1) is emitted when it ends; a literal run's count byte (FF w0 n-1 w1..) is
+// patched when it ends (in the chunk being assembled, or with a byte store once that
+// chunk has been written).
+template <bool WRITE>
+__global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ in_off,
+                                                                const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint64_t* __restrict__ out_len,
+                                                                int32_t* __restrict__ status, const uint32_t* q) {
+    __shared__ uint64_t lut[256];
+    if (WRITE) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    const uint32_t count = q[3];
+    const uint32_t* const list = q + kQHead + n;
+    const uint32_t lane = lane_id();
+    const uint32_t gw = blockIdx.x * (kSmBlock / kWave) + (threadIdx.x >> 6);
+    const uint32_t GW = gridDim.x * (kSmBlock / kWave);
+    const uint32_t per = (count + GW - 1) / GW;
+    const uint64_t first = (uint64_t)gw * per;
+    const uint64_t last = min((uint64_t)count, first + per);
+    uint64_t cursor = first;  // wave-uniform
+
+    uint32_t kind = SM_IDLE, unit = 0;
+    const uint8_t* cb = in;     // 16-B aligned base of the unit's input
+    uint32_t s8 = 0, nw = 0;    // word index space: the unit's words are [s8, nw)
+    uint32_t cj = 0, nch = 0;   // chunk in (c0, c1); chunks of the unit
+    uint64_t c0 = 0, c1 = 0, n0 = 0, n1 = 0;
+    uint8_t* db = out;          // 16-B aligned base of the output slot
+    uint32_t da = 0;            // slot start & 15
+    uint64_t cap = 0, op = 0;   // slot capacity; packed bytes so far
+    uint64_t b0 = 0, b1 = 0;    // the output chunk being assembled: chunk (da + op) >> 4
+    uint32_t mode = 0, run = 0; // 0: none, 1: zero run, 2: literal run; its length
+    uint64_t cpos = 0;          // literal run: output offset of its count byte
+
+    auto finish = [&](int32_t st, uint64_t len) {
+        out_len[unit] = len;
+        status[unit] = st;
+        kind = SM_IDLE;
+    };
+    // write bytes [lo, hi) of output chunk `ch` (slot-relative, clipped to the slot)
+    auto flush = [&](uint64_t ch, uint32_t lo, uint32_t hi) {
+        const uint64_t cs = 16 * ch;
+        const uint64_t lim = cap > ~0ull - 16 ? ~0ull : da + cap;  // slot end (saturated)
+        const uint64_t a = max(cs + lo, (uint64_t)da), e = min(cs + hi, lim);
+        if (a >= e) return;
+        if (a == cs && e == cs + 16) {
+            // plain store: a later count-byte patch of this chunk must land after it
+            *reinterpret_cast<u32x4*>(db + cs) = u32x4{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1,
+                                                      (uint32_t)(b1 >> 32)};
+        } else {
+            for (uint64_t x = a; x < e; ++x) {
+                const uint32_t k = (uint32_t)(x - cs);
+                db[x] = (uint8_t)((k < 8 ? b0 >> (8 * k) : b1 >> (8 * (k - 8))) & 0xFF);
+            }
+        }
+    };
+    auto append = [&](uint64_t v, uint32_t nb) {  // nb <= 8 bytes of v (higher bytes zero)
+        if (WRITE) {
+            const uint32_t k = (uint32_t)((da + op) & 15);
+            uint64_t spill = 0;
+            if (k < 8) {
+                b0 |= v << (8 * k);
+                if (k) b1 |= v >> (64 - 8 * k);
+            } else {
+                const uint32_t j = k - 8;
+                b1 |= v << (8 * j);
+                if (j) spill = v >> (64 - 8 * j);
+            }
+            if (k + nb >= 16) {
+                flush((da + op) >> 4, 0, 16);
+                b0 = spill;
+                b1 = 0;
+            }
+        }
+        op += nb;
+    };
+    auto close_run = [&]() {
+        if (mode == 1) {
+            append((uint64_t)(run - 1) << 8, 2);  // 00 <count>
+        } else if (mode == 2 && WRITE) {           // the literal run's count byte
+            const uint64_t x = da + cpos;
+            if ((x >> 4) == ((da + op) >> 4)) {
+                const uint32_t k = (uint32_t)(x & 15);
+                if (k < 8) b0 |= (uint64_t)(run - 1) << (8 * k);
+                else b1 |= (uint64_t)(run - 1) << (8 * (k - 8));
+            } else if (cpos < cap) {
+                db[x] = (uint8_t)(run - 1);
+            }
+        }
+        mode = 0;
+    };
+    auto word = [&](uint64_t w) {  // message.zig:206-266, one word
+        const uint32_t tg = nonzero_tag(w);
+        if (mode == 1) {
+            if (tg == 0 && run < 256) { ++run; return; }
+            close_run();
+        } else if (mode == 2) {
+            if (tg == 0xFF && run < 256) { append(w, 8); ++run; return; }
+            close_run();
+        }
+        if (tg == 0) {
+            mode = 1;
+            run = 1;
+        } else if (tg == 0xFF) {
+            append(0xFFull | (w << 8), 8);  // FF w0 ...
+            append(w >> 56, 1);
+            cpos = op;
+            append(0, 1);                   // count, patched by close_run
+            mode = 2;
+            run = 1;
+        } else {
+            append((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) << 8 : 0ull), 1 + __popc(tg));
+        }
+    };
+
+    for (;;) {
+        const uint64_t idle = __ballot(kind == SM_IDLE);
+        if (idle) {
+            if (cursor < last) {
+                if (kind == SM_IDLE) {
+                    const uint64_t id = cursor + __popcll(idle & ((1ull << lane) - 1ull));
+                    if (id < last) {
+                        unit = list[id];
+                        kind = SM_META;
+                    } else {
+                        kind = SM_EXIT;
+                    }
+                }
+                cursor += __popcll(idle);
+            } else if (kind == SM_IDLE) {
+                kind = SM_EXIT;
+            }
+        }
+        if (__ballot(kind != SM_EXIT) == 0) break;
+        // ---- this turn's read -----------------------------------------------------------
+        uint64_t m_off = 0, m_len = 0, m_oo = 0, m_cap = 0;
+        if (kind == SM_META) {
+            m_off = in_off[unit];
+            m_len = in_len[unit];
+            if (WRITE) {
+                m_oo = out_off[unit];
+                m_cap = out_cap[unit];
+            }
+        } else if (kind == SM_RUN && cj + 1 < nch) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(cb + 16ull * (cj + 1));
+            n0 = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+            n1 = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+        }
+        // ---- code what the previous turn read -----------------------------------------------
+        if (kind == SM_META) {
+            const uint8_t* const src = in + m_off;
+            if (reinterpret_cast<uintptr_t>(src) & 7) finish(ST_ARG, 0);
+            else if (m_len & 7) finish(ST_SIZE, 0);  // message.zig:201
+            else if (m_len == 0) finish(ST_OK, 0);
+            else {
+                s8 = (uint32_t)((reinterpret_cast<uintptr_t>(src) >> 3) & 1);
+                cb = src - 8 * s8;
+                nw = s8 + (uint32_t)(m_len >> 3);
+                nch = (nw + 1) >> 1;
+                uint8_t* const dst = out + m_oo;
+                da = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
+                db = dst - da;
+                cap = m_cap;
+                op = 0;
+                b0 = b1 = 0;
+                mode = 0;
+                cj = 0;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(cb);  // chunk 0 (once per unit)
+                c0 = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                c1 = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+                kind = SM_RUN;
+            }
+        } else if (kind == SM_RUN) {
+            const uint32_t w0 = 2 * cj;
+            if (w0 >= s8) word(c0);
+            if (w0 + 1 < nw) word(c1);
+            if (cj + 1 < nch) {
+                c0 = n0;
+                c1 = n1;
+                ++cj;
+            } else {
+                close_run();
+                if (WRITE && ((da + op) & 15)) flush((da + op) >> 4, 0, (uint32_t)((da + op) & 15));
+                finish((WRITE && op > cap) ? ST_SPACE : ST_OK, op);
+            }
+        }
+    }
+}
+
+// unpackPacked (message.zig:88-145) for one unit per lane: a 32-B window of the packed
+// bytes in registers (pieces wb/16, wb/16 + 1) and the next piece read each turn; a
+// turn decodes the records that start in the window's first piece. A truncated record
+// is UnexpectedEof with nothing more written (the batch contract: INTEGRATION.md §4).
+__global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ in_off,
+                                                                const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                const uint64_t* __restrict__ out_cap,
+                                                                uint64_t* __restrict__ out_len,
+                                                                int32_t* __restrict__ status, const uint32_t* q) {
+    __shared__ uint64_t lut[256];
+    lut[threadIdx.x] = expand_selector(threadIdx.x);
+    __syncthreads();
+    const uint32_t count = q[3];
+    const uint32_t* const list = q + kQHead + n;
+    const uint32_t lane = lane_id();
+    const uint32_t gw = blockIdx.x * (kSmBlock / kWave) + (threadIdx.x >> 6);
+    const uint32_t GW = gridDim.x * (kSmBlock / kWave);
+    const uint32_t per = (count + GW - 1) / GW;
+    const uint64_t first = (uint64_t)gw * per;
+    const uint64_t last = min((uint64_t)count, first + per);
+    uint64_t cursor = first;  // wave-uniform
+
+    uint32_t kind = SM_IDLE, unit = 0;
+    const uint8_t* base = in;  // 16-B aligned base of the packed unit
+    uint32_t end = 0, pos = 0, wb = 0, np = 0;  // aligned space: bytes [s, end); window base
+    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, n0 = 0, n1 = 0;
+    uint64_t* dst = nullptr;
+    uint32_t capw = 0, wo = 0, lit = 0;
+    uint64_t cap = 0;
+
+    auto finish = [&](int32_t st) {
+        if (st == ST_OK) {
+            out_len[unit] = 8ull * wo;
+            status[unit] = 8ull * wo > cap ? ST_SPACE : ST_OK;
+        } else {
+            out_len[unit] = 0;
+            status[unit] = st;
+        }
+        kind = SM_IDLE;
+    };
+    auto piece = [&](uint32_t i, uint64_t& a, uint64_t& b) {
+        if (i < np) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(base + 16ull * i);
+            a = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+            b = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+        } else {
+            a = b = 0;
+        }
+    };
+    auto emit = [&](uint64_t w) {
+        if (wo < capw) dst[wo] = w;
+        ++wo;
+    };
+
+    for (;;) {
+        const uint64_t idle = __ballot(kind == SM_IDLE);
+        if (idle) {
+            if (cursor < last) {
+                if (kind == SM_IDLE) {
+                    const uint64_t id = cursor + __popcll(idle & ((1ull << lane) - 1ull));
+                    if (id < last) {
+                        unit = list[id];
+                        kind = SM_META;
+                    } else {
+                        kind = SM_EXIT;
+                    }
+                }
+                cursor += __popcll(idle);
+            } else if (kind == SM_IDLE) {
+                kind = SM_EXIT;
+            }
+        }
+        if (__ballot(kind != SM_EXIT) == 0) break;
+        // ---- this turn's read -----------------------------------------------------------
+        uint64_t m_off = 0, m_len = 0, m_oo = 0, m_cap = 0;
+        if (kind == SM_META) {
+            m_off = in_off[unit];
+            m_len = in_len[unit];
+            m_oo = out_off[unit];
+            m_cap = out_cap[unit];
+        } else if (kind == SM_FIRST) {
+            piece(0, q0, q1);
+            piece(1, q2, q3);
+            piece(2, n0, n1);
+        } else if (kind == SM_RUN) {
+            piece((wb >> 4) + 2, n0, n1);
+        }
+        // ---- decode ----------------------------------------------------------------------------
+        if (kind == SM_META) {
+            const uint8_t* const src = in + m_off;
+            const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+            base = src - s;
+            end = s + (uint32_t)m_len;  // m_len <= kSmDecP
+            np = (end + 15) >> 4;
+            pos = s;
+            wb = 0;
+            uint8_t* const o = out + m_oo;
+            dst = reinterpret_cast<uint64_t*>(o);
+            cap = m_cap;
+            capw = (uint32_t)(m_cap >> 3);
+            wo = 0;
+            lit = 0;
+            if (reinterpret_cast<uintptr_t>(o) & 7) finish(ST_ARG);
+            else if (m_len == 0) finish(ST_OK);
+            else kind = SM_FIRST;
+        } else if (kind == SM_FIRST || kind == SM_RUN) {
+            const uint32_t limit = wb + 16;
+            int32_t st = ST_OK;
+            bool done = false;
+            for (uint32_t it = 0; it < 16; ++it) {
+                if (lit) {
+                    if (pos >= limit) break;
+                    emit(view_word8(q0, q1, q2, q3, pos - wb));  // an FF run's body word
+                    pos += 8;
+                    --lit;
+                    continue;
+                }
+                if (pos >= end) {
+                    done = true;
+                    break;
+                }
+                if (pos >= limit) break;
+                const uint32_t o = pos - wb;
+                const uint32_t t = view_byte(q0, q1, q2, q3, o);
+                if (t == 0x00) {  // message.zig:101-110
+                    if (pos + 2 > end) { st = ST_EOF; break; }
+                    const uint32_t c = view_byte(q0, q1, q2, q3, o + 1);
+                    const uint32_t k = min(c + 1, capw > wo ? capw - wo : 0u);
+                    for (uint32_t j = 0; j < k; ++j) dst[wo + j] = 0;
+                    wo += c + 1;
+                    pos += 2;
+                } else if (t == 0xFF) {  // message.zig:112-128
+                    if (pos + 10 > end) { st = ST_EOF; break; }
+                    const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
+                    if (pos + 10 + 8 * c > end) { st = ST_EOF; break; }
+                    emit(view_word8(q0, q1, q2, q3, o + 1));
+                    lit = c;
+                    pos += 10;
+                } else {  // message.zig:131-141
+                    const uint32_t k = __popc(t);
+                    if (pos + 1 + k > end) { st = ST_EOF; break; }
+                    emit(perm64(view_word8(q0, q1, q2, q3, o + 1), lut[t]));
+                    pos += 1 + k;
+                }
+            }
+            if (st != ST_OK) finish(st);
+            else if (done) finish(ST_OK);
+            else {
+                q0 = q2;
+                q1 = q3;
+                q2 = n0;
+                q3 = n1;
+                wb += 16;
+                kind = SM_RUN;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2720,7 +3208,33 @@ struct StreamCtx {
 static std::mutex g_ctx_mu;
 static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
 
-size_t queue_bytes(uint32_t n) { return (kQHead + (size_t)n) * sizeof(uint32_t); }
+size_t queue_bytes(uint32_t n) {
+    const size_t nb = ((size_t)n + kClassBlock - 1) / kClassBlock;
+    return (kQHead + 3 * (size_t)n + kClassK * nb) * sizeof(uint32_t);
+}
+
+// Resident blocks of a kernel across the device (hipOccupancy...), for persistent grids.
+template <typename K>
+static uint32_t resident_blocks(K kernel, int block, uint32_t fallback_per_cu) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || per <= 0)
+        per = (int)fallback_per_cu;
+    return (uint32_t)(cus * per);
+}
+
+// Class the batch's units (class_count / class_scan / class_scatter) on the caller's stream.
+template <int KIND>
+static void launch_classes(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                           uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint32_t* q,
+                           int32_t* status, hipStream_t stream) {
+    const uint32_t nb = (n + kClassBlock - 1) / kClassBlock;
+    class_count_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q, status);
+    class_scan_kernel<<<1, 1024, 0, stream>>>(q, n, nb);
+    class_scatter_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q);
+}
 
 class SideLaunch {
   public:
@@ -2755,16 +3269,21 @@ class SideLaunch {
                 return;
             }
         }
-        if (hipEventRecord(ctx_->fork, main_) != hipSuccess || hipStreamWaitEvent(ctx_->s, ctx_->fork, 0) != hipSuccess)
-            return;
         side_ = ctx_->s;
-        forked_ = true;
         ok_ = true;
     }
-    // the stream the long-unit kernels go on (valid once queue() succeeded)
+    // the stream the long-unit kernels go on (after fork())
     hipStream_t stream() const { return side_; }
-    // The long-unit queue for a batch of n units, its counters cleared on the side
-    // stream; nullptr when the side stream or the queue cannot be set up.
+    // The side stream waits for everything enqueued on the caller's stream so far.
+    hipError_t fork() {
+        if (!ok_ || side_ == main_ || forked_) return ok_ ? hipSuccess : hipErrorNotReady;
+        hipError_t e = hipEventRecord(ctx_->fork, main_);
+        if (e == hipSuccess) e = hipStreamWaitEvent(side_, ctx_->fork, 0);
+        if (e == hipSuccess) forked_ = true;
+        return e;
+    }
+    // The class workspace for a batch of n units (queue_bytes), its counters cleared on
+    // the caller's stream; nullptr when the side stream or the queue cannot be set up.
     uint32_t* queue(uint32_t n) {
         if (!ok_) return nullptr;
         uint32_t* q = nullptr;
@@ -2783,7 +3302,7 @@ class SideLaunch {
             }
             q = ctx_->q;
         }
-        if (hipMemsetAsync(q, 0, kQHead * sizeof(uint32_t), side_) != hipSuccess) return nullptr;
+        if (hipMemsetAsync(q, 0, kQHead * sizeof(uint32_t), main_) != hipSuccess) return nullptr;
         return q;
     }
     hipError_t join() {
@@ -2809,28 +3328,37 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    // units of more than 512 words: encode_tiled_kernel over a grid that strides the batch
-    const uint32_t groups = (n + kWave - 1) / kWave;
-    // (side stream, launched first so the long units start early; the two kernels own
-    // disjoint units: encode_tiled_unit)
-    const uint32_t tiled_blocks = min((groups + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    // classes (caller's stream), then the long units on the side stream (encode_tiled_kernel
+    // over a grid taking units from the queue) beside the small units (a lane each) and the
+    // mid units (a wave each) on the caller's stream
+    static const uint32_t sm_res = resident_blocks(encode_small_kernel<true>, kSmBlock, 8);
+    const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
+    const uint32_t mid_blocks = blocks_for(n);  // waves past the mid count return at once
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
+    launch_classes<0>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    hipError_t e = side.fork();
+    if (e != hipSuccess) return e;
     const hipStream_t ss = side.stream();
-    select_long_kernel<0><<<(n + 255) / 256, 256, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap, q, status);
+    const uint32_t* const mid = q + kQHead + 2ull * n;
     if (write) {
         encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, q);
-        encode_kernel<true><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                   out_len, status);
+        encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                       out_len, status, q);
+        encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
+                                                                status, mid, q + 4);
     } else {
         encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status, q);
-        encode_kernel<false><<<blocks_for(n), kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                    out_len, status);
+        encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                        out_len, status, q);
+        encode_kernel<false><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                 out_len, status, mid, q + 4);
     }
-    const hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     const hipError_t j = side.join();
     return e != hipSuccess ? e : j;
 }
@@ -2881,17 +3409,24 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     }
     // index pass, fill pass; the fallback owns the long units from the start
     // (decode_long_unit): it goes first, on the side stream, beside passes 1 and 2
+    static const uint32_t sm_res = resident_blocks(decode_small_kernel, kSmBlock, 8);
+    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-    select_long_kernel<1><<<(n + 255) / 256, 256, 0, side.stream()>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                     q, status);
+    launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    hipError_t e = side.fork();
+    if (e != hipSuccess) return e;
     decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
         in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
-    launch_index<false>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+    decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
+                                                             status, q);
+    const uint32_t* const mid = q + kQHead + 2ull * n;
+    decode_index_kernel<false><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4);
     decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_len,
-                                                                       out_cap, status);
-    const hipError_t e = hipGetLastError();
+                                                                       out_cap, status, mid, q + 4);
+    e = hipGetLastError();
     const hipError_t j = side.join();
     return e != hipSuccess ? e : j;
 }
