@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Phase cycle breakdown of decode_fill_kernel (diagnostic build, CPK_LIB=lib_exp/prof.so)."""
+"""Phase cycle breakdown of decode_unit_kernel (diagnostic build, CPK_LIB=lib_exp/prof.so)."""
 import ctypes, json, os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "capnp-zig_amd"))
 import torch
@@ -22,7 +22,7 @@ ust = torch.zeros(n, dtype=torch.int32, device=dev)
 L = cp.lib()
 f = L.capnp_packed_debug_fill_prof
 f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 cp.decode_batch(d_pk, pk_off, plen, d_out, in_off, in_len, ulen, ust)
 torch.cuda.synchronize()
 f(buf)
@@ -31,6 +31,6 @@ for _ in range(reps):
     cp.decode_batch(d_pk, pk_off, plen, d_out, in_off, in_len, ulen, ust)
 torch.cuda.synchronize()
 f(buf)
-names = ["wait_data", "stage+records", "issue_next", "scan+walk", "total_iter"]
+names = ["wait_data", "stage+issue", "entry_maps", "scan+walk1", "verify", "sums", "codes", "expand", "redo_walks", "units_done"]
 per_unit = {nm: round(buf[i] / (reps * n), 1) for i, nm in enumerate(names)}
 print(json.dumps({"thr": thr, "cycles_per_unit_per_wave": per_unit, "roundtrip": bool(torch.equal(d_out, d_in))}))
