@@ -96,23 +96,46 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane >= (uint32_t)d) v += t;
-    }
+// Wave scans on DPP: row_shr:1/2/4/8 inside each 16-lane row, then row_bcast:15 and
+// row_bcast:31 across rows (gfx9). A lane a step does not reach keeps `ident`. No LDS
+// round trips (the ds_bpermute scans they replace cost ~6 LDS latencies in a row).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v, uint32_t ident) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWS, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t /*lane*/) {
+    v += dpp_mov<0x111, 0xF>(v, 0u);
+    v += dpp_mov<0x112, 0xF>(v, 0u);
+    v += dpp_mov<0x114, 0xF>(v, 0u);
+    v += dpp_mov<0x118, 0xF>(v, 0u);
+    v += dpp_mov<0x142, 0xA>(v, 0u);
+    v += dpp_mov<0x143, 0xC>(v, 0u);
     return v;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane >= (uint32_t)d) v = max(v, t);
-    }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v, uint32_t /*lane*/) {
+    v = max(v, dpp_mov<0x111, 0xF>(v, 0u));
+    v = max(v, dpp_mov<0x112, 0xF>(v, 0u));
+    v = max(v, dpp_mov<0x114, 0xF>(v, 0u));
+    v = max(v, dpp_mov<0x118, 0xF>(v, 0u));
+    v = max(v, dpp_mov<0x142, 0xA>(v, 0u));
+    v = max(v, dpp_mov<0x143, 0xC>(v, 0u));
     return v;
 }
+
+__device__ __forceinline__ uint32_t wave_incl_min(uint32_t v) {
+    v = min(v, dpp_mov<0x111, 0xF>(v, ~0u));
+    v = min(v, dpp_mov<0x112, 0xF>(v, ~0u));
+    v = min(v, dpp_mov<0x114, 0xF>(v, ~0u));
+    v = min(v, dpp_mov<0x118, 0xF>(v, ~0u));
+    v = min(v, dpp_mov<0x142, 0xA>(v, ~0u));
+    v = min(v, dpp_mov<0x143, 0xC>(v, ~0u));
+    return v;
+}
+
+// the previous lane's v (wave_shr:1); lane 0 gets ident
+__device__ __forceinline__ uint32_t wave_prev_lane(uint32_t v, uint32_t ident) { return dpp_mov<0x138, 0xF>(v, ident); }
 
 // inclusive min over lanes >= this lane
 __device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v, uint32_t lane) {
@@ -368,9 +391,7 @@ __device__ __forceinline__ void encode_stage(uint8_t* lds, const uint8_t* src, u
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, kWave));
-    return v;
+    return __builtin_amdgcn_readlane(wave_incl_min(v), kWave - 1);
 }
 
 // First Z break and first F break among words [0, nw) of src, nw <= 256, as
@@ -450,8 +471,8 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
         scan = ((bz0 & (bz7 << 1)) | (bf0 & (bf7 << 1))) != 0;
     }
     if (scan) {
-        cz = __shfl_up(wave_incl_max(lbz, lane), 1, kWave);
-        cf = __shfl_up(wave_incl_max(lbf, lane), 1, kWave);
+        cz = wave_prev_lane(wave_incl_max(lbz, lane), 0u);
+        cf = wave_prev_lane(wave_incl_max(lbf, lane), 0u);
         ez = __shfl_down(wave_incl_suffix_min(fbz, lane), 1, kWave);
         ef = __shfl_down(wave_incl_suffix_min(fbf, lane), 1, kWave);
         if (lane == 0) { cz = cz_c; cf = cf_c; }
@@ -1804,7 +1825,7 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
 
 #ifdef CPK_FILL_PROF
 // Diagnostic build: cycles per fill-kernel phase, summed over waves (s_memtime).
-__device__ unsigned long long cpk_fill_prof[16];
+__device__ unsigned long long cpk_fill_prof[8];
 #define FL_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define FL_ACC(i, d) prof[i] += (d)
 #else
@@ -2076,434 +2097,6 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---- single-pass decoder -------------------------------------------
-// decode_unit_kernel: unpackPacked (message.zig:88-145) for the batch's mid units, a wave
-// per unit, with no earlier pass over the packed bytes. Persistent grid; the wave's next
-// unit is loaded into registers while the current one is decoded. The unit's pieces are
-// staged in LDS and lane l owns pieces [lL, lL + L) (L = ceil(pieces / 64)). The record
-// chain (tag -> record length -> next tag) is resolved in the wave:
-//  1. Entry maps. A lane's state d at byte x means "the next tag is at x + d"; a byte
-//     maps d = 0 to len(x) - 1 and d > 0 to d - 1. For the 8 entry states d in 0..7 at its
-//     range start, the lane composes those maps byte by byte: a map is 8 bytes, one
-//     state per entry, and composing is two v_perm_b32 (the byte's table [len-1, 0, 1,
-//     .., 6] selected by the current states). Records other than FF are 2..8 bytes, so
-//     states stay in 0..7; an FF tag's state (9 + 8c) does not fit and becomes an
-//     absorbing marker (a selector >= 13 yields 0xFF), replaced at the end by the
-//     lane's most common exit (walks from different entries merge within a few records).
-//  2. A wave scan composes the maps: lane k's entry state is (F_{k-1} o .. o F_0)(0)
-//     (lane 0 starts at the unit's first byte: its bytes before it map to themselves).
-//  3. Each lane walks its records from that entry (LDS reads of tag, byte 1, byte 9):
-//     tag mask, decoded words, exit (first tag at or after its range end). The entries
-//     are checked: lane k's must be the furthest exit of lanes < k. Lanes that disagree
-//     walk again from it until all agree; agreement everywhere is the true chain, by
-//     induction from lane 0 (an FF record is the usual cause of a second walk).
-//  4. A wave scan of the words gives each lane its first output word; the lanes list the
-//     source of every output word from their tag masks (u16 codes, as the fill pass) and
-//     the wave expands and stores by output word, coalesced.
-// A record running past the unit's end is UnexpectedEof; like an OutOfSpace unit, its
-// slot is left untouched (the output is written only after the whole chain is known).
-constexpr uint32_t kUnWaves = 4;
-constexpr uint32_t kUnPk = kFlPieces * 16 + 16;  // staged pieces + room for reads past the last tag
-constexpr uint32_t kUnInf = 0xFFFFFFFFu;         // exit of a walk that ran past the unit's end
-constexpr uint32_t kUnMaskW = 3;                 // tag-mask dwords per lane (a lane's range is <= 80 B)
-
-// The units decode_unit_kernel cannot stage (> kFlPieces pieces of 16 B) with an
-// 8-aligned slot: decode_wave_kernel<kWvLong> owns them (unit_class).
-__device__ __forceinline__ bool decode_unit_long(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
-                                                 uint64_t out_off) {
-    if (P == 0 || (reinterpret_cast<uintptr_t>(out + out_off) & 7)) return false;
-    const uint64_t s = reinterpret_cast<uintptr_t>(in + in_off) & 15;
-    return (s + P + 15) >> 4 > kFlPieces;
-}
-
-// ---- wave scans on DPP: row_shr inside 16-lane rows, then row_bcast:15 / :31 across
-// rows (gfx9). Lanes a step does not reach keep `ident`.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp_mov(uint32_t v, uint32_t ident) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWS, 0xF, false);
-}
-__device__ __forceinline__ uint32_t dpp_incl_sum(uint32_t v) {
-    v += dpp_mov<0x111, 0xF>(v, 0u);
-    v += dpp_mov<0x112, 0xF>(v, 0u);
-    v += dpp_mov<0x114, 0xF>(v, 0u);
-    v += dpp_mov<0x118, 0xF>(v, 0u);
-    v += dpp_mov<0x142, 0xA>(v, 0u);
-    v += dpp_mov<0x143, 0xC>(v, 0u);
-    return v;
-}
-__device__ __forceinline__ uint32_t dpp_incl_max(uint32_t v) {
-    v = max(v, dpp_mov<0x111, 0xF>(v, 0u));
-    v = max(v, dpp_mov<0x112, 0xF>(v, 0u));
-    v = max(v, dpp_mov<0x114, 0xF>(v, 0u));
-    v = max(v, dpp_mov<0x118, 0xF>(v, 0u));
-    v = max(v, dpp_mov<0x142, 0xA>(v, 0u));
-    v = max(v, dpp_mov<0x143, 0xC>(v, 0u));
-    return v;
-}
-__device__ __forceinline__ uint32_t dpp_prev_lane(uint32_t v, uint32_t ident) {  // wave_shr:1
-    return dpp_mov<0x138, 0xF>(v, ident);
-}
-
-// Entry maps (decode_unit_kernel step 1): 8 states, one per byte, lo = entries 0..3,
-// hi = entries 4..7. (A o B)(e) = A(B(e)) is two v_perm_b32 with B as the selectors.
-constexpr uint32_t kMapIdLo = 0x03020100u, kMapIdHi = 0x07060504u;
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void map_scan_step(uint32_t& lo, uint32_t& hi) {
-    const uint32_t blo = dpp_mov<CTRL, ROWS>(lo, kMapIdLo), bhi = dpp_mov<CTRL, ROWS>(hi, kMapIdHi);
-    const uint32_t nlo = __builtin_amdgcn_perm(hi, lo, blo);
-    const uint32_t nhi = __builtin_amdgcn_perm(hi, lo, bhi);
-    lo = nlo;
-    hi = nhi;
-}
-// inclusive: lane k ends with F_k o .. o F_0
-__device__ __forceinline__ void map_incl_scan(uint32_t& lo, uint32_t& hi) {
-    map_scan_step<0x111, 0xF>(lo, hi);
-    map_scan_step<0x112, 0xF>(lo, hi);
-    map_scan_step<0x114, 0xF>(lo, hi);
-    map_scan_step<0x118, 0xF>(lo, hi);
-    map_scan_step<0x142, 0xA>(lo, hi);
-    map_scan_step<0x143, 0xC>(lo, hi);
-}
-// byte t's table [len(t) - 1, 0, 1, 2 | 3, 4, 5, 6]: glut[t] = popc(t), 1 for a 00 tag
-// (2-byte record) and 16 for FF, whose 9 + 8c does not fit: a v_perm_b32 selector >= 13
-// yields 0xFF, which selects 0xFF again (absorbing)
-__device__ __forceinline__ uint32_t entry_glut(uint32_t t) {
-    return t == 0 ? 1u : (t == 0xFFu ? 16u : (uint32_t)__builtin_popcount(t));
-}
-
-__global__ __launch_bounds__(kUnWaves * kWave) void decode_unit_kernel(const uint8_t* __restrict__ in,
-                                                                       const uint64_t* __restrict__ in_off,
-                                                                       const uint64_t* __restrict__ in_len,
-                                                                       uint32_t n, uint8_t* __restrict__ out,
-                                                                       const uint64_t* __restrict__ out_off,
-                                                                       const uint64_t* __restrict__ out_cap,
-                                                                       uint64_t* __restrict__ out_len,
-                                                                       int32_t* __restrict__ status,
-                                                                       const uint32_t* __restrict__ list,
-                                                                       const uint32_t* __restrict__ list_count) {
-    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kUnWaves * kUnPk];
-    __shared__ __attribute__((aligned(16))) uint16_t code_all[kUnWaves * (kFlOut + 8)];  // + a dummy slot
-    __shared__ uint32_t tmask_all[kUnWaves * kWave * kUnMaskW];  // lane's tag bits (ds_or)
-    __shared__ uint64_t lut[256];  // tag -> v_perm selector scattering popc(tag) packed bytes
-    __shared__ uint8_t glut[256];  // tag -> entry-map table byte 0 (entry_glut)
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    lut[threadIdx.x] = expand_selector(threadIdx.x);
-    glut[threadIdx.x] = (uint8_t)entry_glut(threadIdx.x);
-    __syncthreads();
-    uint8_t* const pk = pk_all + wave * kUnPk;
-    uint16_t* const code = code_all + wave * (kFlOut + 8);
-    uint32_t* const tmask = tmask_all + (wave * kWave + lane) * kUnMaskW;
-    // persistent: the wave takes list entries u0, u0+G, u0+2G, ...
-    const uint32_t G = gridDim.x * kUnWaves;
-    const uint32_t u0 = blockIdx.x * kUnWaves + wave;
-    const uint32_t count = *list_count;
-    if (u0 >= count) return;
-    if (count == n) list = nullptr;  // every unit is mid: the list is the identity
-
-    uint64_t m_in = 0, m_out = 0, m_cap = 0;
-    uint32_t m_P = 0, m_u = 0;
-    int32_t m_st = -1;
-    auto load_batch = [&](uint32_t k0) {  // meta of the wave's units k0 .. k0+63
-        const uint64_t slot = (uint64_t)u0 + (uint64_t)(k0 + lane) * G;
-        m_st = -1;
-        if (slot < count) {
-            const uint32_t uu = list ? list[slot] : (uint32_t)slot;
-            m_u = uu;
-            m_in = in_off[uu];
-            m_P = (uint32_t)in_len[uu];  // <= kFlPieces * 16 (unit_class)
-            m_out = out_off[uu];
-            m_cap = out_cap[uu];
-            m_st = (reinterpret_cast<uintptr_t>(out + m_out) & 7) ? ST_ARG : ST_OK;
-        }
-    };
-    struct Meta {
-        int32_t st;
-        uint32_t P, u;
-        const uint8_t* src;
-        uint8_t* dst;
-        uint64_t cap;
-    };
-    auto meta = [&](uint32_t j) {  // the batch's unit j (wave-uniform j)
-        Meta m;
-        m.st = (int32_t)readlane((uint32_t)m_st, j);
-        m.P = readlane(m_P, j);
-        m.u = readlane(m_u, j);
-        m.src = in + ((uint64_t)readlane((uint32_t)m_in, j) | ((uint64_t)readlane((uint32_t)(m_in >> 32), j) << 32));
-        m.dst = out + ((uint64_t)readlane((uint32_t)m_out, j) | ((uint64_t)readlane((uint32_t)(m_out >> 32), j) << 32));
-        m.cap = (uint64_t)readlane((uint32_t)m_cap, j) | ((uint64_t)readlane((uint32_t)(m_cap >> 32), j) << 32);
-        return m;
-    };
-    // the prefetched unit's pieces: lane l holds pieces l + 64m
-    uint4 v0, v1, v2, v3, v4;
-    auto load_unit = [&](const Meta& m) {
-        if (m.st != ST_OK || m.P == 0) return;  // wave-uniform
-        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(m.src) & 15);
-        const uint4* const b = reinterpret_cast<const uint4*>(m.src - s);
-        const uint32_t np = (s + m.P + 15) >> 4;
-        const uint32_t last = np - 1;
-        v0 = load_nt(b + min(lane, last));
-        if (np > 64) v1 = load_nt(b + min(lane + 64, last));
-        if (np > 128) v2 = load_nt(b + min(lane + 128, last));
-        if (np > 192) v3 = load_nt(b + min(lane + 192, last));
-        if (np > 256) v4 = load_nt(b + min(lane + 256, last));
-    };
-
-    load_batch(0);
-    Meta cur = meta(0);
-    load_unit(cur);
-    uint32_t younger = 0;  // vector-memory ops issued after cur's loads (its predecessor's stores)
-#ifdef CPK_FILL_PROF
-    uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    for (uint32_t k = 0; (uint64_t)u0 + (uint64_t)k * G < count; ++k) {
-        const bool go = cur.st == ST_OK && cur.P > 0;
-        FL_T(t0);
-        vmcnt_at_most(younger);  // cur's pieces are in registers
-        FL_T(t1);
-        FL_ACC(0, t1 - t0);
-        younger = 0;
-        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(cur.src) & 15);
-        const uint32_t end = s + cur.P;  // aligned space: the unit is bytes [s, end)
-        const uint32_t np = (end + 15) >> 4;
-        if (go) {
-            wave_lds_sync();  // the previous unit's LDS reads are done
-            uint4* const pk4 = reinterpret_cast<uint4*>(pk);
-            pk4[lane] = v0;
-            if (np > 64) pk4[lane + 64] = v1;
-            if (np > 128) pk4[lane + 128] = v2;
-            if (np > 192) pk4[lane + 192] = v3;
-            if (np > 256) pk4[lane + 256] = v4;
-            tmask[0] = 0;
-            tmask[1] = 0;
-            tmask[2] = 0;
-        }
-        // the next unit's loads go out before any store of this unit
-        const uint32_t k1 = k + 1;
-        if ((k1 & 63) == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of cur in flight but its loads (landed)
-            load_batch(k1);
-        }
-        const Meta nxt = meta(k1 & 63);  // st = -1 past the batch end
-        load_unit(nxt);
-        if (!go) {
-            if (lane == 0) {  // an argument error, or an empty unit
-                out_len[cur.u] = 0;
-                status[cur.u] = cur.st;
-            }
-            cur = nxt;
-            continue;
-        }
-        wave_lds_sync();  // pieces staged
-        FL_T(t2);
-        FL_ACC(1, t2 - t1);
-
-        // ---- 1. entry maps over the lane's range [rs, rs + 16L) -----------------------------
-        const uint32_t L = (np + 63) >> 6;  // <= 5
-        const uint32_t q0 = min(lane * L, np), q1 = min(q0 + L, np);
-        const bool active = q0 < np;
-        const uint32_t rs = 16 * q0;
-        const uint32_t jend = min(16 * q1, end);  // tags of this lane start in [.., jend)
-        uint32_t flo = kMapIdLo, fhi = kMapIdHi;
-        for (uint32_t j = 0; j < L; ++j) {
-            const uint4 pc = *reinterpret_cast<const uint4*>(pk + 16 * min(q0 + j, np - 1));
-            const uint32_t dw[4] = {pc.x, pc.y, pc.z, pc.w};
-            uint32_t g[16];
-#pragma unroll
-            for (uint32_t b = 0; b < 16; ++b) g[b] = glut[(dw[b >> 2] >> (8 * (b & 3))) & 0xFFu];
-#pragma unroll
-            for (uint32_t b = 0; b < 16; ++b) {
-                const uint32_t x = g[b] | 0x02010000u;
-                flo = __builtin_amdgcn_perm(0x06050403u, x, flo);
-                fhi = __builtin_amdgcn_perm(0x06050403u, x, fhi);
-                if (b == 7 && j == 0 && lane == 0 && s >= 8) {  // lane 0 enters at s: bytes 0..7 unused
-                    flo = kMapIdLo;
-                    fhi = kMapIdHi;
-                }
-            }
-        }
-        // absorbed (FF) entries: 16 -> 0xFF, then the exit state of the first entry that is not
-        flo = __builtin_amdgcn_perm(kMapIdHi, kMapIdLo, flo);
-        fhi = __builtin_amdgcn_perm(kMapIdHi, kMapIdLo, fhi);
-        {
-            const uint64_t F = (uint64_t)flo | ((uint64_t)fhi << 32);
-            const uint64_t xm = (F >> 7) & 0x0101010101010101ull;  // 1 in each absorbed entry
-            const uint64_t nx = xm ^ 0x0101010101010101ull;
-            const uint32_t R = nx ? (uint32_t)(F >> (__builtin_ctzll(nx) & 56u)) & 0xFFu : 0u;
-            const uint64_t xmask = (xm << 8) - xm;  // 0xFF in each absorbed entry
-            const uint32_t Rb = R * 0x01010101u;
-            flo = (flo & ~(uint32_t)xmask) | (Rb & (uint32_t)xmask);
-            fhi = (fhi & ~(uint32_t)(xmask >> 32)) | (Rb & (uint32_t)(xmask >> 32));
-        }
-        FL_T(t3);
-        FL_ACC(2, t3 - t2);
-        // ---- 2. compose across lanes: lane k enters at (F_{k-1} o .. o F_0)(e0) ----------------
-        map_incl_scan(flo, fhi);
-        const uint32_t plo = dpp_prev_lane(flo, kMapIdLo), phi = dpp_prev_lane(fhi, kMapIdHi);
-        const uint32_t e0 = s >= 8 ? s - 8 : s;  // lane 0's entry state
-        uint32_t entry = lane == 0 ? s : rs + (__builtin_amdgcn_perm(phi, plo, e0) & 0xFFu);
-
-        // ---- 3. walk the lane's records from its entry; re-walk until the entries agree ------
-        uint32_t words = 0, exitp = 0;
-        bool eof = false;
-        auto walk = [&](bool mine) {
-            uint32_t pos = entry, wd_sum = 0;
-            bool e_any = false;
-            for (;;) {  // one record per lane per pass; predicated body, uniform exit
-                const bool act = mine && pos < jend;
-                if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                const uint32_t pp = act ? pos : 0u;
-                uint32_t t = pk[pp];
-                uint32_t b1 = pk[pp + 1];
-                uint32_t c9 = pk[pp + 9];
-                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per record
-                const bool z = t == 0u, f = t == 0xFFu;
-                const uint32_t len = __popc(t) + ((z | f) ? 2u : 1u) + (f ? 8u * c9 : 0u);
-                const bool e = act && pos + len > end;  // message.zig:101-141: record past the input
-                const bool ok = act && !e;
-                if (ok) {
-                    const uint32_t o = pos - rs;
-                    __hip_atomic_fetch_or(tmask + (o >> 5), 1u << (o & 31), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WAVEFRONT);
-                }
-                wd_sum += ok ? 1u + (z ? b1 : 0u) + c9 * (uint32_t)f : 0u;
-                e_any = e_any || e;
-                pos = e ? kUnInf : (ok ? pos + len : pos);
-            }
-            if (mine) {
-                exitp = pos;
-                words = wd_sum;
-                eof = e_any;
-            }
-        };
-        walk(active);
-        FL_T(t4);
-        FL_ACC(3, t4 - t3);
-        for (uint32_t it = 0; it < kWave; ++it) {
-            const uint32_t want = dpp_prev_lane(dpp_incl_max(active ? exitp : 0u), 0u);  // furthest exit of lanes < k
-            const bool redo = active && lane > 0 && want != entry;
-            if (__builtin_amdgcn_ballot_w64(redo) == 0) break;
-            if (redo) {
-                entry = want;
-                tmask[0] = 0;
-                tmask[1] = 0;
-                tmask[2] = 0;
-            }
-            walk(redo);
-            FL_ACC(8, 1);
-        }
-        FL_T(t5);
-        FL_ACC(4, t5 - t4);
-        const bool ueof = __builtin_amdgcn_ballot_w64(active && eof) != 0;
-        const uint32_t incl = dpp_incl_sum(words);
-        const uint32_t wbase = incl - words;
-        const uint32_t T = readlane(incl, kWave - 1);
-        const bool space = 8ull * T > cur.cap;
-        if (lane == 0) {
-            out_len[cur.u] = ueof ? 0ull : 8ull * T;
-            status[cur.u] = ueof ? ST_EOF : (space ? ST_SPACE : ST_OK);
-        }
-        FL_T(t6);
-        FL_ACC(5, t6 - t5);
-        FL_ACC(9, 1);
-        if (ueof || space) {
-            cur = nxt;
-            continue;
-        }
-#ifdef CPK_FILL_PROF
-        uint64_t tex = 0;
-#endif
-
-        // ---- 4. codes from the tag masks, expansion by output word --------------------------
-        const bool a16 = !(reinterpret_cast<uintptr_t>(cur.dst) & 15);
-        uint64_t* const dst = reinterpret_cast<uint64_t*>(cur.dst);
-        wave_lds_sync();  // the walks' tag bits (ds_or) are in
-        const uint32_t mk0 = tmask[0], mk1 = tmask[1], mk2 = tmask[2];
-        for (uint32_t W0 = 0; W0 < T; W0 += kFlOut) {
-            const uint32_t W1 = min(T, W0 + kFlOut);
-            wave_lds_sync();  // the previous pass's code reads are done
-            reinterpret_cast<uint4*>(code)[lane] = make_uint4(kFlZero * 0x10001u, kFlZero * 0x10001u,
-                                                              kFlZero * 0x10001u, kFlZero * 0x10001u);
-            wave_lds_sync();
-            const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
-            uint64_t a0 = mine ? ((uint64_t)mk0 | ((uint64_t)mk1 << 32)) : 0ull;
-            uint32_t a1 = mine ? mk2 : 0u;
-            uint32_t w = wbase;
-            // two records per pass: both records' bytes are read before either is coded
-            auto take = [&](uint32_t& o) {
-                const bool has = (a0 | (uint64_t)a1) != 0;
-                o = a0 ? (uint32_t)__builtin_ctzll(a0) : 64u + (uint32_t)__builtin_ctz(a1 | 0x10000u);
-                if (a0) a0 &= a0 - 1;
-                else a1 &= a1 - 1;
-                return has;
-            };
-            for (;;) {
-                const bool more = (a0 | (uint64_t)a1) != 0 && w < W1;
-                if (__builtin_amdgcn_ballot_w64(more) == 0) break;
-                uint32_t oa = 0, ob = 0;
-                const bool ha = more && take(oa);
-                const bool hb = more && take(ob);
-                const uint32_t pa = ha ? rs + oa : 0u, pb = hb ? rs + ob : 0u;
-                uint32_t ta = pk[pa], ba = pk[pa + 1], ca = pk[pa + 9];
-                uint32_t tb = pk[pb], bb = pk[pb + 1], cb = pk[pb + 9];
-                asm volatile("" : "+v"(ta), "+v"(ba), "+v"(ca), "+v"(tb), "+v"(bb), "+v"(cb));
-                auto rec = [&](bool act, uint32_t pp, uint32_t t, uint32_t b1, uint32_t c9) {
-                    act = act && w < W1;
-                    const bool z = t == 0u, f = t == 0xFFu;
-                    // message.zig:101-141: 00 -> zero word(s) (the list starts as kFlZero), FF ->
-                    // its first word (tag 0xFF selects the 8 bytes) + c literal words, other
-                    // tags -> scatter of popc(t) bytes
-                    code[(act && !z && w >= W0) ? w - W0 : kFlOut] = (uint16_t)pp;
-                    const uint32_t c = f ? c9 : 0u;
-                    if (act && c) {  // FF run body: literal word i at bytes pp+2+8i .. pp+9+8i
-                        for (uint32_t i = 1; i <= c; ++i) {
-                            const uint32_t wi = w + i;
-                            if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (pp + 1 + 8 * i));
-                        }
-                    }
-                    w = act ? w + 1u + (z ? b1 : 0u) + c : w;
-                };
-                rec(ha, pa, ta, ba, ca);
-                rec(hb, pb, tb, bb, cb);
-            }
-            wave_lds_sync();
-            FL_T(t7);
-            const uint32_t nw = W1 - W0;
-            if (a16) {
-                for (uint32_t i = 2 * lane; i < nw; i += 2 * kWave) {
-                    const uint32_t cc = *reinterpret_cast<const uint32_t*>(code + i);
-                    const uint64_t x0 = fill_word(pk, lut, cc & 0xFFFFu);
-                    const uint64_t x1 = fill_word(pk, lut, cc >> 16);
-                    if (i + 1 < nw) {  // streaming output: non-temporal
-                        const u32x4 v = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
-                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + W0 + i));
-                    }
-                    else dst[W0 + i] = x0;
-                }
-                younger += (nw + 2 * kWave - 1) / (2 * kWave);
-            } else {
-                for (uint32_t i = lane; i < nw; i += kWave) dst[W0 + i] = fill_word(pk, lut, code[i]);
-                younger += (nw + kWave - 1) / kWave;
-            }
-#ifdef CPK_FILL_PROF
-            FL_T(t8);
-            tex += t8 - t7;
-#endif
-        }
-#ifdef CPK_FILL_PROF
-        FL_T(t9);
-        FL_ACC(7, tex);
-        FL_ACC(6, t9 - t6 - tex);
-#endif
-        cur = nxt;
-    }
-#ifdef CPK_FILL_PROF
-    if (lane == 0)
-        for (int i = 0; i < 10; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // ---- size classes ------------------------------------------------
 // A batch's units are split by size before the coding kernels run, so each kernel gets
 // units of the shape it is built for:
@@ -2539,7 +2132,7 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
     }
     const uint64_t cap = out_cap[u];
     if (len <= kSmDecP && cap <= kSmDecCap) return CL_SMALL;
-    if (decode_unit_long(in, off, len, out, out_off[u])) return len > kQHuge ? CL_HUGE : CL_LONG;
+    if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
     return CL_MID;
 }
 
@@ -3835,8 +3428,8 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
             in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
         return hipGetLastError();
     }
-    // classes; the fallback owns the long units (decode_unit_long): it goes first, on the
-    // side stream, beside the small units (a lane each) and the mid units (a wave each)
+    // index pass, fill pass; the fallback owns the long units from the start
+    // (decode_long_unit): it goes first, on the side stream, beside passes 1 and 2
     static const uint32_t sm_res = resident_blocks(decode_small_kernel, kSmBlock, 8);
     const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
     SideLaunch side(stream, ws, ws_bytes);
@@ -3850,10 +3443,10 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                              status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
-    static const uint32_t un_res = resident_blocks(decode_unit_kernel, kUnWaves * kWave, 4);
-    const uint32_t un_blocks = min((n + kUnWaves - 1) / kUnWaves, un_res);
-    decode_unit_kernel<<<un_blocks, kUnWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                   out_len, status, mid, q + 4);
+    decode_index_kernel<false><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4);
+    decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_len,
+                                                                       out_cap, status, mid, q + 4);
     e = hipGetLastError();
     const hipError_t j = side.join();
     return e != hipSuccess ? e : j;
@@ -3962,7 +3555,7 @@ hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t*
 #ifdef CPK_FILL_PROF
 // Diagnostic build only: read and clear the fill-kernel phase cycle sums.
 extern "C" int capnp_packed_debug_fill_prof(unsigned long long* out8) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_fill_prof), sizeof(z)) != hipSuccess) return 1;
     return hipMemcpyToSymbol(HIP_SYMBOL(cpk::cpk_fill_prof), z, sizeof(z)) != hipSuccess;
 }
