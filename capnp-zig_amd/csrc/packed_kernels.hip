@@ -169,30 +169,35 @@ __device__ __forceinline__ uint64_t perm64(uint64_t d, uint64_t sel) {
     return (uint64_t)a | ((uint64_t)b << 32);
 }
 
-// Selector that gathers the nonzero bytes of a word with tag t into bytes 0..popc-1.
-__device__ inline uint64_t compact_selector(uint32_t t) {
-    uint64_t sel = 0x0C0C0C0C0C0C0C0CULL;
-    int r = 0;
-    for (int k = 0; k < 8; ++k) {
-        if ((t >> k) & 1u) {
-            sel = (sel & ~(0xFFULL << (8 * r))) | ((uint64_t)k << (8 * r));
-            ++r;
+// v_perm_b32 selector tables, built at compile time (a block copies one into LDS):
+//   compact: gathers the nonzero bytes of a word with tag t into bytes 0..popc-1
+//            (0x0C = zero above them);
+//   expand:  scatters popc(t) packed bytes back to the set-bit positions of t.
+struct SelLut {
+    uint64_t v[256];
+};
+constexpr SelLut make_sel_lut(bool expand) {
+    SelLut lut{};
+    for (uint32_t t = 0; t < 256; ++t) {
+        uint64_t sel = expand ? 0ull : 0x0C0C0C0C0C0C0C0CULL;
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < 8; ++k) {
+            const bool set = (t >> k) & 1u;
+            if (expand) {
+                sel |= (set ? (uint64_t)(r++) : 0x0Cull) << (8 * k);
+            } else if (set) {
+                sel = (sel & ~(0xFFULL << (8 * r))) | ((uint64_t)k << (8 * r));
+                ++r;
+            }
         }
+        lut.v[t] = sel;
     }
-    return sel;
+    return lut;
 }
-
-// Selector that scatters popc(t) packed bytes back to the set-bit positions of t.
-__device__ inline uint64_t expand_selector(uint32_t t) {
-    uint64_t sel = 0;
-    int r = 0;
-    for (int k = 0; k < 8; ++k) {
-        uint64_t s = 0x0C;
-        if ((t >> k) & 1u) s = (uint64_t)(r++);
-        sel |= s << (8 * k);
-    }
-    return sel;
-}
+__device__ constexpr SelLut kCompactLut = make_sel_lut(false);
+__device__ constexpr SelLut kExpandLut = make_sel_lut(true);
+__device__ __forceinline__ uint64_t compact_selector(uint32_t t) { return kCompactLut.v[t]; }
+__device__ __forceinline__ uint64_t expand_selector(uint32_t t) { return kExpandLut.v[t]; }
 
 // Unaligned 8-byte read from an LDS byte array (two aligned ds_read_b64 + funnel).
 __device__ __forceinline__ uint64_t lds_read_u64_unaligned(const uint8_t* base, uint32_t p) {
