@@ -3358,7 +3358,10 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     // over a grid taking units from the queue) beside the small units (a lane each) and the
     // mid units (a wave each) on the caller's stream
     static const uint32_t sm_res = resident_blocks(encode_small_kernel<true>, kSmBlock, 8);
-    const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    // long-unit workers: up to one wave per unit, at most the resident grid (a batch of a
+    // few long units must not get a grid sized by its unit count / 256)
+    static const uint32_t tiled_res = resident_blocks(encode_tiled_kernel<true>, kBlock, 3);
+    const uint32_t tiled_blocks = min((n + kWavesPerBlock - 1) / kWavesPerBlock, tiled_res);
     const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
     const uint32_t mid_blocks = blocks_for(n);  // waves past the mid count return at once
     SideLaunch side(stream, ws, ws_bytes);
@@ -3443,7 +3446,9 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
-    decode_wave_kernel<kWvLong><<<fallback_blocks(n), kWvBlock, 0, side.stream()>>>(
+    static const uint32_t long_res = resident_blocks(decode_wave_kernel<kWvLong>, kWvBlock, 4);
+    const uint32_t long_blocks = min((n + kWvWaves - 1) / kWvWaves, long_res);  // up to a wave per unit
+    decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, side.stream()>>>(
         in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
     decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                              status, q);
