@@ -134,6 +134,21 @@ __device__ __forceinline__ uint32_t wave_incl_min(uint32_t v) {
     return v;
 }
 
+// sum of a u64 over the wave (DPP steps on both halves, 64-bit adds)
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#define CPK_SUM64_STEP(CTRL, ROWS)                                                              \
+    v += (uint64_t)dpp_mov<CTRL, ROWS>((uint32_t)v, 0u) | ((uint64_t)dpp_mov<CTRL, ROWS>((uint32_t)(v >> 32), 0u) << 32)
+    CPK_SUM64_STEP(0x111, 0xF);
+    CPK_SUM64_STEP(0x112, 0xF);
+    CPK_SUM64_STEP(0x114, 0xF);
+    CPK_SUM64_STEP(0x118, 0xF);
+    CPK_SUM64_STEP(0x142, 0xA);
+    CPK_SUM64_STEP(0x143, 0xC);
+#undef CPK_SUM64_STEP
+    return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, kWave - 1) |
+           ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), kWave - 1) << 32);
+}
+
 // the previous lane's v (wave_shr:1); lane 0 gets ident
 __device__ __forceinline__ uint32_t wave_prev_lane(uint32_t v, uint32_t ident) { return dpp_mov<0x138, 0xF>(v, ident); }
 
@@ -361,12 +376,12 @@ __device__ void serial_unpack(const uint8_t* p, uint64_t n, uint8_t* out) {
 //     more than 256 words ahead cannot change a count, so 256 words suffice.
 
 // Stage words [0, words) of src (8-aligned) into the row layout: word w at
-// lds[(w >> 3) * kEncRow + (w & 7) * 8].
-__device__ __forceinline__ void encode_stage(uint8_t* lds, const uint8_t* src, uint32_t words, uint32_t lane) {
+// lds[(w >> 3) * kEncRow + (w & 7) * 8]. Split in two so a persistent wave can have the
+// next unit's loads in flight while it codes the current one (encode_kernel).
+__device__ __forceinline__ void encode_load(uint4 (&v)[5], const uint8_t* src, uint32_t words, uint32_t lane) {
     const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);  // 0 or 8
     const uint8_t* g = src - s;
     const uint32_t nch = (s + 8 * words + 15) >> 4;
-    uint4 v[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         if ((uint32_t)(64 * k) < nch) {
@@ -374,6 +389,10 @@ __device__ __forceinline__ void encode_stage(uint8_t* lds, const uint8_t* src, u
             v[k] = *reinterpret_cast<const uint4*>(g + 16 * (uint64_t)c);  // (non-temporal: slower, 1.52 -> 1.72 ms)
         }
     }
+}
+__device__ __forceinline__ void encode_put(uint8_t* lds, const uint4 (&v)[5], uint32_t s, uint32_t words,
+                                           uint32_t lane) {
+    const uint32_t nch = (s + 8 * words + 15) >> 4;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         uint32_t c = lane + 64 * k;
@@ -393,6 +412,11 @@ __device__ __forceinline__ void encode_stage(uint8_t* lds, const uint8_t* src, u
             }
         }
     }
+}
+__device__ __forceinline__ void encode_stage(uint8_t* lds, const uint8_t* src, uint32_t words, uint32_t lane) {
+    uint4 v[5];
+    encode_load(v, src, words, lane);
+    encode_put(lds, v, (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15), words, lane);
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
@@ -694,7 +718,7 @@ __device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t of
 // takes entries one at a time (a lane-0 vector atomic), huge units first, so the
 // units that set the tail start first and the rest spread over every worker wave.
 constexpr uint64_t kQHuge = 65536;
-constexpr uint32_t kQHead = 8;
+constexpr uint32_t kQHead = 16;
 __device__ __forceinline__ uint32_t queue_listed(const uint32_t* q) { return q[0] + q[2]; }
 __device__ __forceinline__ bool queue_take(uint32_t* q, uint32_t n, uint32_t lane, uint32_t& unit) {
     uint32_t i = 0;
@@ -728,14 +752,23 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
     __shared__ uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (queue_listed(q) == 0) return;  // no long units (block-uniform)
+    if (q[5] == 0) return;  // no serial units (block-uniform)
     if (WRITE) {
         lut[threadIdx.x] = compact_selector(threadIdx.x);
         __syncthreads();
     }
     uint8_t* lds = smem + wave * kEncLds;
     uint32_t unit = 0;
-    while (queue_take(q, n, lane, unit)) {  // wave-uniform
+    // the units long_tiles_kernel could not list (the serial list), one after another
+    const uint32_t* const serial = q + kQHead + 3ull * n + 4 * ((n + 1023) / 1024);
+    for (;;) {  // wave-uniform
+    {
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(q + 10, 1u);
+        i = __builtin_amdgcn_readfirstlane(i);
+        if (i >= q[5]) break;
+        unit = serial[i];
+    }
     const uint8_t* const src = in + in_off[unit];
     const uint32_t words = (uint32_t)(in_len[unit] >> 3);
     uint64_t ob = 0, cap = 0;
@@ -747,21 +780,29 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
     uint64_t pos = 0;   // packed bytes so far
     bool fits = true;   // every tile so far was written (WRITE)
     for (uint32_t tb = 0; tb < words; tb += kEncMaxWords) {
+        // lane-derived addresses are recomputed per tile, not held across the loops in
+        // registers (loop-invariant hoisting had this kernel at 140 VGPRs)
+        uint32_t lane_u = lane;
+        asm volatile("" : "+v"(lane_u));
         const uint32_t tw = min(kEncMaxWords, words - tb);
         const uint32_t te = tb + tw;
+        // the tile's staging loads go out first, so they and the lookahead's loads land
+        // together (one memory round trip per tile, not two)
+        uint4 v[5];
+        encode_load(v, src + 8ull * tb, tw, lane_u);
         uint32_t nbz = words, nbf = words;
         if (te < words) {
             const uint32_t la = min(256u, words - te);
             uint32_t bz, bf;
-            encode_lookahead(src + 8ull * te, la, lane, bz, bf);
+            encode_lookahead(src + 8ull * te, la, lane_u, bz, bf);
             nbz = bz < la ? te + bz : (la == 256u ? te + 256u : words);
             nbf = bf < la ? te + bf : (la == 256u ? te + 256u : words);
         }
         wave_lds_sync();  // the previous tile's write-back read the slice
-        encode_stage(lds, src + 8ull * tb, tw, lane);
+        encode_put(lds, v, (uint32_t)(reinterpret_cast<uintptr_t>(src + 8ull * tb) & 15), tw, lane_u);
         wave_lds_sync();
         const uint64_t room = (WRITE && fits && pos <= cap) ? cap - pos : 0;
-        const uint32_t Pt = encode_tile<WRITE, false>(lds, lut, lane, tw, tb, cz, cf, nbz, nbf, out + ob + pos,
+        const uint32_t Pt = encode_tile<WRITE, false>(lds, lut, lane_u, tw, tb, cz, cf, nbz, nbf, out + ob + pos,
                                                       room);
         if ((uint64_t)Pt > room) fits = false;
         pos += Pt;
@@ -954,6 +995,10 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
     uint64_t pos = 0;
     bool fits = true;
     for (uint32_t tb = 0; tb < words; tb += kEncMaxWords) {
+        // lane-derived addresses are recomputed per tile, not held across the loops in
+        // registers (loop-invariant hoisting had this kernel at 140 VGPRs)
+        uint32_t lane_u = lane;
+        asm volatile("" : "+v"(lane_u));
         const uint32_t tw = min(kEncMaxWords, words - tb);
         const uint32_t te = tb + tw;
         uint32_t nbz = words, nbf = words;
@@ -2235,6 +2280,184 @@ __global__ __launch_bounds__(kClassBlock) void class_scatter_kernel(const uint8_
     else q[kQHead + (c == CL_SMALL ? 1ull : 2ull) * n + idx] = u;
 }
 
+// ---- long units, tile-parallel encode ---------------------------------
+// A long unit's tiles (512 words) are encoded by different waves, each like a mid unit
+// (encode_tile), instead of one wave walking the unit tile by tile:
+//   long_tiles_kernel  lists every tile of every long unit in a tile table (a unit's
+//                      tiles adjacent; a unit that does not fit the table goes to the
+//                      serial list, encode_tiled_kernel's);
+//   tile_encode_kernel<kTilesSize>   per tile: the runs open at its start (the last
+//                      zero-run / literal-run break before it, read backwards from the
+//                      input: the carries encode_tiled_kernel passes from tile to tile),
+//                      the first breaks after its end (lookahead), its packed size;
+//   tile_encode_kernel<kTilesWrite>  per tile: its output offset = the unit's earlier
+//                      tiles' sizes (one wave reduction), the tile coded again and
+//                      written there; the unit's last tile writes out_len and status.
+// The table lives in the class workspace after the class lists: tile sizes (u64), units,
+// first tile of the unit; capacity n + kTileExtra tiles.
+constexpr uint64_t kTileExtra = 65536;
+constexpr uint32_t kTileSkip = 0xFFFFFFFFu;  // a table entry of a unit that went to the serial list
+struct TileTab {
+    uint64_t* size;
+    uint32_t* unit;
+    uint32_t* first;
+    uint32_t* serial;
+    uint64_t cap;
+};
+__host__ __device__ inline uint64_t class_blocks(uint64_t n) { return (n + 1023) / 1024; }  // kClassBlock
+__host__ __device__ inline uint64_t tile_tab_off(uint64_t n) {  // u32 index of the tile table (8-B aligned)
+    return (kQHead + 4 * n + 4 * class_blocks(n) + 1) & ~1ull;
+}
+__device__ __forceinline__ TileTab tile_tab(uint32_t* q, uint32_t n) {
+    TileTab t;
+    t.cap = (uint64_t)n + kTileExtra;
+    t.serial = q + kQHead + 3ull * n + 4 * class_blocks(n);
+    t.size = reinterpret_cast<uint64_t*>(q + tile_tab_off(n));
+    t.unit = q + tile_tab_off(n) + 2 * t.cap;
+    t.first = t.unit + t.cap;
+    return t;
+}
+// q[5]: serial units; q[8..9]: tiles reserved (u64); q[10]: serial take cursor
+__device__ __forceinline__ unsigned long long* q_tiles(uint32_t* q) { return reinterpret_cast<unsigned long long*>(q + 8); }
+
+__global__ __launch_bounds__(256) void long_tiles_kernel(const uint64_t* __restrict__ in_len, uint32_t n, uint32_t* q) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nh = q[2], nl = q[0];
+    if (i >= nl + nh) return;
+    const uint32_t unit = i < nh ? q[kQHead + n - 1 - i] : q[kQHead + (i - nh)];
+    const TileTab t = tile_tab(q, n);
+    const uint64_t k = ((in_len[unit] >> 3) + kEncMaxWords - 1) / kEncMaxWords;  // >= 2 tiles
+    uint64_t base = t.cap;
+    if (k <= t.cap) base = atomicAdd(q_tiles(q), (unsigned long long)k);
+    if (base + k <= t.cap) {
+        for (uint64_t j = 0; j < k; ++j) {
+            t.unit[base + j] = unit;
+            t.first[base + j] = (uint32_t)base;
+        }
+    } else {
+        for (uint64_t j = base; j < t.cap; ++j) t.unit[j] = kTileSkip;  // reserved past the end: unused
+        t.serial[atomicAdd(q + 5, 1u)] = unit;
+    }
+}
+
+// Last zero-run break (a word that is not zero) and last literal-run break (a word with a
+// zero byte) before word tb, as run starts (break + 1; 0: the run starts the unit);
+// wave-uniform results. Reads 256 words back at a time (one pass for most data).
+__device__ __forceinline__ void encode_lookback(const uint8_t* src, uint32_t tb, uint32_t lane, uint32_t& cz,
+                                                uint32_t& cf) {
+    uint32_t lz = 0, lf = 0;
+    bool fz = false, ff = false;
+    uint32_t end = tb;
+    while (end > 0 && !(fz && ff)) {  // wave-uniform
+        const uint32_t w0 = end > 256 ? end - 256 : 0;
+        uint32_t bz = 0, bf = 0;  // last break + 1 among this lane's words
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t i = w0 + 4 * lane + k;
+            if (i < end) {
+                const uint32_t tg = nonzero_tag(*reinterpret_cast<const uint64_t*>(src + 8ull * i));
+                if (tg != 0) bz = i + 1;
+                if (tg != 0xFF) bf = i + 1;
+            }
+        }
+        bz = readlane(wave_incl_max(bz, lane), kWave - 1);
+        bf = readlane(wave_incl_max(bf, lane), kWave - 1);
+        if (!fz && bz) { lz = bz; fz = true; }
+        if (!ff && bf) { lf = bf; ff = true; }
+        end = w0;
+    }
+    cz = lz;
+    cf = lf;
+}
+
+constexpr int kTilesSize = 0, kTilesWrite = 1;
+template <int PASS, bool WRITE>
+__global__ __launch_bounds__(kBlock) void tile_encode_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len, uint32_t n,
+                                                             uint8_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ out_off,
+                                                             const uint64_t* __restrict__ out_cap,
+                                                             uint64_t* __restrict__ out_len,
+                                                             int32_t* __restrict__ status, uint32_t* q) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const TileTab t = tile_tab(q, n);
+    const uint64_t T = min((uint64_t)*q_tiles(q), t.cap);
+    if ((uint64_t)blockIdx.x * kWavesPerBlock >= T) return;  // block-uniform
+    constexpr bool CODE = PASS == kTilesSize || WRITE;  // the pass codes tiles (else: totals only)
+    if (CODE && PASS == kTilesWrite) {
+        lut[threadIdx.x] = compact_selector(threadIdx.x);
+        __syncthreads();
+    }
+    uint8_t* const lds = smem + wave * kEncLds;
+    const uint64_t G = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + wave; g < T; g += G) {
+        uint32_t lane_g = lane;
+        asm volatile("" : "+v"(lane_g));  // lane-derived addresses: recomputed, not held across the loop
+        const uint32_t unit = __builtin_amdgcn_readfirstlane(t.unit[g]);
+        if (unit == kTileSkip) continue;
+        const uint64_t g0 = __builtin_amdgcn_readfirstlane(t.first[g]);
+        const uint32_t j = (uint32_t)(g - g0);
+        const uint8_t* const src = in + in_off[unit];
+        const uint32_t words = (uint32_t)(in_len[unit] >> 3);
+        const uint32_t tb = j * kEncMaxWords;
+        const uint32_t tw = min(kEncMaxWords, words - tb);
+        const uint32_t te = tb + tw;
+        const bool last = te == words;
+        uint64_t off = 0;  // the tile's output offset: the unit's earlier tiles' sizes
+        if (PASS == kTilesWrite) {
+            uint64_t acc = 0;
+            for (uint32_t b = 0; b < j; b += kWave) {
+                const uint32_t i = b + lane_g;
+                const uint64_t v = i < j ? t.size[g0 + i] : 0ull;
+                acc += v;
+            }
+            off = wave_sum64(acc);
+        }
+        uint64_t ob = 0, cap = 0;
+        if (WRITE) {
+            ob = out_off[unit];
+            cap = out_cap[unit];
+        }
+        if (!CODE) {  // encoded-size pass: the last tile reports the unit's total
+            if (last && lane_g == 0) {
+                out_len[unit] = off + t.size[g];
+                status[unit] = ST_OK;
+            }
+            continue;
+        }
+        uint4 v[5];
+        encode_load(v, src + 8ull * tb, tw, lane_g);
+        uint32_t cz = 0, cf = 0;
+        if (tb > 0) encode_lookback(src, tb, lane_g, cz, cf);
+        uint32_t nbz = words, nbf = words;
+        if (!last) {
+            const uint32_t la = min(256u, words - te);
+            uint32_t bz, bf;
+            encode_lookahead(src + 8ull * te, la, lane_g, bz, bf);
+            nbz = bz < la ? te + bz : (la == 256u ? te + 256u : words);
+            nbf = bf < la ? te + bf : (la == 256u ? te + 256u : words);
+        }
+        wave_lds_sync();  // the previous tile's write-back read the slice
+        encode_put(lds, v, (uint32_t)(reinterpret_cast<uintptr_t>(src + 8ull * tb) & 15), tw, lane_g);
+        wave_lds_sync();
+        if (PASS == kTilesSize) {
+            const uint32_t P = encode_tile<false, false>(lds, lut, lane_g, tw, tb, cz, cf, nbz, nbf, nullptr, 0);
+            if (lane_g == 0) t.size[g] = P;
+        } else {
+            const uint64_t room = off <= cap ? cap - off : 0;
+            const uint32_t P = encode_tile<true, false>(lds, lut, lane_g, tw, tb, cz, cf, nbz, nbf, out + ob + off, room);
+            if (last && lane_g == 0) {
+                out_len[unit] = off + P;
+                status[unit] = off + P > cap ? ST_SPACE : ST_OK;
+            }
+        }
+    }
+}
+
 // ---- small units, lane per unit -----------------------------------------------------------
 // A persistent grid: each wave owns a contiguous range of the small list and its lanes
 // take the range's next unit as they finish (a wave-uniform cursor, as in
@@ -3236,7 +3459,8 @@ static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
 
 size_t queue_bytes(uint32_t n) {
     const size_t nb = ((size_t)n + kClassBlock - 1) / kClassBlock;
-    return (kQHead + 3 * (size_t)n + kClassK * nb) * sizeof(uint32_t);
+    (void)nb;
+    return (tile_tab_off(n) + 4 * ((uint64_t)n + kTileExtra)) * sizeof(uint32_t);  // lists, serial list, tile table
 }
 
 // Resident blocks of a kernel across the device (hipOccupancy...), for persistent grids.
@@ -3372,7 +3596,13 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     if (e != hipSuccess) return e;
     const hipStream_t ss = side.stream();
     const uint32_t* const mid = q + kQHead + 2ull * n;
+    static const uint32_t tiles_res = resident_blocks(tile_encode_kernel<kTilesWrite, true>, kBlock, 4);
+    long_tiles_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
     if (write) {
+        tile_encode_kernel<kTilesSize, true><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
+                                                                             out_cap, out_len, status, q);
+        tile_encode_kernel<kTilesWrite, true><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
+                                                                              out_cap, out_len, status, q);
         encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, q);
         encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
@@ -3380,6 +3610,10 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
         encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                                 status, mid, q + 4);
     } else {
+        tile_encode_kernel<kTilesSize, false><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
+                                                                              out_cap, out_len, status, q);
+        tile_encode_kernel<kTilesWrite, false><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
+                                                                               out_cap, out_len, status, q);
         encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status, q);
         encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
