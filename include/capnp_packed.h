@@ -125,8 +125,10 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
  * per-unit results are in d_status / d_out_len. A unit whose status is an error
  * has unspecified slot contents (the reference returns no output for it).
  *
- * Workspace: encode / encoded_size / decode batches need a long-unit queue of
- * capnp_packed_batch_workspace_bytes(n) bytes (4 B per unit + 16). The plain calls
+ * Workspace: encode / encoded_size / decode batches need a class workspace of
+ * capnp_packed_batch_workspace_bytes(n) bytes (~32 B per unit + 1 MiB: the small / mid /
+ * long unit lists, the per-block class counts, and the long-unit tile table of n + 65536
+ * tiles that the tile-parallel long-unit encoder uses). The plain calls
  * use a queue the library keeps per caller stream (made or grown on a batch larger
  * than any earlier one on that stream; growing is refused with DEVICE_ERROR inside
  * a hipGraph capture, and an old queue is never freed, so graphs that captured it

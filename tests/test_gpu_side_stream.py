@@ -194,3 +194,32 @@ def test_workspace_too_small_is_rejected():
     ws = cp.workspace(10, device=DEV)
     with pytest.raises(cp.InvalidArgument):
         b.run(ws=ws)
+
+
+def test_tile_table_overflow_goes_serial():
+    # Long-unit encode is tile-parallel through a tile table of n + 65536 tiles
+    # (long_tiles_kernel). Three units of 30000 tiles (123 MB each) need 90000 > 65539:
+    # the unit whose reservation does not fit is encoded by the serial tiled kernel
+    # instead. Both paths must give the oracle's bytes.
+    words = 30000 * 512
+    b = Batch(np.array([words * 8, 4096 * 3 + 8, words * 8, words * 8], dtype=np.int64), seed=0xC0DE0601)
+    b.run()
+    torch.cuda.synchronize()
+    b.check_roundtrip()
+    b.check_oracle(range(4))
+    # the encoded-size pass over the same tiles
+    plen2 = torch.zeros_like(b.plen)
+    st2 = torch.full_like(b.pst, -1)
+    cp.encoded_size_batch(b.d_in, b.in_off, b.sizes, plen2, st2)
+    torch.cuda.synchronize()
+    assert (st2 == 0).all().item() and torch.equal(plen2, b.plen)
+
+
+def test_few_large_units():
+    # a batch of a few large units gets up to a wave per unit (round 1 sized the
+    # long-unit grids by unit count / 256: a handful of waves for the whole batch)
+    b = Batch(np.full(8, 262144, dtype=np.int64), seed=0xC0DE0701)
+    b.run()
+    torch.cuda.synchronize()
+    b.check_roundtrip()
+    b.check_oracle(range(8))
