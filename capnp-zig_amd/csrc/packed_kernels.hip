@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -711,34 +712,18 @@ __device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t of
            (len >> 3) <= 0xFFFFF000ull;
 }
 
-// Long-unit work queue (device memory, filled by the class kernels below) for a batch
-// of n units: q[0] = long units listed, q[1] = next entry to take, q[2] = huge units
-// listed (more than kQHuge bytes in); the long units at q[kQHead ..] upwards, the huge
-// ones from q[kQHead + n - 1] downwards. A worker wave
-// takes entries one at a time (a lane-0 vector atomic), huge units first, so the
-// units that set the tail start first and the rest spread over every worker wave.
+// Long-unit lists (device memory, filled by the class kernels below) for a batch of n
+// units: q[0] = long units listed, q[2] = huge units listed (more than kQHuge bytes in);
+// the long units at q[kQHead ..] upwards, the huge ones from q[kQHead + n - 1] downwards.
+// long_tiles_kernel / long_windows_kernel turn them into the tile / window tables (huge
+// units first) and the serial list of units the table could not hold.
 constexpr uint64_t kQHuge = 65536;
 constexpr uint32_t kQHead = 16;
-__device__ __forceinline__ uint32_t queue_listed(const uint32_t* q) { return q[0] + q[2]; }
-__device__ __forceinline__ bool queue_take(uint32_t* q, uint32_t n, uint32_t lane, uint32_t& unit) {
-    uint32_t i = 0;
-    if (lane == 0) i = atomicAdd(q + 1, 1u);
-    i = (uint32_t)__shfl((int)i, 0, kWave);
-    const uint32_t nh = q[2];
-    if (i < nh) {
-        unit = q[kQHead + n - 1 - i];
-        return true;
-    }
-    if (i - nh >= q[0]) return false;
-    unit = q[kQHead + i - nh];
-    return true;
-}
-
 __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
                                                  uint64_t out_off, uint64_t cap);
 
-// Units longer than one tile (encode_tiled_unit), taken from the long-unit queue
-// and encoded one after another, tile by tile.
+// Units longer than one tile (encode_tiled_unit) that the tile table could not hold,
+// taken from the serial list and encoded one after another, tile by tile.
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __restrict__ in,
                                                               const uint64_t* __restrict__ in_off,
@@ -1368,9 +1353,187 @@ __device__ __forceinline__ uint64_t gload_u64_unaligned(const uint8_t* p) {
 }
 
 
-// SEL: kWvMarked the units a first pass marked
-// kStNeedFull; kWvLong the units decode_long_unit selects (the indexed decoder's
-// fallback, which owns them from the start and may run beside passes 1 and 2).
+// A window of a unit's packed bytes staged in the wave's LDS slice: window byte r (unit
+// byte X + r) at pk[sh + r] for r < nload. Records starting in [0, Pw) belong to the
+// window; nload adds the <= 9 bytes such a record reaches past Pw.
+struct WvWin {
+    const uint8_t* g;  // unit byte X
+    uint32_t sh;       // g & 15
+    uint32_t rem;      // unit bytes from X on (clamped to 2^31 - 1)
+    uint32_t Pw;       // window bytes
+    uint32_t nload;    // staged bytes
+};
+
+// Stage window [X, X + kWvWin) of a unit of P packed bytes and clear its marks.
+__device__ __forceinline__ WvWin wv_stage(uint8_t* pk, uint8_t* mk, const uint8_t* src, uint64_t P, uint64_t X,
+                                          uint32_t lane) {
+    WvWin w;
+    const uint64_t rem64 = P - X;
+    w.rem = rem64 > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)rem64;
+    w.Pw = min(w.rem, kWvWin);
+    w.nload = min(w.rem, w.Pw + 16);
+    w.g = src + X;
+    w.sh = (uint32_t)(reinterpret_cast<uintptr_t>(w.g) & 15);
+    wave_lds_sync();
+    stage_linear<kWvStageK>(pk, w.g - w.sh, (w.sh + w.nload + 15) >> 4, lane);
+    for (uint32_t i = lane * 16; i < w.Pw; i += 16 * kWave) *reinterpret_cast<uint4*>(mk + i) = make_uint4(0, 0, 0, 0);
+    wave_lds_sync();
+    return w;
+}
+
+// The record chain through a staged window whose first record starts at window byte d0
+// (lane 0's entry, exact). Lane j owns the chunk [cs, ce); on return `ent` is the verified
+// record start where the chain enters it, and the result is the window's exit: the first
+// record start at or past Pw (window-relative), or kEOFX when a record runs past the
+// unit's end (walks A and B and the verification rounds: see above).
+__device__ __forceinline__ uint32_t wv_resolve(const uint8_t* pk, uint8_t* mk, const WvWin& w, uint32_t d0,
+                                               uint32_t lane, uint32_t& ent, uint32_t& cs, uint32_t& ce) {
+    const uint32_t C = max(kWvCmin, (w.Pw + 63) >> 6);
+    cs = min(lane * C, w.Pw);
+    ce = min(cs + C, w.Pw);
+
+    // ---- walk A: lane 0 from d0, every other lane from its chunk start (a guess) -----
+    const uint32_t a0 = lane == 0 ? d0 : cs;
+    uint32_t hit;
+    const uint32_t e1 = wv_walk(pk, mk, w.sh, w.rem, a0, ce, 1, hit);
+    uint32_t e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0, e7 = 0;
+
+    // ---- walk B: enter where the left neighbour's walk A left off ---------------------
+    // An entry far past the chunk start (a misread FF run, or a misread record running
+    // past the input end) would only pass through; keep walk A's guess.
+    ent = __shfl_up(e1, 1, kWave);
+    if (lane == 0) ent = d0;
+    else if (ent > cs + kWvSlack) ent = cs;
+    uint32_t ex = e1;
+    if (ent != a0) {
+        ex = wv_walk(pk, mk, w.sh, w.rem, ent, ce, 2, hit);
+        if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
+        e2 = ex;
+    }
+
+    // ---- verification rounds ------------------------------------------------------------
+    // Lanes before the first disagreeing lane f are verified. A disagreeing lane re-walks
+    // from its neighbour's exit when that neighbour is verified (lane f), or when the
+    // neighbour agrees with ITS neighbour this round and the exit is a plausible entry
+    // (<= kWvSlack into the chunk): far or EOF exits adopted from an unverified neighbour
+    // would otherwise ripple one lane per round.
+    uint32_t nid = 3;
+    for (;;) {
+        uint32_t prev = __shfl_up(ex, 1, kWave);
+        if (lane == 0) prev = d0;
+        const bool bad = ent != prev;
+        const uint64_t bm = __ballot(bad);
+        if (!bm) break;
+        const uint32_t f = (uint32_t)__builtin_ctzll(bm);
+        const bool left_bad = lane > 0 && ((bm >> (lane - 1)) & 1);
+        if (bad && (lane == f || (!left_bad && prev <= cs + kWvSlack))) {
+            ent = prev;
+            const uint32_t id = nid <= 7 ? nid : 0;
+            ex = wv_walk(pk, mk, w.sh, w.rem, ent, ce, id, hit);
+            if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
+            e3 = (id == 3) ? ex : e3;
+            e4 = (id == 4) ? ex : e4;
+            e5 = (id == 5) ? ex : e5;
+            e6 = (id == 6) ? ex : e6;
+            e7 = (id == 7) ? ex : e7;
+            ++nid;
+        }
+    }
+    return readlane(ex, kWave - 1);
+}
+
+// Output words of a lane's verified records [ent, ce).
+__device__ __forceinline__ uint32_t wv_count(const uint8_t* pk, uint32_t sh, uint32_t ent, uint32_t ce) {
+    uint32_t words = 0;
+    for (uint32_t r = ent; r < ce;) {
+        uint32_t t = pk[sh + r];
+        uint32_t b1 = pk[sh + r + 1];
+        uint32_t c9 = pk[sh + r + 9];
+        asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+        words += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+        r += wv_len(t, c9);
+    }
+    return words;
+}
+
+// Expand the window's verified records into o[0 .. total): lane records produce words
+// [wbeg, wend). Passes of kWvList output words:
+//   list:   each lane walks its verified records once more and writes, for every output
+//           word of the pass that its records produce, a 16-bit source code into a list
+//           in LDS (the mark array, dead by now): code = q (window position of a tag;
+//           word = perm(bytes q+1..q+8, lut[byte q])) or kLit | (s - 1) (literal word at
+//           bytes s..s+7); zero-run words keep the kZero code the list is reset to;
+//   expand: lane i turns list entry i into its word and stores it, so every store
+//           instruction writes 64 consecutive output words (512 B).
+__device__ __forceinline__ void wv_expand(const uint8_t* pk, uint8_t* mk, const uint64_t* lut, const WvWin& w,
+                                          uint32_t ent, uint32_t ce, uint32_t wbeg, uint32_t wend, uint32_t total,
+                                          uint64_t* o, uint32_t lane) {
+    const uint32_t sh = w.sh;
+    uint16_t* const list = reinterpret_cast<uint16_t*>(mk);
+    for (uint32_t W0 = 0; W0 < total; W0 += kWvList) {
+        const uint32_t W1 = min(total, W0 + kWvList);
+        wave_lds_sync();
+        for (uint32_t i = lane * 8; i < kWvList; i += 8 * kWave)
+            *reinterpret_cast<uint4*>(list + i) = make_uint4(kZero2, kZero2, kZero2, kZero2);
+        wave_lds_sync();
+        uint32_t pn = 0, ps = 0, pw = 0;  // long literal run handed to the wave
+        if (wbeg < W1 && wend > W0) {
+            uint32_t wo = wbeg;
+            for (uint32_t r = ent; r < ce && wo < W1;) {
+                uint32_t t = pk[sh + r];
+                uint32_t b1 = pk[sh + r + 1];
+                uint32_t c9 = pk[sh + r + 9];
+                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                const bool z = t == 0, f = t == 0xFFu;
+                if (!z && wo >= W0) list[wo - W0] = (uint16_t)r;
+                if (f && c9) {  // literal words r+10 .. r+10+8c
+                    if (c9 <= kWvExtLane || pn != 0) {  // one long run per lane goes to the wave
+                        for (uint32_t i = 0; i < c9; ++i) {
+                            const uint32_t wi = wo + 1 + i;
+                            if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (r + 9 + 8 * i));
+                        }
+                    } else {
+                        pn = c9;
+                        ps = r + 9;
+                        pw = wo + 1;
+                    }
+                }
+                wo += 1u + (z ? b1 : 0u) + (f ? c9 : 0u);
+                r += wv_len(t, c9);
+            }
+        }
+        uint64_t pm = __ballot(pn != 0);
+        while (pm) {  // long literal runs: the whole wave fills their entries
+            const uint32_t l = (uint32_t)__builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t nn = readlane(pn, l), ss = readlane(ps, l), ww = readlane(pw, l);
+            for (uint32_t i = lane; i < nn; i += kWave) {
+                const uint32_t wi = ww + i;
+                if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (ss + 8 * i));
+            }
+        }
+        wave_lds_sync();
+        for (uint32_t i = W0 + lane; i < W1; i += kWave) {
+            const uint32_t code = list[i - W0];
+            const uint32_t q = code & kPosMask;
+            const bool lit = (code & kLit) != 0;
+            uint64_t word = 0;
+            if (!(code & kZero)) {
+                if (!lit || q + 9 <= w.nload) {  // a tag's bytes are always staged
+                    const uint32_t t = lit ? 0xFFu : pk[sh + q];
+                    word = perm64(lds_u64_at(pk, sh + q + 1), lut[t]);
+                } else {  // literal word past the staged bytes (long FF run), inside the input
+                    word = gload_u64_unaligned(w.g + q + 1);
+                }
+            }
+            __builtin_nontemporal_store(word, o + i);  // streaming output (as the fill pass)
+        }
+    }
+}
+
+// SEL: kWvMarked the units a first pass marked kStNeedFull (the read-message passes);
+// kWvLong the long units the window table could not hold (the serial list that
+// long_windows_kernel fills), one after another.
 constexpr int kWvMarked = 1, kWvLong = 2;
 
 template <int SEL>
@@ -1385,23 +1548,20 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
     __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
     __shared__ uint64_t lut[256];  // tag -> v_perm selector that scatters the packed bytes (FF: identity, 00: zero)
+    constexpr bool CK = SEL == kWvMarked;
+    const bool QD = SEL == kWvLong;
+    if (QD && q[5] == 0) return;  // no serial units (block-uniform)
     lut[threadIdx.x] = expand_selector(threadIdx.x);
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* pk = pk_all + wave * kWvPk;
     uint8_t* mk = mk_all + wave * kWvWin;
-    // CK: a first pass (decode_index_kernel / decode_ckpt_kernel) ran; this kernel
-    // then takes only the units it marked kStNeedFull, with a small grid striding
-    // over the batch (every other status is final or the fill pass's).
-    // The wave tests 64 statuses per load (CK) and walks the marked units in order.
-    // kWvLong: the units come from the long-unit queue (queue_take), one at a time.
-    constexpr bool CK = SEL == kWvMarked;
-    const bool QD = SEL == kWvLong;
-    if (QD && queue_listed(q) == 0) return;  // no long units
-    const uint32_t stride = QD ? 0u : CK ? gridDim.x * kWvWaves * kWave : gridDim.x * kWvWaves;
-    for (uint32_t ubase = QD ? 0u : CK ? (blockIdx.x * kWvWaves + wave) * kWave : blockIdx.x * kWvWaves + wave;
-         ubase < n; ubase += stride) {
+    // CK: a first pass ran; this kernel takes only the units it marked kStNeedFull, with a
+    // small grid striding over the batch (64 statuses per load). QD: units from the serial list.
+    const uint32_t* const serial = q + kQHead + 3ull * n + 4 * ((n + 1023) / 1024);
+    const uint32_t stride = QD ? 0u : gridDim.x * kWvWaves * kWave;
+    for (uint32_t ubase = QD ? 0u : (blockIdx.x * kWvWaves + wave) * kWave; ubase < n; ubase += stride) {
     uint64_t todo = 1;
     if (CK) {
         const uint32_t u = ubase + lane;
@@ -1410,7 +1570,11 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     while (todo) {  // wave-uniform
     uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : ubase;
     if (QD) {
-        if (!queue_take(q, n, lane, unit)) return;  // todo stays set: the next entry
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(q + 10, 1u);
+        i = __builtin_amdgcn_readfirstlane(i);
+        if (i >= q[5]) return;
+        unit = serial[i];
     } else {
         todo &= todo - 1;
     }
@@ -1432,168 +1596,18 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     int32_t st = ST_OK;
     bool fits = true;
     while (X < P) {
-        const uint64_t rem64 = P - X;
-        const uint32_t rem = rem64 > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)rem64;
-        const uint32_t Pw = min(rem, kWvWin);
-        const uint32_t nload = min(rem, Pw + 16);  // records starting in the window end <= 9 B past it
-        const uint8_t* g = src + X;
-        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15);
-
-        // ---- stage the window (pk[sh + r] = byte r) and clear the marks ------------
-        wave_lds_sync();
-        stage_linear<kWvStageK>(pk, g - sh, (sh + nload + 15) >> 4, lane);
-        for (uint32_t i = lane * 16; i < Pw; i += 16 * kWave) *reinterpret_cast<uint4*>(mk + i) = make_uint4(0, 0, 0, 0);
-        wave_lds_sync();
-
-        uint32_t cs, ce, ent, wbeg, wend, total, xw;
-        {
-
-        const uint32_t C = max(kWvCmin, (Pw + 63) >> 6);
-        cs = min(lane * C, Pw);
-        ce = min(cs + C, Pw);
-
-        // ---- walk A: guess "the chain enters at the chunk start" --------------------
-        uint32_t hit;
-        const uint32_t e1 = wv_walk(pk, mk, sh, rem, cs, ce, 1, hit);
-        uint32_t e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0, e7 = 0;
-
-        // ---- walk B: enter where the left neighbour's walk A left off ---------------
-        // An entry far past the chunk start (a misread FF run, or a misread record
-        // running past the input end) would only pass through; keep walk A's guess.
-        ent = __shfl_up(e1, 1, kWave);
-        if (lane == 0) ent = 0;
-        if (ent > cs + kWvSlack) ent = cs;
-        uint32_t ex = e1;
-        if (ent != cs) {
-            ex = wv_walk(pk, mk, sh, rem, ent, ce, 2, hit);
-            if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
-            e2 = ex;
-        }
-
-        // ---- verification rounds ------------------------------------------------------
-        // Lanes before the first disagreeing lane f are verified. A disagreeing lane
-        // re-walks from its neighbour's exit when that neighbour is verified (lane f),
-        // or when the neighbour agrees with ITS neighbour this round and the exit is a
-        // plausible entry (<= kWvSlack into the chunk): far or EOF exits adopted from
-        // an unverified neighbour would otherwise ripple one lane per round.
-        uint32_t nid = 3;
-        for (;;) {
-            uint32_t prev = __shfl_up(ex, 1, kWave);
-            if (lane == 0) prev = 0;
-            const bool bad = ent != prev;
-            const uint64_t bm = __ballot(bad);
-            if (!bm) break;
-            const uint32_t f = (uint32_t)__builtin_ctzll(bm);
-            const bool left_bad = lane > 0 && ((bm >> (lane - 1)) & 1);
-            if (bad && (lane == f || (!left_bad && prev <= cs + kWvSlack))) {
-                ent = prev;
-                const uint32_t id = nid <= 7 ? nid : 0;
-                ex = wv_walk(pk, mk, sh, rem, ent, ce, id, hit);
-                if (hit) ex = wv_sel_exit(hit, e1, e2, e3, e4, e5, e6, e7);
-                e3 = (id == 3) ? ex : e3;
-                e4 = (id == 4) ? ex : e4;
-                e5 = (id == 5) ? ex : e5;
-                e6 = (id == 6) ? ex : e6;
-                e7 = (id == 7) ? ex : e7;
-                ++nid;
-            }
-        }
-        xw = readlane(ex, kWave - 1);  // window exit = next window start
+        const WvWin w = wv_stage(pk, mk, src, P, X, lane);
+        uint32_t ent, cs, ce;
+        const uint32_t xw = wv_resolve(pk, mk, w, 0, lane, ent, cs, ce);
         if (xw == kEOFX) {
             st = ST_EOF;
             break;
         }
-
-        // ---- count output words of the verified records ------------------------------
-        uint32_t words = 0;
-        for (uint32_t r = ent; r < ce;) {
-            uint32_t t = pk[sh + r];
-            uint32_t b1 = pk[sh + r + 1];
-            uint32_t c9 = pk[sh + r + 9];
-            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-            words += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
-            r += wv_len(t, c9);
-        }
+        const uint32_t words = wv_count(pk, w.sh, ent, ce);
         const uint32_t incl = wave_incl_sum(words, lane);
-        total = readlane(incl, kWave - 1);
+        const uint32_t total = readlane(incl, kWave - 1);
         if (Wb + total > capw) fits = false;
-        wbeg = incl - words;
-        wend = incl;
-        }
-
-        // ---- expand, by output word ---------------------------------------------------
-        // Output words are produced in passes of kWvList words [W0, W0 + kWvList).
-        // fill:   each lane walks its verified records once more and writes, for
-        //         every output word of the pass that its records produce, a 16-bit
-        //         source code into a list in LDS (the mark array, dead by now):
-        //         code = q (window position of a tag; word = perm(bytes q+1..q+8,
-        //         lut[byte q])) or kLit | (s - 1) (literal word at bytes s..s+7);
-        //         zero-run words keep the kZero code the list is reset to.
-        // expand: lane i turns list entry i into its word and stores it, so every
-        //         store instruction writes 64 consecutive output words (512 B).
-        if (fits) {
-            uint16_t* const list = reinterpret_cast<uint16_t*>(mk);
-            uint64_t* const o = dst + Wb;
-            for (uint32_t W0 = 0; W0 < total; W0 += kWvList) {
-                const uint32_t W1 = min(total, W0 + kWvList);
-                wave_lds_sync();
-                for (uint32_t i = lane * 8; i < kWvList; i += 8 * kWave)
-                    *reinterpret_cast<uint4*>(list + i) = make_uint4(kZero2, kZero2, kZero2, kZero2);
-                wave_lds_sync();
-                uint32_t pn = 0, ps = 0, pw = 0;  // long literal run handed to the wave
-                if (wbeg < W1 && wend > W0) {
-                    uint32_t w = wbeg;
-                    for (uint32_t r = ent; r < ce && w < W1;) {
-                        uint32_t t = pk[sh + r];
-                        uint32_t b1 = pk[sh + r + 1];
-                        uint32_t c9 = pk[sh + r + 9];
-                        asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                        const bool z = t == 0, f = t == 0xFFu;
-                        if (!z && w >= W0) list[w - W0] = (uint16_t)r;
-                        if (f && c9) {  // literal words r+10 .. r+10+8c
-                            if (c9 <= kWvExtLane || pn != 0) {  // one long run per lane goes to the wave
-                                for (uint32_t i = 0; i < c9; ++i) {
-                                    const uint32_t wi = w + 1 + i;
-                                    if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (r + 9 + 8 * i));
-                                }
-                            } else {
-                                pn = c9;
-                                ps = r + 9;
-                                pw = w + 1;
-                            }
-                        }
-                        w += 1u + (z ? b1 : 0u) + (f ? c9 : 0u);
-                        r += wv_len(t, c9);
-                    }
-                }
-                uint64_t pm = __ballot(pn != 0);
-                while (pm) {  // long literal runs: the whole wave fills their entries
-                    const uint32_t l = (uint32_t)__builtin_ctzll(pm);
-                    pm &= pm - 1;
-                    const uint32_t nn = readlane(pn, l), ss = readlane(ps, l), ww = readlane(pw, l);
-                    for (uint32_t i = lane; i < nn; i += kWave) {
-                        const uint32_t wi = ww + i;
-                        if (wi >= W0 && wi < W1) list[wi - W0] = (uint16_t)(kLit | (ss + 8 * i));
-                    }
-                }
-                wave_lds_sync();
-                for (uint32_t i = W0 + lane; i < W1; i += kWave) {
-                    const uint32_t code = list[i - W0];
-                    const uint32_t q = code & kPosMask;
-                    const bool lit = (code & kLit) != 0;
-                    uint64_t word = 0;
-                    if (!(code & kZero)) {
-                        if (!lit || q + 9 <= nload) {  // a tag's bytes are always staged
-                            const uint32_t t = lit ? 0xFFu : pk[sh + q];
-                            word = perm64(lds_u64_at(pk, sh + q + 1), lut[t]);
-                        } else {  // literal word past the staged bytes (long FF run), inside the input
-                            word = gload_u64_unaligned(g + q + 1);
-                        }
-                    }
-                    __builtin_nontemporal_store(word, o + i);  // streaming output (as the fill pass)
-                }
-            }
-        }
+        if (fits) wv_expand(pk, mk, lut, w, ent, ce, incl - words, incl, total, dst + Wb, lane);
         Wb += total;
         X += xw;
     }
@@ -2158,7 +2172,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 //          (encode_tiled_kernel / decode_wave_kernel<kWvLong>), on the side stream.
 // Workspace q (queue_bytes(n)): q[0] long, q[1] take cursor, q[2] huge, q[3] small and
 // q[4] mid counts; the long list at q[kQHead ..] upwards and the huge list from
-// q[kQHead + n - 1] downwards (queue_take), the small list at q[kQHead + n ..], the mid
+// q[kQHead + n - 1] downwards, the small list at q[kQHead + n ..], the mid
 // list at q[kQHead + 2n ..], then kClassK counts per class block. Count, scan, scatter:
 // each list keeps batch order, and no atomic is contended.
 constexpr uint32_t kClassBlock = 1024;
@@ -2455,6 +2469,301 @@ __global__ __launch_bounds__(kBlock) void tile_encode_kernel(const uint8_t* __re
                 status[unit] = off + P > cap ? ST_SPACE : ST_OK;
             }
         }
+    }
+}
+
+// ---- long units, window-parallel decode ------------------------------
+// A long unit's packed bytes are cut into windows of kWvWin bytes at fixed positions
+// X_j = j * kWvWin, and every window is a wave's work, instead of one wave walking the
+// unit window after window. Where the record chain enters window j is only known once
+// window j-1 is resolved, so:
+//   long_windows_kernel   lists every window of every long unit in a window table (a
+//                         unit's windows adjacent; units that do not fit go to the serial
+//                         list, decode_wave_kernel<kWvLong>'s);
+//   window_spec_kernel    per window: the chain as if a record started at X_j (walk A/B
+//                         and the verification rounds of wv_resolve), its exit and word
+//                         count; then, for every possible entry d < kWinD, a walk from d
+//                         until it meets a verified record start of lanes 0/1 (chains
+//                         couple within a few records): from there its records are the
+//                         verified chain's, so the words from entry d are the window's
+//                         count plus delta[d];
+//   window_resolve_kernel per unit (a wave, serial over its windows but table lookups
+//                         only): entry d_0 = 0, d_{j+1} = X_j + exit_j - X_{j+1}, words_j =
+//                         total_j + delta_j[d_j]; an entry the spec pass could not resolve
+//                         (an FF record landing >= kWinD bytes in, or no coupling within
+//                         lanes 0/1) is resolved by staging that window again. It writes
+//                         each window's entry and output offset, and the unit's out_len and
+//                         status BEFORE any output exists: a truncated or oversized unit
+//                         writes nothing (message.zig:90 errors before producing output);
+//   window_fill_kernel    per window of an OK unit: the chain from its exact entry, the
+//                         code list and the expansion (wv_expand) at its output offset.
+// The table shares the class workspace's tile-table region (encode's); capacity
+// n / 8 + kWinExtra windows (4.6 KB each).
+constexpr uint64_t kWinExtra = 32768;
+constexpr uint32_t kWinNone = 0xFFFFFFFFu;  // window entry: nothing to expand
+constexpr int16_t kDeltaEof = -32768;       // delta: the chain from this entry runs past the unit's end
+constexpr uint32_t kWinD = 64;              // entries the spec pass resolves (window bytes 0 .. 63)
+constexpr uint32_t kWinBatch = 32;          // windows whose tables a resolve wave holds at once
+struct WinEnt {
+    uint32_t unit, first;  // the unit (kTileSkip: none); table index of its first window
+    uint32_t exit, total;  // spec pass: exit (window-relative, kEOFX) and words from entry 0
+    uint64_t valid;        // spec pass: bit d = delta[d] holds the words from entry d
+    uint32_t ent, pad;     // resolve pass: the verified entry (window-relative) or kWinNone
+    uint64_t wb;           // resolve pass: output words before the window
+    uint64_t pad2;
+    int16_t delta[kWinD];  // spec pass: words from entry d - total (kDeltaEof: truncated)
+};
+static_assert(sizeof(WinEnt) == 176, "window table entry");
+__host__ __device__ inline uint64_t win_tab_off(uint64_t n) { return (tile_tab_off(n) + 3) & ~3ull; }  // 16-B aligned
+__host__ __device__ inline uint64_t win_cap(uint64_t n) { return n / 8 + kWinExtra; }
+__device__ __forceinline__ WinEnt* win_tab(uint32_t* q, uint32_t n) {
+    return reinterpret_cast<WinEnt*>(q + win_tab_off(n));
+}
+
+__global__ __launch_bounds__(256) void long_windows_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
+                                                           uint32_t* q) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nh = q[2], nl = q[0];
+    if (i >= nl + nh) return;
+    const uint32_t unit = i < nh ? q[kQHead + n - 1 - i] : q[kQHead + (i - nh)];
+    WinEnt* const e = win_tab(q, n);
+    const uint64_t cap = win_cap(n);
+    const uint64_t k = (in_len[unit] + kWvWin - 1) / kWvWin;  // >= 1 (P > 0)
+    uint64_t base = cap;
+    if (k <= cap) base = atomicAdd(q_tiles(q), (unsigned long long)k);
+    if (base + k <= cap) {
+        for (uint64_t j = 0; j < k; ++j) {
+            e[base + j].unit = unit;
+            e[base + j].first = (uint32_t)base;
+        }
+    } else {
+        for (uint64_t j = base; j < cap; ++j) e[j].unit = kTileSkip;  // reserved past the end: unused
+        q[kQHead + 3ull * n + 4 * class_blocks(n) + atomicAdd(q + 5, 1u)] = unit;  // the serial list
+    }
+}
+
+__global__ __launch_bounds__(kWvBlock) void window_spec_kernel(const uint8_t* __restrict__ in,
+                                                               const uint64_t* __restrict__ in_off,
+                                                               const uint64_t* __restrict__ in_len, uint32_t n,
+                                                               uint32_t* q) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
+    __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
+    const uint64_t T = min((uint64_t)*q_tiles(q), win_cap(n));
+    if ((uint64_t)blockIdx.x * kWvWaves >= T) return;  // block-uniform
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const pk = pk_all + wave * kWvPk;
+    uint8_t* const mk = mk_all + wave * kWvWin;
+    WinEnt* const tab = win_tab(q, n);
+    const uint64_t G = (uint64_t)gridDim.x * kWvWaves;
+    for (uint64_t g = (uint64_t)blockIdx.x * kWvWaves + wave; g < T; g += G) {
+        WinEnt* const e = tab + g;
+        const uint32_t unit = __builtin_amdgcn_readfirstlane(e->unit);
+        if (unit == kTileSkip) continue;
+        const uint64_t X = (g - __builtin_amdgcn_readfirstlane(e->first)) * (uint64_t)kWvWin;
+        const WvWin w = wv_stage(pk, mk, in + in_off[unit], in_len[unit], X, lane);
+        uint32_t ent, cs, ce;
+        const uint32_t xw = wv_resolve(pk, mk, w, 0, lane, ent, cs, ce);
+        const uint32_t words = wv_count(pk, w.sh, ent, ce);
+        const uint32_t incl = wave_incl_sum(words, lane);
+        const uint32_t total = readlane(incl, kWave - 1);
+        // words before each verified record start of lanes 0 and 1 (window bytes [0, lim))
+        const uint32_t lim = readlane(ce, 1);   // <= 2 * 73 bytes
+        const uint32_t x1 = readlane(ent, 2);   // where the chain leaves lane 1's chunk
+        const uint32_t w01 = readlane(incl, 1); // words of lanes 0 and 1
+        uint16_t* const pre = reinterpret_cast<uint16_t*>(mk);  // the marks are dead by now
+        wave_lds_sync();
+        for (uint32_t i = lane; i < lim; i += kWave) pre[i] = 0xFFFFu;
+        wave_lds_sync();
+        if (lane < 2) {
+            uint32_t ws = incl - words;
+            for (uint32_t r = ent; r < ce;) {
+                uint32_t t = pk[w.sh + r];
+                uint32_t b1 = pk[w.sh + r + 1];
+                uint32_t c9 = pk[w.sh + r + 9];
+                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                pre[r] = (uint16_t)min(ws, 0xFFFEu);
+                ws += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+                r += wv_len(t, c9);
+            }
+        }
+        wave_lds_sync();
+        // entry d = lane: walk until the chain meets a verified record start
+        uint32_t r = lane, wd = 0;
+        int32_t delta = 0;
+        bool valid = false;
+        for (;;) {
+            if (r >= lim) {  // left lanes 0/1 uncoupled: valid only where the verified chain leaves
+                valid = r == x1 && x1 != kEOFX;
+                delta = (int32_t)wd - (int32_t)w01;
+                break;
+            }
+            const uint32_t p = pre[r];
+            if (p != 0xFFFFu) {
+                valid = true;
+                delta = (int32_t)wd - (int32_t)p;
+                break;
+            }
+            uint32_t t = pk[w.sh + r];
+            uint32_t b1 = pk[w.sh + r + 1];
+            uint32_t c9 = pk[w.sh + r + 9];
+            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+            const uint32_t len = wv_len(t, c9);
+            if (r + len > w.rem) {  // message.zig:152-191: the record runs past the input
+                valid = true;
+                delta = kDeltaEof;
+                break;
+            }
+            wd += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+            r += len;
+        }
+        if (delta != kDeltaEof && (delta < -32767 || delta > 32767)) valid = false;
+        const uint64_t vm = __ballot(valid);
+        e->delta[lane] = (int16_t)(valid ? delta : 0);
+        if (lane == 0) {
+            e->exit = xw;
+            e->total = total;
+            e->valid = vm;
+            e->ent = kWinNone;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWvBlock) void window_resolve_kernel(const uint8_t* __restrict__ in,
+                                                                  const uint64_t* __restrict__ in_off,
+                                                                  const uint64_t* __restrict__ in_len, uint32_t n,
+                                                                  const uint64_t* __restrict__ out_cap,
+                                                                  uint64_t* __restrict__ out_len,
+                                                                  int32_t* __restrict__ status, uint32_t* q) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
+    __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
+    __shared__ int16_t dl_all[kWvWaves][kWinBatch][kWinD];
+    const uint64_t T = min((uint64_t)*q_tiles(q), win_cap(n));
+    if ((uint64_t)blockIdx.x * kWvWaves * kWave >= T) return;  // block-uniform
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const pk = pk_all + wave * kWvPk;
+    uint8_t* const mk = mk_all + wave * kWvWin;
+    WinEnt* const tab = win_tab(q, n);
+    const uint64_t G = (uint64_t)gridDim.x * kWvWaves * kWave;
+    // waves take 64 table entries at a time and resolve the units whose first window is there
+    for (uint64_t gb = ((uint64_t)blockIdx.x * kWvWaves + wave) * kWave; gb < T; gb += G) {
+        const uint64_t gl = gb + lane;
+        bool head = false;
+        if (gl < T) {
+            const uint32_t u = tab[gl].unit;
+            head = u != kTileSkip && tab[gl].first == (uint32_t)gl;
+        }
+        uint64_t hm = __ballot(head);
+        while (hm) {  // wave-uniform
+            const uint64_t g0 = gb + (uint64_t)__builtin_ctzll(hm);
+            hm &= hm - 1;
+            const uint32_t unit = __builtin_amdgcn_readfirstlane(tab[g0].unit);
+            const uint8_t* const src = in + in_off[unit];
+            const uint64_t P = in_len[unit];
+            const uint64_t k = (P + kWvWin - 1) / kWvWin;
+            uint64_t E = 0;     // the chain's next record start (unit-relative)
+            uint64_t wacc = 0;  // output words so far
+            int32_t st = ST_OK;
+            for (uint64_t jb = 0; jb < k && st == ST_OK && E < P; jb += kWinBatch) {
+                const uint32_t kb = (uint32_t)min((uint64_t)kWinBatch, k - jb);
+                // the batch's exits, totals and valid masks (lane i: window jb + i) and deltas (LDS)
+                uint32_t hx = 0, ht = 0, hvl = 0, hvh = 0;
+                if (lane < kb) {
+                    const WinEnt* const e = tab + g0 + jb + lane;
+                    hx = e->exit;
+                    ht = e->total;
+                    const uint64_t v = e->valid;
+                    hvl = (uint32_t)v;
+                    hvh = (uint32_t)(v >> 32);
+                }
+                wave_lds_sync();
+                for (uint32_t i = 0; i < kb; ++i) dl_all[wave][i][lane] = tab[g0 + jb + i].delta[lane];
+                wave_lds_sync();
+                uint32_t rent = kWinNone;  // lane i: the resolved entry of window jb + i
+                uint64_t rwb = 0;
+                for (uint32_t i = 0; i < kb; ++i) {  // wave-uniform
+                    const uint64_t X = (jb + i) * (uint64_t)kWvWin;
+                    if (E >= P) break;  // the unit's records are all resolved (E == P)
+                    const uint32_t d = (uint32_t)(E - X);
+                    const uint64_t vv = (uint64_t)readlane(hvl, i) | ((uint64_t)readlane(hvh, i) << 32);
+                    uint32_t xw, words;
+                    if (d < kWinD && ((vv >> d) & 1)) {
+                        const int32_t dl = dl_all[wave][i][d];
+                        xw = readlane(hx, i);
+                        if (dl == kDeltaEof || xw == kEOFX) {
+                            st = ST_EOF;
+                            break;
+                        }
+                        words = (uint32_t)((int32_t)readlane(ht, i) + dl);
+                    } else {  // stage the window again and resolve it from entry d
+                        const WvWin w = wv_stage(pk, mk, src, P, X, lane);
+                        uint32_t ent, cs, ce;
+                        xw = wv_resolve(pk, mk, w, d, lane, ent, cs, ce);
+                        if (xw == kEOFX) {
+                            st = ST_EOF;
+                            break;
+                        }
+                        const uint32_t wl = wv_count(pk, w.sh, ent, ce);
+                        words = readlane(wave_incl_sum(wl, lane), kWave - 1);
+                    }
+                    if (lane == i) {
+                        rent = d;
+                        rwb = wacc;
+                    }
+                    wacc += words;
+                    E = X + xw;
+                }
+                if (lane < kb) {
+                    WinEnt* const e = tab + g0 + jb + lane;
+                    e->ent = rent;
+                    e->wb = rwb;
+                }
+            }
+            if (lane == 0) {
+                const uint64_t U = 8 * wacc;
+                out_len[unit] = st == ST_OK ? U : 0;
+                status[unit] = st != ST_OK ? st : (U > out_cap[unit] ? ST_SPACE : ST_OK);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __restrict__ in,
+                                                               const uint64_t* __restrict__ in_off,
+                                                               const uint64_t* __restrict__ in_len, uint32_t n,
+                                                               uint8_t* __restrict__ out,
+                                                               const uint64_t* __restrict__ out_off,
+                                                               const int32_t* __restrict__ status, uint32_t* q) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
+    __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
+    __shared__ uint64_t lut[256];  // tag -> v_perm selector that scatters the packed bytes
+    const uint64_t T = min((uint64_t)*q_tiles(q), win_cap(n));
+    if ((uint64_t)blockIdx.x * kWvWaves >= T) return;  // block-uniform
+    lut[threadIdx.x] = expand_selector(threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const pk = pk_all + wave * kWvPk;
+    uint8_t* const mk = mk_all + wave * kWvWin;
+    const WinEnt* const tab = win_tab(q, n);
+    const uint64_t G = (uint64_t)gridDim.x * kWvWaves;
+    for (uint64_t g = (uint64_t)blockIdx.x * kWvWaves + wave; g < T; g += G) {
+        const WinEnt* const e = tab + g;
+        const uint32_t unit = __builtin_amdgcn_readfirstlane(e->unit);
+        if (unit == kTileSkip) continue;
+        const uint32_t d = __builtin_amdgcn_readfirstlane(e->ent);
+        if (d == kWinNone || status[unit] != ST_OK) continue;  // nothing to expand, or a failed unit
+        const uint64_t X = (g - __builtin_amdgcn_readfirstlane(e->first)) * (uint64_t)kWvWin;
+        const uint64_t wb = e->wb;
+        const WvWin w = wv_stage(pk, mk, in + in_off[unit], in_len[unit], X, lane);
+        uint32_t ent, cs, ce;
+        (void)wv_resolve(pk, mk, w, d, lane, ent, cs, ce);
+        const uint32_t words = wv_count(pk, w.sh, ent, ce);
+        const uint32_t incl = wave_incl_sum(words, lane);
+        const uint32_t total = readlane(incl, kWave - 1);
+        uint64_t* const dst = reinterpret_cast<uint64_t*>(out + out_off[unit]) + wb;
+        wv_expand(pk, mk, lut, w, ent, ce, incl - words, incl, total, dst, lane);
     }
 }
 
@@ -3450,7 +3759,7 @@ struct StreamCtx {
     std::mutex mu;
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    uint32_t* q = nullptr;  // long-unit queue (queue_take): kQHead counters + qcap entries
+    uint32_t* q = nullptr;  // class workspace (queue_bytes): kQHead counters, lists, tile / window table
     uint64_t qcap = 0;
     std::vector<uint32_t*> retired;  // replaced queues (kept: graphs may reference them)
 };
@@ -3460,7 +3769,10 @@ static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
 size_t queue_bytes(uint32_t n) {
     const size_t nb = ((size_t)n + kClassBlock - 1) / kClassBlock;
     (void)nb;
-    return (tile_tab_off(n) + 4 * ((uint64_t)n + kTileExtra)) * sizeof(uint32_t);  // lists, serial list, tile table
+    // lists, serial list, then the tile table (encode) or the window table (decode)
+    const uint64_t tiles = tile_tab_off(n) * sizeof(uint32_t) + 16 * ((uint64_t)n + kTileExtra);
+    const uint64_t wins = win_tab_off(n) * sizeof(uint32_t) + sizeof(WinEnt) * win_cap(n);
+    return tiles > wins ? tiles : wins;
 }
 
 // Resident blocks of a kernel across the device (hipOccupancy...), for persistent grids.
@@ -3680,10 +3992,23 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
+    // long units, window-parallel (window table) or, if the table is full, serial
     static const uint32_t long_res = resident_blocks(decode_wave_kernel<kWvLong>, kWvBlock, 4);
+    static const uint32_t spec_res = resident_blocks(window_spec_kernel, kWvBlock, 4);
+    static const uint32_t res_res = resident_blocks(window_resolve_kernel, kWvBlock, 2);
+    static const uint32_t fill_res = resident_blocks(window_fill_kernel, kWvBlock, 4);
     const uint32_t long_blocks = min((n + kWvWaves - 1) / kWvWaves, long_res);  // up to a wave per unit
-    decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, side.stream()>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, q);
+    const uint64_t wcap = win_cap(n);
+    const uint32_t win_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, spec_res);
+    const uint32_t res_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves * kWave - 1) / (kWvWaves * kWave), res_res);
+    const uint32_t wfill_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, fill_res);
+    const hipStream_t ss = side.stream();
+    long_windows_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
+    window_spec_kernel<<<win_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, q);
+    window_resolve_kernel<<<res_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out_cap, out_len, status, q);
+    window_fill_kernel<<<wfill_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, status, q);
+    decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                   out_len, status, q);
     decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                              status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
