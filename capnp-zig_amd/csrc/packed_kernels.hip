@@ -2972,10 +2972,14 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
     }
 }
 
-// unpackPacked (message.zig:88-145) for one unit per lane: a 32-B window of the packed
-// bytes in registers (pieces wb/16, wb/16 + 1) and the next piece read each turn; a
-// turn decodes the records that start in the window's first piece. A truncated record
-// is UnexpectedEof with nothing more written (the batch contract: INTEGRATION.md §4).
+// unpackPacked (message.zig:88-145) for one unit per lane. Each lane keeps a 64-B ring of
+// its unit's packed bytes in LDS (piece p at slot p % 4). A turn codes the records that
+// start in the lane's 32-B span [16k, 16k + 32) -- one record per loop pass on every lane,
+// predicated (no per-record branches: zero-run and literal-run records take the same path
+// as the others, a literal word as if it followed an FF tag) -- while pieces k + 4 and
+// k + 5 are in flight into registers; they enter the ring at the start of the next turn.
+// A truncated record is UnexpectedEof with nothing more written.
+constexpr uint32_t kSdRing = 80;  // LDS bytes per lane: the 64-B ring + 16 B (fewer bank conflicts)
 __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len, uint32_t n,
@@ -2985,6 +2989,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
                                                                 uint64_t* __restrict__ out_len,
                                                                 int32_t* __restrict__ status, const uint32_t* q) {
     __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kSmBlock * kSdRing];
     lut[threadIdx.x] = expand_selector(threadIdx.x);
     __syncthreads();
     const uint32_t count = q[3];
@@ -2996,13 +3001,14 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
     const uint64_t first = (uint64_t)gw * per;
     const uint64_t last = min((uint64_t)count, first + per);
     uint64_t cursor = first;  // wave-uniform
+    uint8_t* const ring = ring_all + threadIdx.x * kSdRing;
 
     uint32_t kind = SM_IDLE, unit = 0;
     const uint8_t* base = in;  // 16-B aligned base of the packed unit
-    uint32_t end = 0, pos = 0, wb = 0, np = 0;  // aligned space: bytes [s, end); window base
-    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, n0 = 0, n1 = 0;
+    uint32_t end = 0, pos = 0, k = 0, np = 0, lit = 0;  // aligned space: bytes [s, end); span start piece
+    uint4 d0, d1, d2, d3;                                // pieces in flight
     uint64_t* dst = nullptr;
-    uint32_t capw = 0, wo = 0, lit = 0;
+    uint32_t capw = 0, wo = 0;
     uint64_t cap = 0;
 
     auto finish = [&](int32_t st) {
@@ -3015,19 +3021,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
         }
         kind = SM_IDLE;
     };
-    auto piece = [&](uint32_t i, uint64_t& a, uint64_t& b) {
-        if (i < np) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(base + 16ull * i);
-            a = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-            b = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
-        } else {
-            a = b = 0;
-        }
-    };
-    auto emit = [&](uint64_t w) {
-        if (wo < capw) dst[wo] = w;
-        ++wo;
-    };
+    auto ld = [&](uint32_t i) { return *reinterpret_cast<const uint4*>(base + 16ull * min(i, np - 1)); };
 
     for (;;) {
         const uint64_t idle = __ballot(kind == SM_IDLE);
@@ -3048,7 +3042,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             }
         }
         if (__ballot(kind != SM_EXIT) == 0) break;
-        // ---- this turn's read -----------------------------------------------------------
+        // ---- this turn's reads (and last turn's pieces into the ring) -------------------
         uint64_t m_off = 0, m_len = 0, m_oo = 0, m_cap = 0;
         if (kind == SM_META) {
             m_off = in_off[unit];
@@ -3056,13 +3050,26 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             m_oo = out_off[unit];
             m_cap = out_cap[unit];
         } else if (kind == SM_FIRST) {
-            piece(0, q0, q1);
-            piece(1, q2, q3);
-            piece(2, n0, n1);
+            d0 = ld(0);
+            d1 = ld(1);
+            d2 = ld(2);
+            d3 = ld(3);
         } else if (kind == SM_RUN) {
-            piece((wb >> 4) + 2, n0, n1);
+            uint4* const r4 = reinterpret_cast<uint4*>(ring);
+            if (k == 0) {
+                r4[0] = d0;
+                r4[1] = d1;
+                r4[2] = d2;
+                r4[3] = d3;
+            } else {
+                r4[(k + 2) & 3] = d0;
+                r4[(k + 3) & 3] = d1;
+            }
+            d0 = ld(k + 4);
+            d1 = ld(k + 5);
         }
-        // ---- decode ----------------------------------------------------------------------------
+        // ---- decode -------------------------------------------------------------------------
+        bool act = kind == SM_RUN;  // the lanes that code this turn
         if (kind == SM_META) {
             const uint8_t* const src = in + m_off;
             const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
@@ -3070,66 +3077,55 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             end = s + (uint32_t)m_len;  // m_len <= kSmDecP
             np = (end + 15) >> 4;
             pos = s;
-            wb = 0;
+            k = 0;
+            lit = 0;
             uint8_t* const o = out + m_oo;
             dst = reinterpret_cast<uint64_t*>(o);
             cap = m_cap;
             capw = (uint32_t)(m_cap >> 3);
             wo = 0;
-            lit = 0;
             if (reinterpret_cast<uintptr_t>(o) & 7) finish(ST_ARG);
             else if (m_len == 0) finish(ST_OK);
             else kind = SM_FIRST;
-        } else if (kind == SM_FIRST || kind == SM_RUN) {
-            const uint32_t limit = wb + 16;
-            int32_t st = ST_OK;
-            bool done = false;
-            for (uint32_t it = 0; it < 16; ++it) {
-                if (lit) {
-                    if (pos >= limit) break;
-                    emit(view_word8(q0, q1, q2, q3, pos - wb));  // an FF run's body word
-                    pos += 8;
-                    --lit;
-                    continue;
-                }
-                if (pos >= end) {
-                    done = true;
-                    break;
-                }
-                if (pos >= limit) break;
-                const uint32_t o = pos - wb;
-                const uint32_t t = view_byte(q0, q1, q2, q3, o);
-                if (t == 0x00) {  // message.zig:101-110
-                    if (pos + 2 > end) { st = ST_EOF; break; }
-                    const uint32_t c = view_byte(q0, q1, q2, q3, o + 1);
-                    const uint32_t k = min(c + 1, capw > wo ? capw - wo : 0u);
-                    for (uint32_t j = 0; j < k; ++j) dst[wo + j] = 0;
-                    wo += c + 1;
-                    pos += 2;
-                } else if (t == 0xFF) {  // message.zig:112-128
-                    if (pos + 10 > end) { st = ST_EOF; break; }
-                    const uint32_t c = view_byte(q0, q1, q2, q3, o + 9);
-                    if (pos + 10 + 8 * c > end) { st = ST_EOF; break; }
-                    emit(view_word8(q0, q1, q2, q3, o + 1));
-                    lit = c;
-                    pos += 10;
-                } else {  // message.zig:131-141
-                    const uint32_t k = __popc(t);
-                    if (pos + 1 + k > end) { st = ST_EOF; break; }
-                    emit(perm64(view_word8(q0, q1, q2, q3, o + 1), lut[t]));
-                    pos += 1 + k;
-                }
-            }
-            if (st != ST_OK) finish(st);
-            else if (done) finish(ST_OK);
-            else {
-                q0 = q2;
-                q1 = q3;
-                q2 = n0;
-                q3 = n1;
-                wb += 16;
-                kind = SM_RUN;
-            }
+        } else if (kind == SM_FIRST) {
+            kind = SM_RUN;  // its first pieces enter the ring next turn
+        }
+        wave_lds_sync();  // the ring writes above are visible to the reads below
+        const uint32_t lim = 16 * (k + 2);  // span end
+        for (;;) {  // one record per lane per pass; predicated body, uniform exit
+            const bool go = act && pos < lim && (lit != 0 || pos < end);
+            if (__ballot(go) == 0) break;
+            const bool isl = lit != 0;
+            const uint32_t qq = isl ? pos - 1 : pos;  // a literal word reads as if after an FF tag at pos - 1
+            uint32_t t = ring[pos & 63];
+            uint32_t b1 = ring[(pos + 1) & 63];
+            uint32_t c9 = ring[(pos + 9) & 63];
+            const uint32_t a = (qq + 1) & ~7u;
+            uint64_t lo = *reinterpret_cast<const uint64_t*>(ring + (a & 63));
+            uint64_t hi = *reinterpret_cast<const uint64_t*>(ring + ((a + 8) & 63));
+            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9), "+v"(lo), "+v"(hi));  // one LDS round trip
+            const uint32_t sh = ((qq + 1) & 7) * 8;
+            const uint64_t pay = (lo >> sh) | ((hi << 1) << (63 - sh));  // bytes qq+1 .. qq+8
+            const bool z = !isl && t == 0u, f = !isl && t == 0xFFu;
+            // message.zig:101-141: 00 c -> c+1 zero words; FF w c -> w, then c literal words;
+            // other tags -> popc(t) bytes scattered to the set bits
+            const uint32_t len = isl ? 8u : 1u + __popc(t) + (uint32_t)(z | f);
+            const bool eof = go && !isl && (pos + len > end || (f && pos + 10u + 8u * c9 > end));
+            const bool ok = go && !eof;
+            const uint64_t word = perm64(pay, lut[isl ? 0xFFu : t]);  // lut[0] = zero word
+            if (ok && wo < capw) dst[wo] = word;
+            const uint32_t zr = (ok && z) ? b1 : 0u;  // the zero run's further words
+            for (uint32_t j = 1; j <= zr; ++j)
+                if (wo + j < capw) dst[wo + j] = 0;
+            pos = ok ? pos + len : pos;
+            lit = ok ? (isl ? lit - 1u : (f ? c9 : 0u)) : lit;
+            wo = ok ? wo + 1u + zr : wo;
+            if (eof) finish(ST_EOF);
+            act = act && !eof;
+        }
+        if (act) {  // still running: done, or the next span
+            if (pos >= end && lit == 0) finish(ST_OK);
+            else k += 2;
         }
     }
 }
