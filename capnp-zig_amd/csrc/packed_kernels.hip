@@ -719,6 +719,11 @@ __device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t of
 // units first) and the serial list of units the table could not hold.
 constexpr uint64_t kQHuge = 65536;
 constexpr uint32_t kQHead = 16;
+constexpr uint32_t kClassBlock = 1024;  // units per class-kernel block
+constexpr uint32_t kClassK = 8;         // per-block class counters (7 classes used)
+__host__ __device__ inline uint64_t class_blocks(uint64_t n) { return (n + kClassBlock - 1) / kClassBlock; }
+// u32 index of the serial list (long units no tile / window table could hold)
+__host__ __device__ inline uint64_t serial_off(uint64_t n) { return kQHead + 3 * n + kClassK * class_blocks(n); }
 __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
                                                  uint64_t out_off, uint64_t cap);
 
@@ -745,7 +750,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
     uint8_t* lds = smem + wave * kEncLds;
     uint32_t unit = 0;
     // the units long_tiles_kernel could not list (the serial list), one after another
-    const uint32_t* const serial = q + kQHead + 3ull * n + 4 * ((n + 1023) / 1024);
+    const uint32_t* const serial = q + serial_off(n);
     for (;;) {  // wave-uniform
     {
         uint32_t i = 0;
@@ -1558,26 +1563,21 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     uint8_t* pk = pk_all + wave * kWvPk;
     uint8_t* mk = mk_all + wave * kWvWin;
     // CK: a first pass ran; this kernel takes only the units it marked kStNeedFull, with a
-    // small grid striding over the batch (64 statuses per load). QD: units from the serial list.
-    const uint32_t* const serial = q + kQHead + 3ull * n + 4 * ((n + 1023) / 1024);
-    const uint32_t stride = QD ? 0u : gridDim.x * kWvWaves * kWave;
-    for (uint32_t ubase = QD ? 0u : (blockIdx.x * kWvWaves + wave) * kWave; ubase < n; ubase += stride) {
+    // small grid striding over the batch (64 statuses per load). QD: the serial list, a
+    // wave per entry striding over it (no shared atomic cursor: contended takes serialise).
+    const uint32_t* const serial = q + serial_off(n);
+    const uint32_t nq = QD ? q[5] : n;
+    const uint32_t stride = QD ? gridDim.x * kWvWaves : gridDim.x * kWvWaves * kWave;
+    for (uint32_t ubase = QD ? blockIdx.x * kWvWaves + wave : (blockIdx.x * kWvWaves + wave) * kWave; ubase < nq;
+         ubase += stride) {
     uint64_t todo = 1;
     if (CK) {
         const uint32_t u = ubase + lane;
         todo = __ballot(u < n && status[u] == kStNeedFull);
     }
     while (todo) {  // wave-uniform
-    uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : ubase;
-    if (QD) {
-        uint32_t i = 0;
-        if (lane == 0) i = atomicAdd(q + 10, 1u);
-        i = __builtin_amdgcn_readfirstlane(i);
-        if (i >= q[5]) return;
-        unit = serial[i];
-    } else {
-        todo &= todo - 1;
-    }
+    const uint32_t unit = CK ? ubase + (uint32_t)__builtin_ctzll(todo) : __builtin_amdgcn_readfirstlane(serial[ubase]);
+    todo &= todo - 1;
     const uint8_t* src = in + in_off[unit];
     const uint64_t P = in_len[unit];
     uint8_t* dstb = out + out_off[unit];
@@ -2170,14 +2170,16 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 //          64 units per wave, then decode_fill_kernel, a wave per unit);
 //   long, huge: a wave per unit walking it tile by tile / window by window
 //          (encode_tiled_kernel / decode_wave_kernel<kWvLong>), on the side stream.
-// Workspace q (queue_bytes(n)): q[0] long, q[1] take cursor, q[2] huge, q[3] small and
-// q[4] mid counts; the long list at q[kQHead ..] upwards and the huge list from
-// q[kQHead + n - 1] downwards, the small list at q[kQHead + n ..], the mid
-// list at q[kQHead + 2n ..], then kClassK counts per class block. Count, scan, scatter:
-// each list keeps batch order, and no atomic is contended.
-constexpr uint32_t kClassBlock = 1024;
-constexpr uint32_t kClassK = 4;
-enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3 };
+// Workspace q (queue_bytes(n)): q[0] long, q[2] huge, q[3] small and q[4] mid counts, q[5]
+// serial units, q[8..9] tiles / windows listed, q[10] serial take cursor, q[11 + b] mid units before bin b; the long list at q[kQHead ..] upwards and the huge list from
+// q[kQHead + n - 1] downwards, the small list at q[kQHead + n ..], the mid list at
+// q[kQHead + 2n ..], kClassK counts per class block, the serial list (serial_off), then the
+// tile table (encode) or the window table (decode). Count, scan, scatter: each list keeps
+// batch order, and no atomic is contended.
+// decode mid units are binned by packed length (CL_MID + 0..3: <= 1280, <= 2048, <= 3072,
+// more bytes), so the lanes of an index-pass wave walk units of similar length in lockstep;
+// the mid list is the bins in order (batch order within a bin)
+enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3, CL_MID_BINS = 4 };
 constexpr uint64_t kSmEncWords = 64;  // encode: units of at most 64 words are small
 constexpr uint64_t kSmDecP = 512;     // decode: small = at most 512 packed bytes ...
 constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
@@ -2197,7 +2199,7 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
     const uint64_t cap = out_cap[u];
     if (len <= kSmDecP && cap <= kSmDecCap) return CL_SMALL;
     if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
-    return CL_MID;
+    return CL_MID + (len > 1280) + (len > 2048) + (len > 3072);
 }
 
 // Pass 1: units per class in each block of kClassBlock units; long units get the
@@ -2262,7 +2264,12 @@ __global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t 
         q[0] = carry[CL_LONG];
         q[2] = carry[CL_HUGE];
         q[3] = carry[CL_SMALL];
-        q[4] = carry[CL_MID];
+        uint32_t mid = 0;  // q[11 + b]: mid units in the bins before bin b
+        for (uint32_t b = 0; b < CL_MID_BINS; ++b) {
+            q[11 + b] = mid;
+            mid += carry[CL_MID + b];
+        }
+        q[4] = mid;
     }
 }
 
@@ -2291,7 +2298,8 @@ __global__ __launch_bounds__(kClassBlock) void class_scatter_kernel(const uint8_
     for (uint32_t j = 0; j < w; ++j) idx += wcnt[j][c];
     if (c == CL_LONG) q[kQHead + idx] = u;
     else if (c == CL_HUGE) q[kQHead + n - 1 - idx] = u;
-    else q[kQHead + (c == CL_SMALL ? 1ull : 2ull) * n + idx] = u;
+    else if (c == CL_SMALL) q[kQHead + 1ull * n + idx] = u;
+    else q[kQHead + 2ull * n + q[11 + (c - CL_MID)] + idx] = u;
 }
 
 // ---- long units, tile-parallel encode ---------------------------------
@@ -2318,14 +2326,13 @@ struct TileTab {
     uint32_t* serial;
     uint64_t cap;
 };
-__host__ __device__ inline uint64_t class_blocks(uint64_t n) { return (n + 1023) / 1024; }  // kClassBlock
 __host__ __device__ inline uint64_t tile_tab_off(uint64_t n) {  // u32 index of the tile table (8-B aligned)
-    return (kQHead + 4 * n + 4 * class_blocks(n) + 1) & ~1ull;
+    return (serial_off(n) + n + 1) & ~1ull;
 }
 __device__ __forceinline__ TileTab tile_tab(uint32_t* q, uint32_t n) {
     TileTab t;
     t.cap = (uint64_t)n + kTileExtra;
-    t.serial = q + kQHead + 3ull * n + 4 * class_blocks(n);
+    t.serial = q + serial_off(n);
     t.size = reinterpret_cast<uint64_t*>(q + tile_tab_off(n));
     t.unit = q + tile_tab_off(n) + 2 * t.cap;
     t.first = t.unit + t.cap;
@@ -2525,7 +2532,8 @@ __global__ __launch_bounds__(256) void long_windows_kernel(const uint64_t* __res
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nh = q[2], nl = q[0];
     if (i >= nl + nh) return;
-    const uint32_t unit = i < nh ? q[kQHead + n - 1 - i] : q[kQHead + (i - nh)];
+    const uint64_t slot = i < nh ? kQHead + n - 1 - i : kQHead + (i - nh);
+    const uint32_t unit = q[slot];
     WinEnt* const e = win_tab(q, n);
     const uint64_t cap = win_cap(n);
     const uint64_t k = (in_len[unit] + kWvWin - 1) / kWvWin;  // >= 1 (P > 0)
@@ -2536,9 +2544,11 @@ __global__ __launch_bounds__(256) void long_windows_kernel(const uint64_t* __res
             e[base + j].unit = unit;
             e[base + j].first = (uint32_t)base;
         }
+        q[slot] = (uint32_t)base;  // the list entry now names the unit's first window (resolve pass)
     } else {
         for (uint64_t j = base; j < cap; ++j) e[j].unit = kTileSkip;  // reserved past the end: unused
-        q[kQHead + 3ull * n + 4 * class_blocks(n) + atomicAdd(q + 5, 1u)] = unit;  // the serial list
+        q[serial_off(n) + atomicAdd(q + 5, 1u)] = unit;  // the serial list
+        q[slot] = kTileSkip;
     }
 }
 
@@ -2638,26 +2648,21 @@ __global__ __launch_bounds__(kWvBlock) void window_resolve_kernel(const uint8_t*
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
     __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
     __shared__ int16_t dl_all[kWvWaves][kWinBatch][kWinD];
-    const uint64_t T = min((uint64_t)*q_tiles(q), win_cap(n));
-    if ((uint64_t)blockIdx.x * kWvWaves * kWave >= T) return;  // block-uniform
+    const uint32_t nlist = q[0] + q[2];
+    if ((uint64_t)blockIdx.x * kWvWaves >= nlist) return;  // block-uniform
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* const pk = pk_all + wave * kWvPk;
     uint8_t* const mk = mk_all + wave * kWvWin;
     WinEnt* const tab = win_tab(q, n);
-    const uint64_t G = (uint64_t)gridDim.x * kWvWaves * kWave;
-    // waves take 64 table entries at a time and resolve the units whose first window is there
-    for (uint64_t gb = ((uint64_t)blockIdx.x * kWvWaves + wave) * kWave; gb < T; gb += G) {
-        const uint64_t gl = gb + lane;
-        bool head = false;
-        if (gl < T) {
-            const uint32_t u = tab[gl].unit;
-            head = u != kTileSkip && tab[gl].first == (uint32_t)gl;
-        }
-        uint64_t hm = __ballot(head);
-        while (hm) {  // wave-uniform
-            const uint64_t g0 = gb + (uint64_t)__builtin_ctzll(hm);
-            hm &= hm - 1;
+    const uint32_t G = gridDim.x * kWvWaves;
+    // a wave per listed long unit: the list entry names its first window (long_windows_kernel)
+    for (uint32_t li = blockIdx.x * kWvWaves + wave; li < nlist; li += G) {
+        {
+            const uint32_t nh = q[2];
+            const uint32_t b0 = q[li < nh ? kQHead + n - 1 - li : kQHead + (li - nh)];
+            if (b0 == kTileSkip) continue;  // the serial decoder's
+            const uint64_t g0 = b0;
             const uint32_t unit = __builtin_amdgcn_readfirstlane(tab[g0].unit);
             const uint8_t* const src = in + in_off[unit];
             const uint64_t P = in_len[unit];
@@ -3996,7 +4001,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const uint32_t long_blocks = min((n + kWvWaves - 1) / kWvWaves, long_res);  // up to a wave per unit
     const uint64_t wcap = win_cap(n);
     const uint32_t win_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, spec_res);
-    const uint32_t res_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves * kWave - 1) / (kWvWaves * kWave), res_res);
+    const uint32_t res_blocks = std::min((n + kWvWaves - 1) / kWvWaves, res_res);  // up to a wave per long unit
     const uint32_t wfill_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, fill_res);
     const hipStream_t ss = side.stream();
     long_windows_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
