@@ -2782,10 +2782,11 @@ __global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __
 constexpr uint32_t kSmBlock = 256;
 enum : uint32_t { SM_IDLE, SM_EXIT, SM_META, SM_FIRST, SM_RUN };
 
-// Zig encoder rules (message.zig:200-271) as a word-at-a-time state machine: a zero run
-// (00 n-1) is emitted when it ends; a literal run's count byte (FF w0 n-1 w1..) is
-// patched when it ends (in the chunk being assembled, or with a byte store once that
-// chunk has been written).
+// Zig encoder rules (message.zig:200-271) as a word-at-a-time state machine, one word per
+// step on every lane with a predicated body (no per-word branches): a zero run (00 n-1) is
+// emitted when it ends; a literal run's count byte (FF w0 n-1 w1..) is patched when it ends
+// (in the 16-B chunk being assembled in registers, or with a byte store once that chunk has
+// been written). A turn codes the 4 words read a turn earlier while the next 32 B are read.
 template <bool WRITE>
 __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
@@ -2811,10 +2812,10 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
     uint64_t cursor = first;  // wave-uniform
 
     uint32_t kind = SM_IDLE, unit = 0;
-    const uint8_t* cb = in;     // 16-B aligned base of the unit's input
+    const uint8_t* cb = in;     // 32-B aligned base of the unit's input
     uint32_t s8 = 0, nw = 0;    // word index space: the unit's words are [s8, nw)
-    uint32_t cj = 0, nch = 0;   // chunk in (c0, c1); chunks of the unit
-    uint64_t c0 = 0, c1 = 0, n0 = 0, n1 = 0;
+    uint32_t cj = 0, nch = 0;   // current 32-B chunk; chunks of the unit
+    uint4 c0, c1, n0, n1;       // the chunk being coded, the next one (in flight)
     uint8_t* db = out;          // 16-B aligned base of the output slot
     uint32_t da = 0;            // slot start & 15
     uint64_t cap = 0, op = 0;   // slot capacity; packed bytes so far
@@ -2827,79 +2828,86 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
         status[unit] = st;
         kind = SM_IDLE;
     };
-    // write bytes [lo, hi) of output chunk `ch` (slot-relative, clipped to the slot)
-    auto flush = [&](uint64_t ch, uint32_t lo, uint32_t hi) {
+    // write bytes [lo, hi) of output chunk `ch` = (x0, x1) (slot-relative, clipped to the slot)
+    auto flush = [&](uint64_t ch, uint64_t x0, uint64_t x1, uint32_t lo, uint32_t hi) {
         const uint64_t cs = 16 * ch;
         const uint64_t lim = cap > ~0ull - 16 ? ~0ull : da + cap;  // slot end (saturated)
         const uint64_t a = max(cs + lo, (uint64_t)da), e = min(cs + hi, lim);
         if (a >= e) return;
         if (a == cs && e == cs + 16) {
             // plain store: a later count-byte patch of this chunk must land after it
-            *reinterpret_cast<u32x4*>(db + cs) = u32x4{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1,
-                                                      (uint32_t)(b1 >> 32)};
+            *reinterpret_cast<u32x4*>(db + cs) = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
+                                                      (uint32_t)(x1 >> 32)};
         } else {
             for (uint64_t x = a; x < e; ++x) {
                 const uint32_t k = (uint32_t)(x - cs);
-                db[x] = (uint8_t)((k < 8 ? b0 >> (8 * k) : b1 >> (8 * (k - 8))) & 0xFF);
+                db[x] = (uint8_t)((k < 8 ? x0 >> (8 * k) : x1 >> (8 * (k - 8))) & 0xFF);
             }
         }
     };
-    auto append = [&](uint64_t v, uint32_t nb) {  // nb <= 8 bytes of v (higher bytes zero)
+    // a step appends <= 12 bytes, so it completes at most one chunk: kept here, written
+    // once at the end of the step
+    uint64_t f0 = 0, f1 = 0, fch = 0;
+    bool fpend = false;
+    // append nb <= 8 bytes of v (higher bytes zero) when p
+    auto app = [&](bool p, uint64_t v, uint32_t nb) {
         if (WRITE) {
             const uint32_t k = (uint32_t)((da + op) & 15);
-            uint64_t spill = 0;
-            if (k < 8) {
-                b0 |= v << (8 * k);
-                if (k) b1 |= v >> (64 - 8 * k);
-            } else {
-                const uint32_t j = k - 8;
-                b1 |= v << (8 * j);
-                if (j) spill = v >> (64 - 8 * j);
+            const uint32_t sh = 8 * (k & 7);
+            const uint64_t lo = v << sh, hi = (v >> 1) >> (63 - sh);  // v's bytes at chunk bytes k ..
+            const bool low = k < 8;
+            if (p) {
+                b0 |= low ? lo : 0ull;
+                b1 |= low ? hi : lo;
             }
-            if (k + nb >= 16) {
-                flush((da + op) >> 4, 0, 16);
-                b0 = spill;
+            if (p && k + nb >= 16) {  // the chunk is complete (k >= 8): keep it, continue with the spill
+                f0 = b0;
+                f1 = b1;
+                fch = (da + op) >> 4;
+                fpend = true;
+                b0 = hi;
                 b1 = 0;
             }
         }
-        op += nb;
+        op += p ? nb : 0u;
     };
-    auto close_run = [&]() {
-        if (mode == 1) {
-            append((uint64_t)(run - 1) << 8, 2);  // 00 <count>
-        } else if (mode == 2 && WRITE) {           // the literal run's count byte
-            const uint64_t x = da + cpos;
-            if ((x >> 4) == ((da + op) >> 4)) {
-                const uint32_t k = (uint32_t)(x & 15);
-                if (k < 8) b0 |= (uint64_t)(run - 1) << (8 * k);
-                else b1 |= (uint64_t)(run - 1) << (8 * (k - 8));
-            } else if (cpos < cap) {
-                db[x] = (uint8_t)(run - 1);
-            }
+    // the open literal run's count byte = c (in the chunk being assembled, the completed
+    // one not yet written, or the slot)
+    auto patch = [&](bool p, uint32_t c) {
+        if (!WRITE || !p) return;
+        const uint64_t x = da + cpos;
+        const uint32_t k = (uint32_t)(x & 15);
+        const uint64_t m0 = k < 8 ? (uint64_t)c << (8 * k) : 0ull, m1 = k < 8 ? 0ull : (uint64_t)c << (8 * (k - 8));
+        if ((x >> 4) == ((da + op) >> 4)) {
+            b0 |= m0;
+            b1 |= m1;
+        } else if (fpend && (x >> 4) == fch) {
+            f0 |= m0;
+            f1 |= m1;
+        } else if (cpos < cap) {
+            db[x] = (uint8_t)c;
         }
-        mode = 0;
     };
-    auto word = [&](uint64_t w) {  // message.zig:206-266, one word
+    auto step = [&](uint64_t w, bool valid) {  // message.zig:206-266, one word
         const uint32_t tg = nonzero_tag(w);
-        if (mode == 1) {
-            if (tg == 0 && run < 256) { ++run; return; }
-            close_run();
-        } else if (mode == 2) {
-            if (tg == 0xFF && run < 256) { append(w, 8); ++run; return; }
-            close_run();
-        }
-        if (tg == 0) {
-            mode = 1;
-            run = 1;
-        } else if (tg == 0xFF) {
-            append(0xFFull | (w << 8), 8);  // FF w0 ...
-            append(w >> 56, 1);
-            cpos = op;
-            append(0, 1);                   // count, patched by close_run
-            mode = 2;
-            run = 1;
-        } else {
-            append((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) << 8 : 0ull), 1 + __popc(tg));
+        const bool isz = tg == 0u, isf = tg == 0xFFu;
+        const bool cz = valid && mode == 1 && isz && run < 256;  // continues the zero run
+        const bool cf = valid && mode == 2 && isf && run < 256;  // continues the literal run
+        const bool cl = valid && mode != 0 && !cz && !cf;        // the open run ends here
+        app(cl && mode == 1, (uint64_t)(run - 1) << 8, 2);       // 00 <count>
+        patch(cl && mode == 2, run - 1);
+        const bool nz = valid && !cz && !cf && isz;  // a new zero run
+        const bool nf = valid && !cz && !cf && isf;  // a new literal run
+        const bool mx = valid && !isz && !isf;       // tag + nonzero bytes
+        const uint64_t v = cf ? w : (nf ? (0xFFull | (w << 8)) : ((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) << 8 : 0ull)));
+        app(cf || nf || mx, v, (cf || nf) ? 8u : 1u + __popc(tg));
+        app(nf, w >> 56, 2);  // w7, then the count byte (0 until patched)
+        cpos = nf ? op - 1 : cpos;
+        mode = (cz || nz) ? 1u : ((cf || nf) ? 2u : (valid ? 0u : mode));
+        run = (cz || cf) ? run + 1 : ((nz || nf) ? 1u : run);
+        if (WRITE && fpend) {
+            flush(fch, f0, f1, 0, 16);
+            fpend = false;
         }
     };
 
@@ -2922,7 +2930,7 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
             }
         }
         if (__ballot(kind != SM_EXIT) == 0) break;
-        // ---- this turn's read -----------------------------------------------------------
+        // ---- this turn's reads -----------------------------------------------------------
         uint64_t m_off = 0, m_len = 0, m_oo = 0, m_cap = 0;
         if (kind == SM_META) {
             m_off = in_off[unit];
@@ -2931,22 +2939,27 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
                 m_oo = out_off[unit];
                 m_cap = out_cap[unit];
             }
+        } else if (kind == SM_FIRST) {
+            c0 = *reinterpret_cast<const uint4*>(cb);
+            c1 = *reinterpret_cast<const uint4*>(cb + 16 * (uint32_t)(nw > 2));
         } else if (kind == SM_RUN && cj + 1 < nch) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(cb + 16ull * (cj + 1));
-            n0 = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-            n1 = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+            const uint8_t* const g = cb + 32ull * (cj + 1);
+            n0 = *reinterpret_cast<const uint4*>(g);
+            n1 = *reinterpret_cast<const uint4*>(g + 16 * (uint32_t)(4 * (cj + 1) + 2 < nw));
         }
         // ---- code what the previous turn read -----------------------------------------------
+        const bool run_now = kind == SM_RUN;
         if (kind == SM_META) {
             const uint8_t* const src = in + m_off;
             if (reinterpret_cast<uintptr_t>(src) & 7) finish(ST_ARG, 0);
             else if (m_len & 7) finish(ST_SIZE, 0);  // message.zig:201
             else if (m_len == 0) finish(ST_OK, 0);
             else {
-                s8 = (uint32_t)((reinterpret_cast<uintptr_t>(src) >> 3) & 1);
-                cb = src - 8 * s8;
+                const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 31);  // 0, 8, 16, 24
+                s8 = s >> 3;
+                cb = src - s;
                 nw = s8 + (uint32_t)(m_len >> 3);
-                nch = (nw + 1) >> 1;
+                nch = (nw + 3) >> 2;
                 uint8_t* const dst = out + m_oo;
                 da = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
                 db = dst - da;
@@ -2955,23 +2968,34 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
                 b0 = b1 = 0;
                 mode = 0;
                 cj = 0;
-                const u32x4 v = *reinterpret_cast<const u32x4*>(cb);  // chunk 0 (once per unit)
-                c0 = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-                c1 = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
-                kind = SM_RUN;
+                kind = SM_FIRST;
             }
-        } else if (kind == SM_RUN) {
-            const uint32_t w0 = 2 * cj;
-            if (w0 >= s8) word(c0);
-            if (w0 + 1 < nw) word(c1);
-            if (cj + 1 < nch) {
-                c0 = n0;
-                c1 = n1;
-                ++cj;
-            } else {
-                close_run();
-                if (WRITE && ((da + op) & 15)) flush((da + op) >> 4, 0, (uint32_t)((da + op) & 15));
-                finish((WRITE && op > cap) ? ST_SPACE : ST_OK, op);
+        } else if (kind == SM_FIRST) {
+            kind = SM_RUN;  // chunk 0 is coded next turn
+        }
+        if (__ballot(run_now) != 0) {
+            const uint32_t w0 = 4 * cj;
+#pragma nounroll
+            for (uint32_t t = 0; t < 4; ++t) {  // one word after another (unrolled: 116 VGPRs)
+                const uint4 c = t < 2 ? c0 : c1;
+                const uint64_t w = (t & 1) ? ((uint64_t)c.z | ((uint64_t)c.w << 32)) : ((uint64_t)c.x | ((uint64_t)c.y << 32));
+                step(w, run_now && w0 + t >= s8 && w0 + t < nw);
+            }
+            if (run_now) {
+                if (cj + 1 < nch) {
+                    c0 = n0;
+                    c1 = n1;
+                    ++cj;
+                } else {
+                    app(mode == 1, (uint64_t)(run - 1) << 8, 2);  // the unit ends inside a run
+                    patch(mode == 2, run - 1);
+                    if (WRITE && fpend) {
+                        flush(fch, f0, f1, 0, 16);
+                        fpend = false;
+                    }
+                    if (WRITE && ((da + op) & 15)) flush((da + op) >> 4, b0, b1, 0, (uint32_t)((da + op) & 15));
+                    finish((WRITE && op > cap) ? ST_SPACE : ST_OK, op);
+                }
             }
         }
     }
