@@ -3009,6 +3009,17 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
 // k + 5 are in flight into registers; they enter the ring at the start of the next turn.
 // A truncated record is UnexpectedEof with nothing more written.
 constexpr uint32_t kSdRing = 80;  // LDS bytes per lane: the 64-B ring + 16 B (fewer bank conflicts)
+// Words w-1 (even, held back) and w (odd) of an output slot of capw words: one 16-B store
+// (the slot is 8-B aligned; gfx950 global stores accept that), or the even word alone
+// when only it fits.
+__device__ __forceinline__ void store_pair(uint64_t* dst, uint32_t w, uint32_t capw, uint64_t even, uint64_t odd) {
+    if (w < capw) {
+        const u32x4 v = {(uint32_t)even, (uint32_t)(even >> 32), (uint32_t)odd, (uint32_t)(odd >> 32)};
+        *reinterpret_cast<u32x4*>(dst + w - 1u) = v;
+    } else if (w - 1u < capw) {
+        dst[w - 1u] = even;
+    }
+}
 __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len, uint32_t n,
@@ -3037,6 +3048,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
     uint32_t end = 0, pos = 0, k = 0, np = 0, lit = 0;  // aligned space: bytes [s, end); span start piece
     uint4 d0, d1, d2, d3;                                // pieces in flight
     uint64_t* dst = nullptr;
+    uint64_t pend = 0;  // output word at an even index, stored with the next one
     uint32_t capw = 0, wo = 0;
     uint64_t cap = 0;
 
@@ -3142,10 +3154,17 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             const bool eof = go && !isl && (pos + len > end || (f && pos + 10u + 8u * c9 > end));
             const bool ok = go && !eof;
             const uint64_t word = perm64(pay, lut[isl ? 0xFFu : t]);  // lut[0] = zero word
-            if (ok && wo < capw) dst[wo] = word;
+            // Output words go out in pairs: an even-index word waits in `pend` and is stored
+            // with its odd neighbour as one 16-B store (lanes write to different units, so
+            // each lane's store is its own transaction: 8-B stores cost the kernel half its
+            // time). A word at capw or beyond is not stored.
+            if (ok && (wo & 1u)) store_pair(dst, wo, capw, pend, word);
+            pend = (ok && !(wo & 1u)) ? word : pend;
             const uint32_t zr = (ok && z) ? b1 : 0u;  // the zero run's further words
-            for (uint32_t j = 1; j <= zr; ++j)
-                if (wo + j < capw) dst[wo + j] = 0;
+            for (uint32_t j = 1; j <= zr; ++j) {
+                if ((wo + j) & 1u) store_pair(dst, wo + j, capw, pend, 0ull);
+                else pend = 0ull;
+            }
             pos = ok ? pos + len : pos;
             lit = ok ? (isl ? lit - 1u : (f ? c9 : 0u)) : lit;
             wo = ok ? wo + 1u + zr : wo;
@@ -3153,8 +3172,12 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             act = act && !eof;
         }
         if (act) {  // still running: done, or the next span
-            if (pos >= end && lit == 0) finish(ST_OK);
-            else k += 2;
+            if (pos >= end && lit == 0) {
+                if ((wo & 1u) && wo - 1u < capw) dst[wo - 1u] = pend;  // the last word waiting
+                finish(ST_OK);
+            } else {
+                k += 2;
+            }
         }
     }
 }
