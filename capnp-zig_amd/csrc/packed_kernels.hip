@@ -2839,10 +2839,27 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
             *reinterpret_cast<u32x4*>(db + cs) = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
                                                       (uint32_t)(x1 >> 32)};
         } else {
-            for (uint64_t x = a; x < e; ++x) {
-                const uint32_t k = (uint32_t)(x - cs);
-                db[x] = (uint8_t)((k < 8 ? x0 >> (8 * k) : x1 >> (8 * (k - 8))) & 0xFF);
-            }
+            // a unit's first / last chunk: naturally aligned 1/2/4/8-B stores, up to 8-B
+            // alignment and then down from it (at most 8 predicated stores; a byte loop ran
+            // to the wave's longest partial chunk: ~100 us of C5's small encode)
+            uint32_t lo = (uint32_t)(a - cs);
+            const uint32_t hi = (uint32_t)(e - cs);
+            auto put = [&](uint32_t sz) {  // bytes [lo, lo + sz), lo aligned to sz
+                const uint64_t v = lo < 8 ? x0 >> (8 * lo) : x1 >> (8 * (lo - 8));
+                uint8_t* const p = db + cs + lo;
+                if (sz == 8) *reinterpret_cast<uint64_t*>(p) = v;
+                else if (sz == 4) *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
+                else if (sz == 2) *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+                else *p = (uint8_t)v;
+                lo += sz;
+            };
+            if ((lo & 1) && lo + 1 <= hi) put(1);
+            if ((lo & 2) && lo + 2 <= hi) put(2);
+            if ((lo & 4) && lo + 4 <= hi) put(4);
+            if (lo + 8 <= hi) put(8);
+            if (lo + 4 <= hi) put(4);
+            if (lo + 2 <= hi) put(2);
+            if (lo + 1 <= hi) put(1);
         }
     };
     // a step appends <= 12 bytes, so it completes at most one chunk: kept here, written
