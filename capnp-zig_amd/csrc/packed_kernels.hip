@@ -262,6 +262,29 @@ __device__ __forceinline__ uint64_t expand_word(uint64_t d, uint32_t t) {
 // directly over global memory. Used for units beyond the fast-path limits.
 // ---------------------------------------------------------------------------
 
+// Bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk (x0 = bytes 0-7, x1 = bytes 8-15)
+// whose 16-B aligned home is c16: naturally aligned 1/2/4/8-B stores, up to 8-B alignment
+// and then down from it (at most 8 predicated stores). A byte loop runs to the wave's
+// longest partial chunk (C5 small encode: ~100 us of 400).
+__device__ __forceinline__ void store_partial16(uint8_t* c16, uint32_t lo, uint32_t hi, uint64_t x0, uint64_t x1) {
+    auto put = [&](uint32_t sz) {  // bytes [lo, lo + sz), lo aligned to sz
+        const uint64_t v = lo < 8 ? x0 >> (8 * lo) : x1 >> (8 * (lo - 8));
+        uint8_t* const p = c16 + lo;
+        if (sz == 8) *reinterpret_cast<uint64_t*>(p) = v;
+        else if (sz == 4) *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
+        else if (sz == 2) *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+        else *p = (uint8_t)v;
+        lo += sz;
+    };
+    if ((lo & 1) && lo + 1 <= hi) put(1);
+    if ((lo & 2) && lo + 2 <= hi) put(2);
+    if ((lo & 4) && lo + 4 <= hi) put(4);
+    if (lo + 8 <= hi) put(8);
+    if (lo + 4 <= hi) put(4);
+    if (lo + 2 <= hi) put(2);
+    if (lo + 1 <= hi) put(1);
+}
+
 __device__ __forceinline__ uint64_t gload64(const uint8_t* p) {  // 8-aligned
     return *reinterpret_cast<const uint64_t*>(p);
 }
@@ -608,8 +631,9 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
                     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + cb),
                                                 reinterpret_cast<u32x4*>(gdst + cb));
                 } else {
-                    uint32_t a = max(cb, lo), e = min(ce, hi);
-                    for (uint32_t b = a; b < e; ++b) gdst[b] = lds[b];
+                    const uint32_t a = max(cb, lo), e = min(ce, hi);  // the unit's first / last chunk
+                    store_partial16(gdst + cb, a - cb, e - cb, *reinterpret_cast<const uint64_t*>(lds + cb),
+                                    *reinterpret_cast<const uint64_t*>(lds + cb + 8));
                 }
             }
         }
@@ -1850,10 +1874,25 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
                 if ((g & 3) == 3 || k == maxr) {
                     const uint32_t fb = g >> 2;
                     uint8_t* const q = (take && fb < nflush) ? ixp + 64 * fb : cpk_sink64;
-                    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(q), "v"(rq0) : "memory");
-                    asm volatile("global_store_dwordx4 %0, %1, off offset:16" ::"v"(q), "v"(rq1) : "memory");
-                    asm volatile("global_store_dwordx4 %0, %1, off offset:32" ::"v"(q), "v"(rq2) : "memory");
-                    asm volatile("global_store_dwordx4 %0, %1, off offset:48" ::"v"(q), "v"(rq3) : "memory");
+                    // transposed through the ring's first 64 B (round k+1 keeps only its last
+                    // 16 B): store m writes units 16m .. 16m+15, 4 lanes x 16 B per unit, so
+                    // each instruction writes 16 contiguous 64-B runs, not 64 scattered 16-B ones
+                    wave_lds_sync();
+                    *reinterpret_cast<u32x4*>(ring) = rq0;
+                    *reinterpret_cast<u32x4*>(ring + 16) = rq1;
+                    *reinterpret_cast<u32x4*>(ring + 32) = rq2;
+                    *reinterpret_cast<u32x4*>(ring + 48) = rq3;
+                    wave_lds_sync();
+                    const uint64_t qa = reinterpret_cast<uint64_t>(q);
+#pragma unroll
+                    for (uint32_t m = 0; m < 4; ++m) {
+                        const uint32_t u = 16 * m + lane / 4;
+                        const uint64_t ua = (uint64_t)(uint32_t)__shfl((int)(uint32_t)qa, (int)u, kWave) |
+                                            ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(qa >> 32), (int)u, kWave) << 32);
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(ring_all + u * kRing + 16 * (lane & 3));
+                        uint8_t* const qd = reinterpret_cast<uint8_t*>(ua) + 16 * (lane & 3);
+                        asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(qd), "v"(v) : "memory");
+                    }
                 }
             } else {
                 rec0 = rec;
@@ -2839,27 +2878,8 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
             *reinterpret_cast<u32x4*>(db + cs) = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
                                                       (uint32_t)(x1 >> 32)};
         } else {
-            // a unit's first / last chunk: naturally aligned 1/2/4/8-B stores, up to 8-B
-            // alignment and then down from it (at most 8 predicated stores; a byte loop ran
-            // to the wave's longest partial chunk: ~100 us of C5's small encode)
-            uint32_t lo = (uint32_t)(a - cs);
-            const uint32_t hi = (uint32_t)(e - cs);
-            auto put = [&](uint32_t sz) {  // bytes [lo, lo + sz), lo aligned to sz
-                const uint64_t v = lo < 8 ? x0 >> (8 * lo) : x1 >> (8 * (lo - 8));
-                uint8_t* const p = db + cs + lo;
-                if (sz == 8) *reinterpret_cast<uint64_t*>(p) = v;
-                else if (sz == 4) *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
-                else if (sz == 2) *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
-                else *p = (uint8_t)v;
-                lo += sz;
-            };
-            if ((lo & 1) && lo + 1 <= hi) put(1);
-            if ((lo & 2) && lo + 2 <= hi) put(2);
-            if ((lo & 4) && lo + 4 <= hi) put(4);
-            if (lo + 8 <= hi) put(8);
-            if (lo + 4 <= hi) put(4);
-            if (lo + 2 <= hi) put(2);
-            if (lo + 1 <= hi) put(1);
+            // a unit's first / last chunk
+            store_partial16(db + cs, (uint32_t)(a - cs), (uint32_t)(e - cs), x0, x1);
         }
     };
     // a step appends <= 12 bytes, so it completes at most one chunk: kept here, written
