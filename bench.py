@@ -767,7 +767,7 @@ def main():
 
     if args.only:
         legs = {"validate": validate_leg, "c5": skewed_leg, "dense": dense_leg, "read_message": read_message_leg,
-                "framing": message_leg}
+                "framing": message_leg, "rpc_framer": framer_leg}
         print(json.dumps({args.only: legs[args.only](args, dev)}), flush=True)
         return
     n, ub = args.units, args.unit_bytes

@@ -198,6 +198,9 @@ SIGNATURES = {
                                                        _sz, _vp]),
     "capnp_packed_generate": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                              ctypes.c_uint64, ctypes.c_uint32, _vp]),
+    "capnp_packed_frame_connections": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp,
+                                                      ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
+                                                      ctypes.POINTER(ctypes.c_uint32)]),
 }
 
 
@@ -502,71 +505,84 @@ class PackedConnections:
         self.device = torch.device(device)
 
     def handle_read(self, reads: dict) -> dict:
-        for c, data in reads.items():
-            if not self.closed[c]:
-                self.framers[c].push(data)
-        conns = [c for c in range(len(self.framers)) if not self.closed[c] and self.framers[c].buffered_bytes()]
+        """One native call (capnp_packed_frame_connections): the connections' buffered
+        bytes go to the device once, rounds of the batched reader pop every frame, and the
+        frames come back in one host buffer. Each frame is a read-only memoryview into that
+        buffer (no per-frame copy; the buffer lives as long as its frames). A connection's
+        framer keeps only the bytes left after its last whole message."""
+        conns, sizes = [], []
+        for c in range(len(self.framers)):
+            if self.closed[c]:
+                continue
+            m = self.framers[c].buffered_bytes() + (len(reads[c]) if c in reads else 0)
+            if m:
+                conns.append(c)
+                sizes.append(m)
         result = {c: [] for c in conns}
         if not conns:
             return result
-        dev = self.device
-        lens = np.array([self.framers[c].buffered_bytes() for c in conns], dtype=np.int64)
-        base = np.zeros(len(conns), dtype=np.int64)
+        k = len(conns)
+        lens = np.array(sizes, dtype=np.uint64)
+        base = np.zeros(k, dtype=np.uint64)
         base[1:] = np.cumsum(lens)[:-1]
-        host = np.frombuffer(b"".join(bytes(self.framers[c].buffer) for c in conns), dtype=np.uint8)
-        d_in = torch.from_numpy(host.copy()).to(dev) if host.size else torch.zeros(1, dtype=torch.uint8, device=dev)
-        used = np.zeros(len(conns), dtype=np.int64)  # packed bytes popped so far, per connection
-        live = np.ones(len(conns), dtype=bool)
-        # first guess at each frame's size: the connection's last frame (8 KiB at first), at
-        # most 8x its buffered bytes; a round that reports OutOfSpace is redone with the
-        # framed length the reader found
-        cap = np.array([min(self._last.get(c, 8192), max(8, 8 * int(n))) for c, n in zip(conns, lens)],
-                       dtype=np.int64)
-        while True:
-            idx = np.nonzero(live & (used < lens))[0]
-            if idx.size == 0:
-                break
-            k = idx.size
-            in_off = torch.from_numpy(base[idx] + used[idx]).to(dev)
-            in_len = torch.from_numpy(lens[idx] - used[idx]).to(dev)
-            caps = (cap[idx] + 7) // 8 * 8
-            out_off_h = np.zeros(k, dtype=np.int64)
-            out_off_h[1:] = np.cumsum(caps)[:-1]
-            out_off = torch.from_numpy(out_off_h).to(dev)
-            out_cap = torch.from_numpy(caps).to(dev)
-            d_out = torch.empty(int(caps.sum()), dtype=torch.uint8, device=dev)
-            out_len = torch.zeros(k, dtype=torch.int64, device=dev)
-            consumed = torch.zeros(k, dtype=torch.int64, device=dev)
-            status = torch.zeros(k, dtype=torch.int32, device=dev)
-            read_message_batch(d_in, in_off, in_len, d_out, out_off, out_cap, out_len, consumed, status)
-            st = status.cpu().numpy()
-            ol = out_len.cpu().numpy()
-            cons = consumed.cpu().numpy()
-            grow = st == OUT_OF_SPACE
-            if grow.any():  # redo the round with the framed lengths the reader reported
-                cap[idx[grow]] = np.maximum(cap[idx[grow]] * 2, ol[grow])
-                continue
-            out_h = d_out.cpu().numpy() if (st == OK).any() else None
-            for j, i in enumerate(idx):
-                c = conns[i]
-                if st[j] == OK:
-                    result[c].append(out_h[out_off_h[j]:out_off_h[j] + ol[j]].tobytes())
-                    used[i] += cons[j]
-                    cap[i] = max(8, int(ol[j]))
-                    self._last[c] = cap[i]
-                elif st[j] == END_OF_STREAM:
-                    live[i] = False  # the rest waits for the next read
-                else:
-                    live[i] = False
-                    err = _ERRORS.get(int(st[j]), DeviceError)(
-                        f"readPackedMessage: {lib().capnp_packed_status_name(int(st[j])).decode()}")
-                    self.frames_before_error[c] = result[c]
-                    result[c] = err
-                    self.framers[c].reset()
-                    self.closed[c] = True
+        total = int(lens.sum())
+        # the framers' bytes, then this read, straight into one input buffer (the framer's
+        # push is the copy into it)
+        host = np.empty(max(total, 1), dtype=np.uint8)
         for i, c in enumerate(conns):
-            if not self.closed[c]:
-                del self.framers[c].buffer[:int(used[i])]
+            b, old = int(base[i]), self.framers[c].buffer
+            if old:
+                host[b:b + len(old)] = np.frombuffer(old, dtype=np.uint8)
+                b += len(old)
+            if c in reads and len(reads[c]):
+                host[b:b + len(reads[c])] = np.frombuffer(reads[c], dtype=np.uint8)
+        # first guess at each frame's size: the connection's last frame (8 KiB at first), at
+        # most 8x its buffered bytes; OutOfSpace rounds are redone at the framed length
+        guess = np.array([min(self._last.get(c, 8192), max(8, 8 * int(n))) for c, n in zip(conns, sizes)],
+                         dtype=np.uint64)
+        max_frames = total // 64 + k + 16
+        frames_cap = max(1 << 16, 4 * total + 2 * int(guess.sum()))
+        consumed = np.zeros(k, dtype=np.uint64)
+        status = np.zeros(k, dtype=np.int32)
+        nf = ctypes.c_uint32(0)
+        while True:
+            g = guess.copy()
+            frames = np.empty(frames_cap, dtype=np.uint8)
+            f_off = np.empty(max_frames, dtype=np.uint64)
+            f_len = np.empty(max_frames, dtype=np.uint64)
+            f_conn = np.empty(max_frames, dtype=np.uint32)
+            st = lib().capnp_packed_frame_connections(
+                host.ctypes.data, total, base.ctypes.data, lens.ctypes.data, k, g.ctypes.data, frames.ctypes.data,
+                frames_cap, f_off.ctypes.data, f_len.ctypes.data, f_conn.ctypes.data, max_frames,
+                consumed.ctypes.data, status.ctypes.data, ctypes.byref(nf))
+            if st != OUT_OF_SPACE:
+                break
+            # the frames or the frame table did not fit: the call is redone (its input is unchanged)
+            frames_cap *= 2
+            max_frames = min(2 * max_frames, total // 2 + k + 16)
+        _raise(st, "frame_connections")
+        view = memoryview(frames).toreadonly()
+        n = nf.value
+        order = np.argsort(f_conn[:n], kind="stable")  # frames by connection, in pop order
+        offs, flen = f_off[:n][order].tolist(), f_len[:n][order].tolist()
+        ends = np.cumsum(np.bincount(f_conn[:n], minlength=k)).tolist()
+        s0 = 0
+        for i, c in enumerate(conns):
+            s1 = ends[i]
+            if s1 > s0:
+                result[c] = [view[o:o + ln] for o, ln in zip(offs[s0:s1], flen[s0:s1])]
+            s0 = s1
+            self._last[c] = int(g[i])
+            rs = int(status[i])
+            if rs != END_OF_STREAM:
+                err = _ERRORS.get(rs, DeviceError)(f"readPackedMessage: {lib().capnp_packed_status_name(rs).decode()}")
+                self.frames_before_error[c] = result[c]
+                result[c] = err
+                self.framers[c].reset()
+                self.closed[c] = True
+            else:  # the bytes after the last whole message wait for the next read
+                b = int(base[i] + consumed[i])
+                self.framers[c].buffer = bytearray(host[b:int(base[i] + lens[i])].tobytes())
         return result
 
 

@@ -8,11 +8,13 @@
 // compute entry point returns CAPNP_PACKED_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "capnp_packed.h"
 #include "kernels.h"
@@ -98,6 +100,39 @@ struct HostCtx {
 };
 
 HostCtx g_ctx;
+
+// Device buffers of capnp_packed_frame_connections (grow-only; its own stream and lock,
+// so framing never waits on a single-buffer call).
+struct FrameCtx {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    uint8_t* d_meta = nullptr;
+    size_t meta_cap = 0;
+
+    int init() {
+        if (stream) return CAPNP_PACKED_OK;
+        hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "hipStreamCreate");
+    }
+    int reserve(uint8_t** p, size_t* cap, size_t need) {
+        if (need <= *cap && *p) return CAPNP_PACKED_OK;
+        if (need > (SIZE_MAX / 3) * 2) return fail(CAPNP_PACKED_OUT_OF_SPACE, "workspace size overflows size_t");
+        const size_t want = need < 65536 ? 65536 : need + need / 2;
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(p), want);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(framer)");
+        *cap = want;
+        return CAPNP_PACKED_OK;
+    }
+};
+
+FrameCtx g_fr;
 
 // Run one unit through a batch kernel. kind: 0 encode, 1 decode, 2 decoded size, 3 encoded size,
 // 4 read message (reader.zig:84-156; *used_out = packed bytes consumed).
@@ -395,6 +430,115 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
     hipError_t e = cpk::launch_generate(d_out, n_units, unit_bytes, unit_base, seed, zero_thresh,
                                         static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "generate launch");
+}
+
+int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
+                                   const uint64_t* in_len, uint32_t n, uint64_t* slot_guess, uint8_t* frames,
+                                   uint64_t frames_cap, uint64_t* frame_off, uint64_t* frame_len,
+                                   uint32_t* frame_conn, uint32_t max_frames, uint64_t* consumed, int32_t* status,
+                                   uint32_t* n_frames) {
+    if (!n_frames) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "n_frames is null");
+    *n_frames = 0;
+    if (n == 0) return CAPNP_PACKED_OK;
+    if (!in_off || !in_len || !slot_guess || !consumed || !status || (in_bytes && !in) ||
+        (max_frames && (!frame_off || !frame_len || !frame_conn)) || (frames_cap && !frames))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null pointer");
+    for (uint32_t c = 0; c < n; ++c)
+        if (in_off[c] > in_bytes || in_len[c] > in_bytes - in_off[c])
+            return fail(CAPNP_PACKED_INVALID_ARGUMENT, "connection bytes outside the input buffer");
+    int st = ensure_device();
+    if (st) return st;
+    std::lock_guard<std::mutex> lock(g_fr.mu);
+    if ((st = g_fr.init())) return st;
+    if ((st = g_fr.reserve(&g_fr.d_in, &g_fr.in_cap, in_bytes + 16))) return st;
+    if ((st = g_fr.reserve(&g_fr.d_meta, &g_fr.meta_cap, (size_t)n * 7 * sizeof(uint64_t)))) return st;
+    const hipStream_t s = g_fr.stream;
+    hipError_t e = in_bytes ? hipMemcpyAsync(g_fr.d_in, in, in_bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(H2D input)");
+    std::vector<uint64_t> used(n, 0), cap(n), meta(7ull * n);  // meta: in_off, in_len, out_off, out_cap | len, cons, st
+    std::vector<uint32_t> idx(n);
+    std::vector<uint8_t> live(n);
+    for (uint32_t c = 0; c < n; ++c) {
+        live[c] = in_len[c] > 0;
+        cap[c] = slot_guess[c] < 8 ? 8 : slot_guess[c];
+        status[c] = CAPNP_PACKED_END_OF_STREAM;
+    }
+    uint64_t fcur = 0;  // bytes of `frames` used by earlier rounds
+    uint32_t nf = 0;
+    for (;;) {
+        // one round: the next message of every connection that may still hold one
+        uint32_t k = 0;
+        for (uint32_t c = 0; c < n; ++c)
+            if (live[c] && used[c] < in_len[c]) idx[k++] = c;
+        if (k == 0) break;
+        uint64_t* const h_in_off = meta.data();
+        uint64_t* const h_in_len = h_in_off + k;
+        uint64_t* const h_out_off = h_in_off + 2 * k;
+        uint64_t* const h_out_cap = h_in_off + 3 * k;
+        uint64_t slots = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t c = idx[j];
+            h_in_off[j] = in_off[c] + used[c];
+            h_in_len[j] = in_len[c] - used[c];
+            h_out_cap[j] = (cap[c] + 7) & ~7ull;
+            h_out_off[j] = slots;
+            slots += h_out_cap[j];
+        }
+        if ((st = g_fr.reserve(&g_fr.d_out, &g_fr.out_cap, slots + 16))) return st;
+        uint64_t* const dm = reinterpret_cast<uint64_t*>(g_fr.d_meta);
+        e = hipMemcpyAsync(dm, h_in_off, 4ull * k * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(H2D round)");
+        int32_t* const d_st = reinterpret_cast<int32_t*>(dm + 6ull * k);
+        e = cpk::launch_read_message(g_fr.d_in, dm, dm + k, k, g_fr.d_out, dm + 2ull * k, dm + 3ull * k, dm + 4ull * k,
+                                     dm + 5ull * k, d_st, s);
+        if (e != hipSuccess) return hip_fail(e, "read-message launch");
+        uint64_t* const h_len = h_in_off + 4 * k;
+        uint64_t* const h_cons = h_in_off + 5 * k;
+        int32_t* const h_st = reinterpret_cast<int32_t*>(h_in_off + 6 * k);
+        e = hipMemcpyAsync(h_len, dm + 4ull * k, 2ull * k * sizeof(uint64_t) + k * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H round)");
+        // the round's frames go to `frames` as one copy of its slots up to the last good one
+        uint64_t span = 0;
+        uint32_t good = 0;
+        for (uint32_t j = 0; j < k; ++j)
+            if (h_st[j] == CAPNP_PACKED_OK) {
+                span = h_out_off[j] + h_len[j];
+                ++good;
+            }
+        if (good) {
+            if (fcur > frames_cap || span > frames_cap - fcur || good > max_frames - nf)
+                return fail(CAPNP_PACKED_OUT_OF_SPACE, "frames buffer or frame table too small");
+            e = hipMemcpy(frames + fcur, g_fr.d_out, span, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_fail(e, "hipMemcpy(D2H frames)");
+        }
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t c = idx[j];
+            const int32_t rs = h_st[j];
+            if (rs == CAPNP_PACKED_OK) {
+                frame_off[nf] = fcur + h_out_off[j];
+                frame_len[nf] = h_len[j];
+                frame_conn[nf] = c;
+                ++nf;
+                used[c] += h_cons[j];
+                cap[c] = h_len[j] < 8 ? 8 : h_len[j];
+            } else if (rs == CAPNP_PACKED_OUT_OF_SPACE) {
+                // the reader reported the framed length: next round, a slot that holds it
+                cap[c] = std::max(2 * cap[c], (uint64_t)h_len[j]);
+            } else {
+                live[c] = 0;  // END_OF_STREAM: the rest waits for the next read; else the error
+                status[c] = rs;
+            }
+        }
+        fcur += (span + 7) & ~7ull;
+    }
+    for (uint32_t c = 0; c < n; ++c) {
+        consumed[c] = used[c];
+        slot_guess[c] = cap[c];
+    }
+    *n_frames = nf;
+    return CAPNP_PACKED_OK;
 }
 
 }  // extern "C"

@@ -193,6 +193,28 @@ int capnp_packed_read_message_batch(const uint8_t* d_in, const uint64_t* d_in_of
                                     const uint64_t* d_out_cap, uint64_t* d_out_len, uint64_t* d_consumed,
                                     int32_t* d_status, void* stream);
 
+/* Connection.handleRead (src/rpc/level2/connection.zig:153-203) over n connections at
+ * once, with the Framer's popFrame (src/rpc/level0/framing.zig:4-90) as
+ * Reader.readPackedMessage on the device: a native host loop, HOST memory in and out.
+ * Connection c's buffered bytes are in[in_off[c] .. +in_len[c]) of in[0..in_bytes).
+ * One H2D of the input, then rounds of the batched reader (one unit per connection
+ * that may still hold a message); each round's frames are copied D2H straight into
+ * `frames`, so frame i is frames[frame_off[i] .. +frame_len[i]) of connection
+ * frame_conn[i] (frames of a connection in order; *n_frames of them).
+ * slot_guess[c] (in/out): the device slot for c's next frame (its last frame's size;
+ *   a round that reports OUT_OF_SPACE is redone for c with the framed length).
+ * consumed[c]: packed bytes of c's popped frames (the caller drops them from its buffer).
+ * status[c]: END_OF_STREAM when c's bytes end inside a message or are used up (the rest
+ *   waits for the next read: popFrame's null), else the reader's error that closes c
+ *   (frames popped before it are still listed).
+ * Returns OUT_OF_SPACE when `frames` (frames_cap bytes) or the frame table (max_frames)
+ * is too small: nothing is valid then; retry with larger ones. */
+int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
+                                   const uint64_t* in_len, uint32_t n, uint64_t* slot_guess, uint8_t* frames,
+                                   uint64_t frames_cap, uint64_t* frame_off, uint64_t* frame_len,
+                                   uint32_t* frame_conn, uint32_t max_frames, uint64_t* consumed, int32_t* status,
+                                   uint32_t* n_frames);
+
 /* Single-buffer Reader.readPackedMessage on HOST memory: decodes the message at
  * the front of in[0..n) into out[0..*out_len); *consumed = packed bytes used.
  * On OUT_OF_SPACE, *out_len is the framed length. */

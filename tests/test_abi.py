@@ -118,3 +118,24 @@ def test_validate_argument_errors_without_device():
     assert st == cp.OK  # n = 0: nothing to do
     st = L.capnp_packed_validate_batch(None, None, None, 4, 512, 1 << 23, 64, None, None, None)
     assert st == cp.INVALID_ARGUMENT
+
+
+def test_frame_connections_argument_errors_without_device():
+    L = cp.lib()
+    nf = ctypes.c_uint32(7)
+    args = [None, 0, None, None, 0, None, None, 0, None, None, None, 0, None, None]
+    assert L.capnp_packed_frame_connections(*args, ctypes.byref(nf)) == cp.OK and nf.value == 0  # no connections
+    assert L.capnp_packed_frame_connections(*args, None) == cp.INVALID_ARGUMENT
+    import numpy as np
+    off = np.array([0, 6], dtype=np.uint64)
+    ln = np.array([4, 4], dtype=np.uint64)  # connection 1's bytes run past in_bytes = 8
+    guess = np.full(2, 8192, dtype=np.uint64)
+    buf = np.zeros(8, dtype=np.uint8)
+    fr = np.zeros(64, dtype=np.uint8)
+    t64 = np.zeros(4, dtype=np.uint64)
+    t32 = np.zeros(4, dtype=np.uint32)
+    st32 = np.zeros(2, dtype=np.int32)
+    st = L.capnp_packed_frame_connections(buf.ctypes.data, 8, off.ctypes.data, ln.ctypes.data, 2, guess.ctypes.data,
+                                          fr.ctypes.data, 64, t64.ctypes.data, t64.ctypes.data, t32.ctypes.data, 4,
+                                          t64.ctypes.data, st32.ctypes.data, ctypes.byref(nf))
+    assert st == cp.INVALID_ARGUMENT

@@ -52,6 +52,11 @@ extern "capnp_packed" fn capnp_packed_encode(in: [*]const u8, n: usize, out: [*]
 extern "capnp_packed" fn capnp_packed_decoded_size(in: [*]const u8, n: usize, out_size: *usize) c_int;
 extern "capnp_packed" fn capnp_packed_decode(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize) c_int;
 extern "capnp_packed" fn capnp_packed_read_message(in: [*]const u8, n: usize, out: [*]u8, cap: usize, out_len: *usize, consumed: *usize) c_int;
+extern "capnp_packed" fn capnp_packed_frame_connections(
+    in: [*]const u8, in_bytes: u64, in_off: [*]const u64, in_len: [*]const u64, n: u32,
+    slot_guess: [*]u64, frames: [*]u8, frames_cap: u64, frame_off: [*]u64, frame_len: [*]u64,
+    frame_conn: [*]u32, max_frames: u32, consumed: [*]u64, status: [*]i32, n_frames: *u32,
+) c_int;
 
 // ---- device batch entry points (pointers are device memory) ----------------
 pub extern "capnp_packed" fn capnp_packed_encode_batch(
@@ -238,6 +243,25 @@ pub fn readPackedMessageBuffered(allocator: std.mem.Allocator, buffered: []const
         };
         return .{ .framed = try allocator.realloc(buf, len), .consumed = used };
     }
+}
+
+/// Connection.handleRead (connection.zig:153-203) over many connections in one native
+/// call: `frames` receives every popped frame; frame i is
+/// frames[frame_off[i]..][0..frame_len[i]] of connection frame_conn[i]. Per connection,
+/// consumed[c] bytes leave its buffer and status[c] is .end_of_stream (wait for more
+/// bytes) or the error that closes it. error.OutOfSpace: grow `frames` and call again.
+pub const FrameTable = struct { off: []u64, len: []u64, conn: []u32 };
+pub fn frameConnections(
+    buffered: []const u8, in_off: []const u64, in_len: []const u64, slot_guess: []u64,
+    frames: []u8, table: FrameTable, consumed: []u64, status: []i32,
+) Error!u32 {
+    var nf: u32 = 0;
+    try check(capnp_packed_frame_connections(
+        buffered.ptr, buffered.len, in_off.ptr, in_len.ptr, @intCast(in_off.len), slot_guess.ptr,
+        frames.ptr, frames.len, table.off.ptr, table.len.ptr, table.conn.ptr, @intCast(table.off.len),
+        consumed.ptr, status.ptr, &nf,
+    ));
+    return nf;
 }
 
 /// A validate_batch per-message status as the error Message.validate would return.
