@@ -129,3 +129,64 @@ def test_packed_connections_batched(n_conns):
             assert c not in errors and conns.framers[c].buffered_bytes() == (len(rest) if rc else 0)
         else:
             assert errors[c].status == rc and conns.closed[c] and conns.framers[c].buffered_bytes() == 0
+
+
+def _zero_heavy_message(words):
+    """A 1-segment framed message of `words` zero words: 2 packed bytes per 256 words, so its
+    framed length is far beyond any slot guessed from the packed size (the OUT_OF_SPACE
+    round of capnp_packed_frame_connections)."""
+    return pyref.frame([bytes(8 * words)])
+
+
+def test_frame_connections_slot_growth_and_small_buffers():
+    """capnp_packed_frame_connections through the C-ABI: frames of zero-run messages whose
+    framed length is ~100x their packed bytes (each connection's slot grows across
+    OUT_OF_SPACE rounds), empty connections beside them, a truncated last message, and a
+    frame buffer / frame table too small (OUT_OF_SPACE for the call, then a retry)."""
+    import ctypes
+    rng = np.random.default_rng(0xF8)
+    conns = []
+    for c in range(40):
+        msgs = []
+        for _ in range(int(rng.integers(0, 4))):
+            if rng.random() < 0.5:
+                msgs.append(_zero_heavy_message(int(rng.integers(300, 20000))))
+            else:
+                msgs.append(random_message(rng))
+        data = b"".join(oracle.pack(m)[1] for m in msgs)
+        if c % 9 == 4 and data:
+            data = data[:-1]  # the last message is cut short: END_OF_STREAM, its bytes kept
+        conns.append(data)
+    expect = [oracle_frames(d) for d in conns]
+    lens = np.array([len(d) for d in conns], dtype=np.uint64)
+    base = np.zeros(len(conns), dtype=np.uint64)
+    base[1:] = np.cumsum(lens)[:-1]
+    host = np.frombuffer(b"".join(conns) or b"\0", dtype=np.uint8)
+    total = int(lens.sum())
+
+    def call(frames_cap, max_frames):
+        g = np.full(len(conns), 64, dtype=np.uint64)  # small guesses: every big frame grows its slot
+        fr = np.zeros(max(frames_cap, 1), dtype=np.uint8)
+        fo = np.zeros(max(max_frames, 1), dtype=np.uint64)
+        fl = np.zeros(max(max_frames, 1), dtype=np.uint64)
+        fc = np.zeros(max(max_frames, 1), dtype=np.uint32)
+        cons = np.zeros(len(conns), dtype=np.uint64)
+        st = np.zeros(len(conns), dtype=np.int32)
+        nf = ctypes.c_uint32(0)
+        rc = cp.lib().capnp_packed_frame_connections(
+            host.ctypes.data, total, base.ctypes.data, lens.ctypes.data, len(conns), g.ctypes.data, fr.ctypes.data,
+            frames_cap, fo.ctypes.data, fl.ctypes.data, fc.ctypes.data, max_frames, cons.ctypes.data,
+            st.ctypes.data, ctypes.byref(nf))
+        return rc, fr, fo, fl, fc, cons, st, nf.value
+
+    assert call(64, 1024)[0] == cp.OUT_OF_SPACE   # frames do not fit
+    assert call(1 << 26, 1)[0] == cp.OUT_OF_SPACE  # frame table too small
+    rc, fr, fo, fl, fc, cons, st, n = call(1 << 26, 1024)
+    assert rc == cp.OK
+    got = [[] for _ in conns]
+    for i in range(n):
+        got[int(fc[i])].append(fr[int(fo[i]):int(fo[i]) + int(fl[i])].tobytes())
+    for c, (frames, rest, code) in enumerate(expect):
+        assert got[c] == frames, f"connection {c}"
+        assert int(cons[c]) == len(conns[c]) - len(rest)
+        assert int(st[c]) == (cp.END_OF_STREAM if code in (cp.OK, cp.END_OF_STREAM) else code)
