@@ -1619,6 +1619,32 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     uint64_t Wb = 0;  // output words before the current window
     int32_t st = ST_OK;
     bool fits = true;
+    if (QD) {
+        // a counting walk first (the serial units are the rare ones the window table
+        // cannot hold): a truncated or oversized unit writes nothing, as unpackPacked
+        // returns its error before any output (message.zig:88-145)
+        while (X < P) {
+            const WvWin w = wv_stage(pk, mk, src, P, X, lane);
+            uint32_t ent, cs, ce;
+            const uint32_t xw = wv_resolve(pk, mk, w, 0, lane, ent, cs, ce);
+            if (xw == kEOFX) {
+                st = ST_EOF;
+                break;
+            }
+            const uint32_t words = wv_count(pk, w.sh, ent, ce);
+            Wb += readlane(wave_incl_sum(words, lane), kWave - 1);
+            X += xw;
+        }
+        if (st != ST_OK || Wb > capw) {
+            if (lane == 0) {
+                out_len[unit] = st == ST_OK ? 8 * Wb : 0;
+                status[unit] = st != ST_OK ? st : ST_SPACE;
+            }
+            continue;
+        }
+        X = 0;
+        Wb = 0;
+    }
     while (X < P) {
         const WvWin w = wv_stage(pk, mk, src, P, X, lane);
         uint32_t ent, cs, ce;
@@ -1654,24 +1680,34 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
 //          own pieces' first tags (no chain to resolve), take their output word
 //          offsets from a scan of the records' word counts, expand into LDS and
 //          store coalesced.
-// Units pass 2 cannot stage (> kFlPieces pieces) or whose slot cannot hold the
-// records (decode_long_unit) belong to decode_wave_kernel<kWvLong>, which runs beside
-// passes 1 and 2 on the side stream; the read-message passes mark them kStNeedFull
-// for decode_wave_kernel<kWvMarked> instead.
+// Units pass 2 cannot stage (> kFlPieces pieces; decode_long_unit) belong to the
+// window-parallel / serial long-unit decoders, which run beside passes 1 and 2 on the
+// side stream; the read-message passes (records in the slot, below) also mark units
+// whose slot cannot hold the records kStNeedFull for decode_wave_kernel<kWvMarked>.
+//
+// Piece records live in a library workspace region (rec_region: kRecStride bytes per
+// mid-list entry), not in the caller's output slot, so a unit that ends UNEXPECTED_EOF
+// or OUT_OF_SPACE leaves its slot untouched (message.zig:90 errors before any output).
+// The read-message passes have no workspace: their gated write pass runs only over
+// units whose framed length the walk already verified, and keeps the records at the
+// front of the slot (rec = nullptr).
 constexpr uint32_t kIxDead = 0xFFFFFFFFu;         // walk position of a lane with nothing (more) to walk
 constexpr uint32_t kFlPieces = 320;               // pass-2 window: 64 lanes x 5 pieces
 constexpr uint64_t kIxSizeMax = 1ull << 31;       // size-only walk: longer units use decode_lane_kernel
+// record bytes per unit: 64 B per 8 rounds (+1 store) of at most kFlPieces * 16 B
+constexpr uint32_t kRecStride = 64 * ((kFlPieces * 16 / 64 + 8) / 8);
+static_assert(kRecStride == 704, "record region stride");
 
-// The units the indexed decoder's fallback owns (decode_wave_kernel<kWvLong>): an
-// 8-aligned output slot and a packed length pass 2 cannot stage (> kFlPieces pieces),
-// or a slot too small for pass 1's piece records. Passes 1 and 2 leave exactly these
-// units alone, so the fallback can run beside them (launch_decode).
+// The units the indexed decoder's fallback owns (the long-unit decoders): an 8-aligned
+// output slot and a packed length pass 2 cannot stage (> kFlPieces pieces). Passes 1
+// and 2 leave exactly these units alone, so the fallback can run beside them
+// (launch_decode).
 __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_off, uint64_t P, uint8_t* out,
                                                  uint64_t out_off, uint64_t cap) {
+    (void)cap;
     if (P == 0 || (reinterpret_cast<uintptr_t>(out + out_off) & 7)) return false;
     const uint64_t s = reinterpret_cast<uintptr_t>(in + in_off) & 15;
-    const uint64_t np = (s + P + 15) >> 4, nr = (s + P + 63) >> 6;
-    return !(np <= kFlPieces && cap >= 64 * ((nr + 8) / 8));
+    return ((s + P + 15) >> 4) > kFlPieces;
 }
 
 
@@ -1693,9 +1729,10 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 //
 // Per piece p the walk yields a u16 record — the offset of the first tag that
 // starts in p (4 bits) | the words its records produce << 4 (0: no tag) — kept at
-// index p + 1 of the record array at the start of the unit's output slot (so a
-// round's four records and a 16-B store stay aligned). Pass 2 reads them before it
-// writes any output. The walk also yields the decoded size and the EOF status.
+// index p + 1 of the unit's record array (so a round's four records and a 16-B store
+// stay aligned): rec + kRecStride * (list entry) in the workspace, or the front of the
+// unit's output slot when rec is null (the read-message gate pass). The walk also
+// yields the decoded size and the EOF status.
 //
 // RD selects the Reader.readPackedMessage passes (reader.zig:84-156; launch_read_message):
 //   kRdNone  unpackPacked / estimateUnpackedSize as above;
@@ -1713,7 +1750,7 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
     uint64_t* __restrict__ consumed, const uint32_t* __restrict__ list = nullptr,
-    const uint32_t* __restrict__ list_count = nullptr) {
+    const uint32_t* __restrict__ list_count = nullptr, uint8_t* __restrict__ rec = nullptr) {
     static_assert(RD != kRdWalk || SIZE_ONLY, "the read walk writes no output");
     static_assert(RD != kRdGate || !SIZE_ONLY, "the gated pass is the write pass");
     constexpr uint32_t kRing = 80;  // [0, 16): block k-1's last piece, [16, 80): block k
@@ -1754,7 +1791,7 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
     if (take) {
         const uint64_t np = (s + P64 + 15) >> 4;
         const uint64_t nr = (s + P64 + 63) >> 6;  // rounds; records take 16 B per two rounds (+1)
-        const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && cap >= 64 * ((nr + 8) / 8));
+        const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && (rec || cap >= 64 * ((nr + 8) / 8)));
         if (!fits) {
             take = false;
             st = kStNeedFull;
@@ -1795,7 +1832,7 @@ __global__ __launch_bounds__(kWave) void decode_index_kernel(
     uint64_t wrun = 0;                  // kRdWalk: decoded words so far, per record
     uint64_t rec0 = 0;                 // records of the previous (even) round
     u32x4 rq0 = {0, 0, 0, 0}, rq1 = rq0, rq2 = rq0, rq3 = rq0;  // 64 B of records waiting for their store
-    uint8_t* const ixp = (!SIZE_ONLY && take) ? dstb : cpk_sink64;
+    uint8_t* const ixp = (!SIZE_ONLY && take) ? (rec ? rec + (uint64_t)kRecStride * slot : dstb) : cpk_sink64;
     const uint32_t nflush = (nr + 8) / 8;  // 64-B record stores of this unit
     if (maxr > 0) load(0);
     for (uint32_t k = 0; k <= maxr; ++k) {
@@ -1975,6 +2012,7 @@ struct FillMeta {
     const uint8_t* src;
     uint8_t* dst;
     uint32_t T;  // output words
+    const uint16_t* rec;  // piece records
 };
 
 // Word of a code (see kFlLit): 16 bytes around its position from the staged
@@ -1999,7 +2037,8 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                                                                        const uint64_t* __restrict__ out_cap,
                                                                        const int32_t* __restrict__ status,
                                                                        const uint32_t* __restrict__ list = nullptr,
-                                                                       const uint32_t* __restrict__ list_count = nullptr) {
+                                                                       const uint32_t* __restrict__ list_count = nullptr,
+                                                                       const uint8_t* __restrict__ rec = nullptr) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFlWaves * kFlPk];
     __shared__ __attribute__((aligned(16))) uint16_t code_all[kFlWaves * (kFlOut + 8)];  // + a dummy slot
     __shared__ uint64_t lut[256];  // tag -> v_perm selector scattering popc(tag) packed bytes
@@ -2018,7 +2057,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     if (u0 >= n) return;
     if (n == n_all) list = nullptr;  // a list as long as the batch is the identity (batch order)
 
-    uint64_t m_in = 0, m_out = 0;
+    uint64_t m_in = 0, m_out = 0, m_rec = 0;  // m_rec: the unit's piece records (decode_index_kernel)
     uint32_t m_P = 0, m_T = 0;
     int32_t m_st = -1;
     auto load_batch = [&](uint32_t k0) {  // meta of the wave's units k0 .. k0+63
@@ -2030,6 +2069,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
             const uint64_t P = in_len[uu];
             m_P = (uint32_t)P;
             m_out = out_off[uu];
+            m_rec = reinterpret_cast<uint64_t>(rec ? rec + (uint64_t)kRecStride * slot : out + m_out);
             // the fallback's units (it may be writing their status right now) are skipped
             // without reading what pass 1 left for them (a class list holds none)
             if (listed || !decode_long_unit(in, m_in, P, out, m_out, out_cap[uu])) {
@@ -2045,6 +2085,8 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
         m.src = in + ((uint64_t)readlane((uint32_t)m_in, j) | ((uint64_t)readlane((uint32_t)(m_in >> 32), j) << 32));
         m.dst = out + ((uint64_t)readlane((uint32_t)m_out, j) | ((uint64_t)readlane((uint32_t)(m_out >> 32), j) << 32));
         m.T = readlane(m_T, j);
+        m.rec = reinterpret_cast<const uint16_t*>((uint64_t)readlane((uint32_t)m_rec, j) |
+                                                  ((uint64_t)readlane((uint32_t)(m_rec >> 32), j) << 32));
         return m;
     };
 
@@ -2066,13 +2108,13 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
         if (np > 192) v3 = load_nt(b + min(lane + 192, last));
         if (np > 256) v4 = load_nt(b + min(lane + 256, last));
         const uint32_t L = (np + 63) >> 6;
-        const uint16_t* const rec = reinterpret_cast<const uint16_t*>(m.dst);
+        const uint16_t* const rc = m.rec;
         const uint32_t q = lane * L + 1;  // record of piece p: index p + 1 (decode_index_kernel)
-        r0 = rec[min(q, np)];             // lanes past the last piece read the last record (unused)
-        if (L > 1) r1 = rec[min(q + 1, np)];
-        if (L > 2) r2 = rec[min(q + 2, np)];
-        if (L > 3) r3 = rec[min(q + 3, np)];
-        if (L > 4) r4 = rec[min(q + 4, np)];
+        r0 = rc[min(q, np)];              // lanes past the last piece read the last record (unused)
+        if (L > 1) r1 = rc[min(q + 1, np)];
+        if (L > 2) r2 = rc[min(q + 2, np)];
+        if (L > 3) r3 = rc[min(q + 3, np)];
+        if (L > 4) r4 = rc[min(q + 4, np)];
     };
 
     load_batch(0);
@@ -3851,14 +3893,16 @@ struct StreamCtx {
 static std::mutex g_ctx_mu;
 static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
 
-size_t queue_bytes(uint32_t n) {
-    const size_t nb = ((size_t)n + kClassBlock - 1) / kClassBlock;
-    (void)nb;
+// Byte offset of the piece-record region (decode: kRecStride per mid-list entry) in the
+// class workspace, after the lists and the tile / window table.
+static uint64_t rec_region_off(uint32_t n) {
     // lists, serial list, then the tile table (encode) or the window table (decode)
     const uint64_t tiles = tile_tab_off(n) * sizeof(uint32_t) + 16 * ((uint64_t)n + kTileExtra);
     const uint64_t wins = win_tab_off(n) * sizeof(uint32_t) + sizeof(WinEnt) * win_cap(n);
-    return tiles > wins ? tiles : wins;
+    return ((tiles > wins ? tiles : wins) + 255) & ~255ull;
 }
+
+size_t queue_bytes(uint32_t n) { return rec_region_off(n) + (uint64_t)kRecStride * n; }
 
 // Resident blocks of a kernel across the device (hipOccupancy...), for persistent grids.
 template <typename K>
@@ -4097,10 +4141,11 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                              status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
+    uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
     decode_index_kernel<false><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4);
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4, rec);
     decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_len,
-                                                                       out_cap, status, mid, q + 4);
+                                                                       out_cap, status, mid, q + 4, rec);
     e = hipGetLastError();
     const hipError_t j = side.join();
     return e != hipSuccess ? e : j;

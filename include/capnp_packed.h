@@ -122,13 +122,17 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
  *
  * `stream` is a hipStream_t (NULL = default stream). Calls are asynchronous:
  * they enqueue kernels and return. The return value reports launch errors only;
- * per-unit results are in d_status / d_out_len. A unit whose status is an error
- * has unspecified slot contents (the reference returns no output for it).
+ * per-unit results are in d_status / d_out_len. A decode unit of more than 512
+ * packed bytes (or into a slot over 8 KiB) whose status is an error leaves its slot
+ * untouched (message.zig:88-145 returns the error before any output); a smaller one,
+ * and an encode unit that ends OUT_OF_SPACE, may hold a prefix (never a byte past
+ * its capacity). Run capnp_packed_decoded_size_batch first for all-or-nothing there.
  *
  * Workspace: encode / encoded_size / decode batches need a class workspace of
- * capnp_packed_batch_workspace_bytes(n) bytes (~32 B per unit + 1 MiB: the small / mid /
- * long unit lists, the per-block class counts, and the long-unit tile table of n + 65536
- * tiles that the tile-parallel long-unit encoder uses). The plain calls
+ * capnp_packed_batch_workspace_bytes(n) bytes (~750 B per unit + ~6 MiB: the small / mid /
+ * long unit lists, the per-block class counts, the long-unit tile / window table, and
+ * 704 B per unit of piece records for the indexed decoder, kept out of the caller's
+ * output slots). The plain calls
  * use a queue the library keeps per caller stream (made or grown on a batch larger
  * than any earlier one on that stream; growing is refused with DEVICE_ERROR inside
  * a hipGraph capture, and an old queue is never freed, so graphs that captured it

@@ -194,3 +194,36 @@ def test_more_windows_than_the_table_holds():
     assert (pst == 0).all().item() and int(plen.sum().item()) > 32768 * WIN
     assert (ust == 0).all().item() and torch.equal(ulen, in_len)
     assert torch.equal(d_out, d_in)
+
+
+def test_failures_beyond_the_window_table_write_nothing():
+    # as above (some units go to the serial decoder), with units cut one byte short
+    # (UNEXPECTED_EOF) and slots 8 B short (OUT_OF_SPACE): their slots keep the sentinel
+    n, ub = 6, 44 << 20
+    d_in = cp.generate(n, ub, seed=0xC0DE090A, zero_thresh=26, device=DEV)
+    in_off, in_len = cp.uniform_layout(n, ub, device=DEV)
+    slot = cp.encode_bound(ub)
+    pk_off, pk_cap = cp.uniform_layout(n, slot, device=DEV)
+    d_pk = torch.empty(n * slot, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_batch(d_in, in_off, in_len, d_pk, pk_off, pk_cap, plen, pst)
+    torch.cuda.synchronize()
+    assert (pst == 0).all().item() and int(plen.sum().item()) > 32768 * WIN
+    kind = [i % 3 for i in range(n)]  # 0 OK, 1 truncated, 2 slot too small
+    cut = torch.tensor([1 if k == 1 else 0 for k in kind], dtype=torch.int64, device=DEV)
+    short = torch.tensor([8 if k == 2 else 0 for k in kind], dtype=torch.int64, device=DEV)
+    d_out = torch.full((n * ub,), 0xA5, dtype=torch.uint8, device=DEV)
+    ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.decode_batch(d_pk, pk_off, plen - cut, d_out, in_off, in_len - short, ulen, ust)
+    torch.cuda.synchronize()
+    for i, k in enumerate(kind):
+        s = d_out[i * ub:(i + 1) * ub]
+        if k == 0:
+            assert ust[i].item() == cp.OK and ulen[i].item() == ub
+            assert torch.equal(s, d_in[i * ub:(i + 1) * ub])
+        else:
+            assert ust[i].item() == (cp.UNEXPECTED_EOF if k == 1 else cp.OUT_OF_SPACE)
+            assert ulen[i].item() == (0 if k == 1 else ub)
+            assert (s == 0xA5).all().item(), (i, k, "failed unit wrote into its slot")
