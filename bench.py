@@ -21,6 +21,9 @@ Run: python bench.py [--gpus N --steps K --warmup W]
      their status; under torchrun (WORLD_SIZE set) each process is one rank.
      --dry-run: the same launcher on the CPU (gloo), each rank packing a small shard
      with the oracle: checks the rank plumbing and the all-gather without a GPU.
+     --same-gpu: a rehearsal of the N-rank GPU step on a one-GPU box: every rank on
+     cuda:0 and gloo collectives over host copies (RCCL needs a GPU per rank). The
+     ranks share the card, so its `value` is not a scaling number.
 """
 import argparse
 import json
@@ -60,6 +63,8 @@ def parse():
     ap.add_argument("--no-dense", action="store_true", help="skip the dense packed-stream decode leg")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 bench-message leg")
     ap.add_argument("--dry-run", action="store_true", help="CPU (gloo) rehearsal of the multi-rank path")
+    ap.add_argument("--same-gpu", action="store_true",
+                    help="rehearsal on one GPU: all ranks on cuda:0, gloo collectives (not a scaling number)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory leg")
     ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
     ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
@@ -96,6 +101,10 @@ class Workload:
         return ok
 
 
+def _host_collectives():
+    return dist.is_initialized() and dist.get_backend() == "gloo"
+
+
 def time_steps(wl, steps, warmup, world, dev):
     stream = torch.cuda.current_stream()
     gathered = [torch.zeros(world, dtype=torch.int64, device=dev)]
@@ -109,8 +118,10 @@ def time_steps(wl, steps, warmup, world, dev):
         wl.decode(stream)
         if ev is not None:
             ev[2].record(stream)
-        # per-rank packed total -> RCCL all-gather (the only collective)
-        gathered[0] = sharding.gather_packed_totals(wl.plen.sum())
+        # per-rank packed total -> RCCL all-gather (the only collective);
+        # gloo (the --same-gpu rehearsal) gathers a host copy
+        total = wl.plen.sum()
+        gathered[0] = sharding.gather_packed_totals(total.cpu() if _host_collectives() else total)
 
     for _ in range(warmup):
         step()
@@ -127,7 +138,7 @@ def time_steps(wl, steps, warmup, world, dev):
     t1 = time.perf_counter()
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / steps
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cpu" if _host_collectives() else dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     return float(elapsed.item()), enc_ms, dec_ms, gathered[0]
@@ -759,7 +770,11 @@ def main():
         if args.units == 1 << 20:
             args.units = 64
         return dry_run(args, world, rank)
-    if world > 1:
+    if args.same_gpu:
+        local = 0
+    if world > 1 and args.same_gpu:
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if world > 1 else 0)
@@ -773,7 +788,7 @@ def main():
     n, ub = args.units, args.unit_bytes
     wl = Workload(n, ub, args.seed, args.zero_thresh, unit_base=rank * n, dev=dev)
     head = measure(wl, args, args.steps, args.warmup, world, dev)
-    ok_t = torch.tensor([1 if head["ok"] else 0], device=dev)
+    ok_t = torch.tensor([1 if head["ok"] else 0], device="cpu" if _host_collectives() else dev)
     if world > 1:
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
     packed_all = int(head["gathered"].sum().item())
@@ -861,6 +876,9 @@ def main():
             "bit_exact_roundtrip": bool(ok_t.item()),
         }
         line.update(extra)
+        if args.same_gpu and world > 1:
+            line["same_gpu_rehearsal"] = {"ranks": world, "devices": 1, "collectives": "gloo",
+                                          "note": "all ranks share cuda:0: checks the N-rank step, not a scaling number"}
         if world == 1 and not args.no_host_path:
             line["host_path"] = host_path(args, dev)
         if world == 1 and not args.no_cpu_baseline:
