@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 import oracle
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,3 +39,23 @@ def test_launcher_two_ranks_all_gather():
 def test_launcher_single_rank():
     res = _run("--units", "16", "--unit-bytes", "512")
     assert res["n_gpus"] == 1 and len(res["packed_totals"]) == 1
+
+
+@pytest.mark.gpu
+def test_same_gpu_rehearsal_two_ranks():
+    # the N-rank GPU step (bench.py --gpus 2 --same-gpu): both ranks code their own units
+    # on cuda:0 with the HIP library, bit-exact, and all-gather their packed totals; the
+    # gathered total must equal the oracle's over the same global units
+    n, ub, seed, thr = 512, 4096, 0xC0DE000A, 128
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--same-gpu",
+                          "--units", str(n), "--seed", str(seed), "--steps", "2", "--warmup", "1"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["bit_exact_roundtrip"] and res["same_gpu_rehearsal"]["devices"] == 1
+    data = oracle.generate(2 * n, ub, seed=seed, zero_thresh=thr)
+    total = sum(len(oracle.pack(data[i * ub:(i + 1) * ub].tobytes())[1]) for i in range(2 * n))
+    assert res["packed_total_all_ranks"] == total
