@@ -101,7 +101,8 @@ pub extern "capnp_packed" fn capnp_packed_validate_batch(
     segment_count_limit: u64, traversal_limit_words: u64, nesting_limit: u32,
     d_status: [*]i32, d_words: ?[*]u64, stream: ?*anyopaque,
 ) c_int;
-/// Long-unit workspace for the *_batch_ws calls (graph-safe batches with no shared state).
+/// Class workspace for the *_batch_ws calls (graph-safe batches with no shared state): unit
+/// lists, the long-unit tile / window table and the decoder's piece records (~750 B per unit).
 pub extern "capnp_packed" fn capnp_packed_batch_workspace_bytes(n: u32) usize;
 pub extern "capnp_packed" fn capnp_packed_encode_batch_ws(
     d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
