@@ -201,7 +201,11 @@ SIGNATURES = {
     "capnp_packed_frame_connections": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                                       ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                                       ctypes.POINTER(ctypes.c_uint32)]),
+    "capnp_packed_set_decoder": (ctypes.c_int, [ctypes.c_int]),
 }
+
+# capnp_packed_set_decoder values (include/capnp_packed.h)
+DECODERS = {"auto": 0, "twopass": 1, "fused": 2}
 
 
 def lib():
@@ -589,6 +593,30 @@ class PackedConnections:
 # ---------------------------------------------------------------------------
 # device-resident batch API (torch tensors in HBM)
 # ---------------------------------------------------------------------------
+
+def set_decoder(name: str) -> str:
+    """Select the mid-unit batch decoder ("auto", "twopass" or "fused"; every one is
+    bit-exact) for batches enqueued from now on; returns the previous setting's name."""
+    prev = lib().capnp_packed_set_decoder(DECODERS[name])
+    if prev < 0 or prev not in DECODERS.values():
+        _raise(prev, "set_decoder")
+    return {v: k for k, v in DECODERS.items()}[prev]
+
+
+class decoder:
+    """Context manager: `with decoder("fused"): ...` restores the previous decoder after."""
+
+    def __init__(self, name: str):
+        self.name, self.prev = name, None
+
+    def __enter__(self):
+        self.prev = set_decoder(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        set_decoder(self.prev)
+        return False
+
 
 def _ptr(t) -> int:
     return 0 if t is None else t.data_ptr()

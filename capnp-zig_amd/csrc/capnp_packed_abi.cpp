@@ -273,6 +273,12 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
 
 size_t capnp_packed_batch_workspace_bytes(uint32_t n) { return cpk::queue_bytes(n); }
 
+int capnp_packed_set_decoder(int decoder) {
+    if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_FUSED)
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "unknown decoder");
+    return cpk::set_decoder(decoder);
+}
+
 int capnp_packed_encode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                  uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
                                  uint64_t* d_out_len, int32_t* d_status, void* d_workspace, size_t workspace_bytes,

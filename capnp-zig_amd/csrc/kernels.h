@@ -20,6 +20,9 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
 
 size_t queue_bytes(uint32_t n);
 
+// capnp_packed_set_decoder: returns the previous setting
+int set_decoder(int decoder);
+
 // Reader.readPackedMessage over a batch of reader streams (reader.zig:84-156).
 hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,

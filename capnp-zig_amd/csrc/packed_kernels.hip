@@ -26,9 +26,11 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "capnp_packed.h"
@@ -2242,6 +2244,486 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------
+// DECODE, fused single pass (round 3): the packed bytes cross HBM once
+// and no piece records exist. One wave per unit, persistent grid, the next unit's pieces
+// prefetched into registers while this one is decoded (as decode_fill_kernel).
+//   stage  the unit's pieces go to the wave's LDS window at their 16-B aligned positions
+//          (unit byte 0 at window byte s = src & 15); the window past the unit, up to the
+//          end of the lanes' blocks (1024 L bytes, L pieces per lane) and 32 bytes beyond,
+//          is filled with 0x7F, a tag whose record is 8 bytes long: every lane then owns a
+//          whole block, and a record chain that reaches the unit's end continues through
+//          the fill 8 bytes at a time (lanes past the unit compose to the identity);
+//   map    lane k composes, over its block [16kL, 16(k+1)L), the map "state at the block
+//          start -> state at the block end" of the 8 chain states d = 0..7 (d = bytes to
+//          the next tag; a non-FF record is at most 8 bytes long, message.zig:101-141).
+//          A byte pair (b1, b2) maps d to [len(b1)-2, len(b2)-1, 0, 1, 2, 3, 4, 5][d]:
+//          two v_perm_b32 per pair for all 8 states, the source bytes from two 256-B LDS
+//          tables. An FF tag's length (10 + 8c) has no state: it maps to 0xFF, which
+//          v_perm keeps (a selector >= 13 gives 0xFF): "unknown";
+//   fix    a lane with unknown states and exactly one FF byte in its block: every unknown
+//          state reached that byte as a tag, so its exit is the exact walk from the FF
+//          record's landing (a landing more than 7 bytes past the block is "far": 0xFE);
+//   scan   a DPP prefix composition of the maps (6 steps, two v_perm each) gives every
+//          lane its entry state; lane 0's entry is s (a 0x7F tag at s - 8 when s >= 8);
+//   serial the first lane whose entry is unknown follows a lane whose own state there is
+//          far (its exit is known) or unresolved (several FF bytes: an exact walk from its
+//          entry); the scan restarts after the exit's lane (p = 0.5: ~0.4 per unit);
+//   count  each lane walks its records from its entry (exact): words and UnexpectedEof
+//          (a record running past the unit) before any output, as unpackPacked;
+//   codes, expansion: decode_fill_kernel's code walk and expansion.
+// Exactness does not depend on the data: every state the maps cannot carry is either
+// resolved exactly (fix) or walked (serial).
+constexpr uint32_t kFuWaves = 4;
+constexpr uint32_t kFuPk = kFlPieces * 16 + 32;  // 64 lanes x L <= 5 pieces + the 32-B 0x7F lookahead
+constexpr uint32_t kFuNone = 0xFFFFu;            // lane entry: no record starts in the lane's block
+constexpr uint32_t kFuFar = 0xFEu;               // map state: exit more than 7 bytes past the block
+constexpr uint32_t kFuIdLo = 0x03020100u, kFuIdHi = 0x07060504u;  // identity map
+constexpr uint32_t kFuOut = 512;   // output words per code pass (the code list)
+constexpr uint32_t kFuLoc = 16;    // records per lane the walk lists (u8 offsets in the lane's block)
+
+// Exact record walk (lengths of message.zig:152-191) from the tag at window position p to
+// the first record start at or past hi.
+__device__ __forceinline__ uint32_t fu_walk(const uint8_t* pk, uint32_t p, uint32_t hi) {
+    while (p < hi) {
+        uint32_t t = pk[p];
+        uint32_t c = pk[p + 9];
+        asm volatile("" : "+v"(t), "+v"(c));
+        p += 1u + __popc(t) + (uint32_t)((t == 0u) | (t == 0xFFu)) + (t == 0xFFu ? 8u * c : 0u);
+    }
+    return p;
+}
+
+// Inclusive prefix composition of 8-state maps over the wave (lane k: G_k o ... o G_0;
+// lanes a DPP step does not reach compose with the identity).
+__device__ __forceinline__ void fu_scan(uint32_t& lo, uint32_t& hi) {
+#define CPK_FU_STEP(CTRL, ROWS)                                                        \
+    {                                                                                  \
+        const uint32_t plo = dpp_mov<CTRL, ROWS>(lo, kFuIdLo);                         \
+        const uint32_t phi = dpp_mov<CTRL, ROWS>(hi, kFuIdHi);                         \
+        const uint32_t nlo = __builtin_amdgcn_perm(hi, lo, plo);                       \
+        hi = __builtin_amdgcn_perm(hi, lo, phi);                                       \
+        lo = nlo;                                                                      \
+    }
+    CPK_FU_STEP(0x111, 0xF);
+    CPK_FU_STEP(0x112, 0xF);
+    CPK_FU_STEP(0x114, 0xF);
+    CPK_FU_STEP(0x118, 0xF);
+    CPK_FU_STEP(0x142, 0xA);
+    CPK_FU_STEP(0x143, 0xC);
+#undef CPK_FU_STEP
+}
+
+// Lane l - 1's v (lane 0: 0), read with every lane active: the asm pins the DPP move (and
+// the computation of v) in front of any branch on the lane, since a DPP read of a lane the
+// EXEC mask excludes returns that lane's stale register.
+__device__ __forceinline__ uint32_t fu_prev_lane(uint32_t v) {
+    uint32_t r = dpp_mov<0x138, 0xF>(v, 0u);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+
+// The map of one dword of a lane's block (two byte pairs): d -> src[d], src = [TA[b1],
+// TB[b2], 0, 1 | 2, 3, 4, 5] with TA = len - 2, TB = len - 1 (0xFF for an FF byte).
+__device__ __forceinline__ void fu_map_dword(const uint8_t* tab, uint32_t w, uint32_t& mlo, uint32_t& mhi) {
+    uint32_t a = tab[w & 0xFFu];
+    uint32_t b = tab[256u + ((w >> 8) & 0xFFu)];
+    uint32_t src = (a | (b << 8)) | 0x01000000u;
+    mlo = __builtin_amdgcn_perm(0x05040302u, src, mlo);
+    mhi = __builtin_amdgcn_perm(0x05040302u, src, mhi);
+    a = tab[(w >> 16) & 0xFFu];
+    b = tab[256u + (w >> 24)];
+    src = (a | (b << 8)) | 0x01000000u;
+    mlo = __builtin_amdgcn_perm(0x05040302u, src, mlo);
+    mhi = __builtin_amdgcn_perm(0x05040302u, src, mhi);
+}
+
+// 0x80 in each byte of w that is 0xFF (exact per byte)
+__device__ __forceinline__ uint32_t fu_ff_bytes(uint32_t w) {
+    const uint32_t y = ~w;
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+
+__global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const uint8_t* __restrict__ in,
+                                                                        const uint64_t* __restrict__ in_off,
+                                                                        const uint64_t* __restrict__ in_len,
+                                                                        uint32_t n, uint8_t* __restrict__ out,
+                                                                        const uint64_t* __restrict__ out_off,
+                                                                        const uint64_t* __restrict__ out_cap,
+                                                                        uint64_t* __restrict__ out_len,
+                                                                        int32_t* __restrict__ status,
+                                                                        const uint32_t* __restrict__ list,
+                                                                        const uint32_t* __restrict__ list_count) {
+    __shared__ uint8_t tab[512];  // [0, 256): len - 2 of a tag, [256, 512): len - 1 (FF: 0xFF)
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFuWaves * kFuPk];
+    __shared__ __attribute__((aligned(16))) uint16_t code_all[kFuWaves * (kFuOut + 8)];  // + a dummy slot
+    __shared__ __attribute__((aligned(16))) uint8_t rl_all[kFuWaves * (kWave * kFuLoc + 16)];  // + a dummy row
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    {
+        const uint32_t b = threadIdx.x;  // 256 threads: one table entry each
+        const uint32_t lm1 = max((uint32_t)__popc(b), 1u);  // 00 -> 2-byte record
+        tab[b] = (uint8_t)(b == 0xFFu ? 0xFFu : lm1 - 1u);
+        tab[256u + b] = (uint8_t)(b == 0xFFu ? 0xFFu : lm1);
+        lut[b] = expand_selector(b);
+    }
+    __syncthreads();
+    uint8_t* const pk = pk_all + wave * kFuPk;
+    uint4* const pk4 = reinterpret_cast<uint4*>(pk);
+    uint16_t* const code = code_all + wave * (kFuOut + 8);
+    uint8_t* const rl = rl_all + wave * (kWave * kFuLoc + 16);  // lane l's record list at rl[16 l ..]
+    const uint32_t G = gridDim.x * kFuWaves;
+    const uint32_t u0 = blockIdx.x * kFuWaves + wave;
+    const uint32_t n_all = n;
+    if (list) n = *list_count;
+    if (u0 >= n) return;
+    if (n == n_all) list = nullptr;  // every unit is listed: batch order
+
+    // per-unit values of the wave's units k0 .. k0+63 (lane i: unit k0 + i)
+    uint64_t m_in = 0, m_out = 0, m_cap = 0;
+    uint32_t m_P = 0, m_unit = 0xFFFFFFFFu;
+    auto load_batch = [&](uint32_t k0) {
+        const uint64_t slot = (uint64_t)u0 + (uint64_t)(k0 + lane) * G;
+        m_unit = 0xFFFFFFFFu;
+        if (slot < n) {
+            const uint32_t uu = list ? list[slot] : (uint32_t)slot;
+            m_unit = uu;
+            m_in = in_off[uu];
+            m_P = (uint32_t)in_len[uu];  // mid units: <= kFlPieces * 16 bytes
+            m_out = out_off[uu];
+            m_cap = out_cap[uu];
+        }
+    };
+    struct FuMeta {
+        uint32_t unit, P;
+        const uint8_t* src;
+        uint8_t* dst;
+        uint64_t cap;
+    };
+    auto meta = [&](uint32_t j) {
+        FuMeta m;
+        m.unit = readlane(m_unit, j);
+        m.P = readlane(m_P, j);
+        m.src = in + ((uint64_t)readlane((uint32_t)m_in, j) | ((uint64_t)readlane((uint32_t)(m_in >> 32), j) << 32));
+        m.dst = out + ((uint64_t)readlane((uint32_t)m_out, j) | ((uint64_t)readlane((uint32_t)(m_out >> 32), j) << 32));
+        m.cap = (uint64_t)readlane((uint32_t)m_cap, j) | ((uint64_t)readlane((uint32_t)(m_cap >> 32), j) << 32);
+        return m;
+    };
+    auto runnable = [&](const FuMeta& m) {  // wave-uniform
+        return m.unit != 0xFFFFFFFFu && m.P > 0 && !(reinterpret_cast<uintptr_t>(m.dst) & 7);
+    };
+    uint4 v0, v1, v2, v3, v4;
+    auto load_unit = [&](const FuMeta& m) {
+        if (!runnable(m)) return;
+        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(m.src) & 15);
+        const uint4* const b = reinterpret_cast<const uint4*>(m.src - s);
+        const uint32_t np = (s + m.P + 15) >> 4;
+        const uint32_t last = np - 1;
+        v0 = load_nt(b + min(lane, last));
+        if (np > 64) v1 = load_nt(b + min(lane + 64, last));
+        if (np > 128) v2 = load_nt(b + min(lane + 128, last));
+        if (np > 192) v3 = load_nt(b + min(lane + 192, last));
+        if (np > 256) v4 = load_nt(b + min(lane + 256, last));
+    };
+
+    load_batch(0);
+    FuMeta cur = meta(0);
+    load_unit(cur);
+    uint32_t younger = 0;  // vector-memory ops issued after cur's loads (its predecessor's stores)
+#ifdef CPK_FILL_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    for (uint32_t k = 0; (uint64_t)u0 + (uint64_t)k * G < n; ++k) {
+        const bool go = runnable(cur);
+        FL_T(t0);
+        vmcnt_at_most(younger);  // cur's pieces are in registers
+        FL_T(t1);
+        FL_ACC(0, t1 - t0);
+        younger = 0;
+        uint32_t s = 0, end = 0, L = 0;
+        if (go) {
+            s = (uint32_t)(reinterpret_cast<uintptr_t>(cur.src) & 15);
+            end = s + cur.P;
+            const uint32_t np = (end + 15) >> 4;  // <= kFlPieces (a mid unit)
+            L = (np + 63) >> 6;
+            wave_lds_sync();  // the previous unit's LDS reads are done
+            // ---- stage: pieces, 0x7F past the unit up to 1024 L (+ 32 B) -----------------
+            const uint4 f7 = make_uint4(0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu);
+            const uint32_t keep = end - 16 * (np - 1);  // unit bytes in the last piece (1..16)
+            auto put = [&](uint32_t m, uint4 v) {
+                const uint32_t pc = lane + 64 * m;
+                if (pc >= np) v = f7;
+                else if (pc == np - 1 && keep < 16) {  // bytes [keep, 16) of the last piece -> 0x7F
+                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        const uint32_t lo = 4 * i;
+                        const uint32_t mask = keep <= lo ? 0u : (keep >= lo + 4 ? 0xFFFFFFFFu : (1u << (8 * (keep - lo))) - 1u);
+                        w[i] = (w[i] & mask) | (0x7F7F7F7Fu & ~mask);
+                    }
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                pk4[pc] = v;
+            };
+            put(0, v0);
+            if (L > 1) put(1, v1);
+            if (L > 2) put(2, v2);
+            if (L > 3) put(3, v3);
+            if (L > 4) put(4, v4);
+            if (lane < 2) pk4[64 * L + lane] = f7;  // lookahead of the last block's records
+            wave_lds_sync();
+            if (lane == 0 && s >= 8) pk[s - 8] = 0x7F;  // lane 0 enters at s & 7: an 8-byte record to s
+            wave_lds_sync();
+        }
+        // the next unit's loads go out before any work or store of this unit
+        const uint32_t k1 = k + 1;
+        if ((k1 & 63) == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            load_batch(k1);
+        }
+        const FuMeta nxt = meta(k1 & 63);
+        load_unit(nxt);
+        FL_T(t2);
+        FL_ACC(1, t2 - t1);
+        if (cur.unit != 0xFFFFFFFFu && !go) {  // empty unit, or a misaligned output slot
+            if (lane == 0) {
+                out_len[cur.unit] = 0;
+                status[cur.unit] = cur.P == 0 ? ST_OK : ST_ARG;
+            }
+            younger += 2;
+        }
+        if (go) {
+            const uint32_t blk = 16 * L;          // block bytes per lane
+            const uint32_t lo = lane * blk, hi = lo + blk;
+            // ---- map -----------------------------------------------------------------
+            uint32_t mlo = kFuIdLo, mhi = kFuIdHi;
+            const uint4* const bp = pk4 + lane * L;
+            uint32_t um = 0, nchg = 0, jst = 0;  // unknown states, pieces that changed them, the last one
+#pragma unroll
+            for (uint32_t j = 0; j < kFlMaxL; ++j) {
+                if (j < L) {
+                    const uint4 d = bp[j];
+                    fu_map_dword(tab, d.x, mlo, mhi);
+                    fu_map_dword(tab, d.y, mlo, mhi);
+                    fu_map_dword(tab, d.z, mlo, mhi);
+                    fu_map_dword(tab, d.w, mlo, mhi);
+                    const uint32_t u2 = (mlo & 0x80808080u) | ((mhi & 0x80808080u) >> 1);  // unknown lo / hi states
+                    nchg += u2 != um ? 1u : 0u;
+                    jst = u2 != um ? j : jst;
+                    um = u2;
+                }
+            }
+            FL_T(t3);
+            FL_ACC(2, t3 - t2);
+            // ---- fix: unknown states that all appeared in one piece with one FF byte ----------
+            // (then each of them reached that byte as a tag; otherwise they stay unresolved)
+            uint32_t farx = 0;
+            const bool unk = um != 0;
+            if (__builtin_amdgcn_ballot_w64(unk) != 0 && unk && nchg == 1) {
+                const uint4 d = bp[jst];
+                const uint32_t f4[4] = {fu_ff_bytes(d.x), fu_ff_bytes(d.y), fu_ff_bytes(d.z), fu_ff_bytes(d.w)};
+                uint32_t J = 0, x = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    if (J == 0 && f4[i]) x = lo + 16 * jst + 4 * i + (__builtin_ctz(f4[i]) >> 3);
+                    J += __popc(f4[i]);
+                }
+                if (J == 1) {
+                    const uint32_t X = fu_walk(pk, x + 10u + 8u * pk[x + 9], hi);
+                    farx = X;
+                    const uint32_t st = X - hi <= 7u ? X - hi : kFuFar;
+                    const uint32_t um_lo = ((mlo & 0x80808080u) >> 7) * 0xFFu;  // unknown bytes
+                    const uint32_t um_hi = ((mhi & 0x80808080u) >> 7) * 0xFFu;
+                    mlo = (mlo & ~um_lo) | (st * 0x01010101u & um_lo);
+                    mhi = (mhi & ~um_hi) | (st * 0x01010101u & um_hi);
+                }
+            }
+            FL_T(t4);
+            FL_ACC(3, t4 - t3);
+            // ---- scan: entry state of every lane ---------------------------------------------
+            const uint32_t e0 = s & 7u;
+            uint32_t glo = mlo, ghi = mhi;
+            if (lane == 0) glo = ghi = (__builtin_amdgcn_perm(mhi, mlo, e0) & 0xFFu) * 0x01010101u;
+            fu_scan(glo, ghi);
+            uint32_t eoff = fu_prev_lane(glo) & 0xFFu;  // entry state
+            if (lane == 0) eoff = e0;
+            uint32_t ent = lane == 0 ? s : (eoff <= 7u ? lo + eoff : kFuNone);
+            // ---- serial: lanes behind an unresolved or far state ---------------------------
+            uint64_t badm = __builtin_amdgcn_ballot_w64(lane > 0 && eoff > 7u);
+            while (badm) {
+                uint32_t kb = (uint32_t)__builtin_ctzll(badm) - 1u;  // entry known, exit not
+                uint32_t mv = __builtin_amdgcn_perm(mhi, mlo, eoff);
+                asm volatile("" : "+v"(mv));  // computed by every lane before lane kb's is read
+                const uint32_t v = readlane(mv, kb) & 0xFFu;
+                uint32_t X = v == kFuFar ? readlane(farx, kb) : fu_walk(pk, readlane(ent, kb), (kb + 1) * blk);
+                badm = 0;
+                for (;;) {  // place the exit X: the lane it enters, or the unit's end
+                    const uint32_t j = X / blk;
+                    if (j >= 64u || X >= end) {  // no record starts in lanes kb+1 ..
+                        if (lane > kb) ent = kFuNone;
+                        break;
+                    }
+                    if (lane > kb && lane < j) ent = kFuNone;  // blocks the record jumps over
+                    const uint32_t f = X - j * blk;
+                    if (lane == j) ent = X;
+                    if (f > 7u) {  // deep into lane j's block: walk it
+                        X = fu_walk(pk, X, (j + 1) * blk);
+                        kb = j;
+                        continue;
+                    }
+                    // restart the scan after lane j: lane j's map applied to f
+                    uint32_t rlo = lane < j ? kFuIdLo : mlo, rhi = lane < j ? kFuIdHi : mhi;
+                    if (lane == j) rlo = rhi = (__builtin_amdgcn_perm(mhi, mlo, f) & 0xFFu) * 0x01010101u;
+                    fu_scan(rlo, rhi);
+                    const uint32_t eb = fu_prev_lane(rlo) & 0xFFu;
+                    if (lane == j) eoff = f;
+                    if (lane > j) {
+                        eoff = eb;
+                        ent = eb <= 7u ? lo + eb : kFuNone;
+                    }
+                    badm = __builtin_amdgcn_ballot_w64(lane > j && eb > 7u);
+                    break;
+                }
+            }
+            FL_T(t5);
+            FL_ACC(4, t5 - t4);
+            // ---- walk: the lane's records from its entry (exact), one per pass: words,
+            //      UnexpectedEof, and each record's offset in the lane's block in its list
+            //      (rl: kFuLoc u8 per lane; a lane with more records takes the code walk) ---------
+            const uint32_t lim = min(hi, end);
+            const uint32_t pos = ent == kFuNone ? lim : ent;
+            uint32_t words = 0, ne = 0;
+            bool eof = false;
+            {
+                uint32_t p = pos;
+                for (;;) {  // one record per lane per pass; predicated body, uniform exit
+                    const bool act = p < lim;
+                    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                    const uint32_t pp = act ? p : 0u;
+                    uint32_t t = pk[pp];
+                    uint32_t b1 = pk[pp + 1];
+                    uint32_t c9 = pk[pp + 9];
+                    asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                    const bool z = t == 0u, f = t == 0xFFu;
+                    const uint32_t len = 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u);
+                    rl[(act && ne < kFuLoc) ? kFuLoc * lane + ne : kWave * kFuLoc] = (uint8_t)(pp - lo);
+                    ne += act ? 1u : 0u;
+                    eof = eof || (act && p + len > end);  // message.zig:152-191
+                    words += act ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
+                    p = act ? p + len : p;
+                }
+            }
+            const bool any_eof = __builtin_amdgcn_ballot_w64(eof) != 0;
+            const bool ovf = __builtin_amdgcn_ballot_w64(ne > kFuLoc) != 0;  // a list overflowed: code walk
+            FL_T(t6);
+            FL_ACC(5, t6 - t5);
+            const uint32_t incl = wave_incl_sum(words, lane);
+            const uint32_t T = readlane(incl, kWave - 1);
+            const uint32_t wbase = incl - words;
+            int32_t st = ST_OK;
+            if (any_eof) st = ST_EOF;
+            else if (8ull * T > cur.cap) st = ST_SPACE;
+            if (st == ST_OK) {
+                const bool a16 = !(reinterpret_cast<uintptr_t>(cur.dst) & 15);
+                uint64_t* const dst = reinterpret_cast<uint64_t*>(cur.dst);
+                const uint32_t nl = min(ne, kFuLoc);
+                for (uint32_t W0 = 0; W0 < T; W0 += kFuOut) {
+                    const uint32_t W1 = min(T, W0 + kFuOut);
+                    wave_lds_sync();
+                    reinterpret_cast<uint4*>(code)[lane] = make_uint4(kFlZero * 0x10001u, kFlZero * 0x10001u,
+                                                                      kFlZero * 0x10001u, kFlZero * 0x10001u);
+                    wave_lds_sync();
+                    if (!ovf) {
+                        // ---- codes from the list: a tag position per output word (zero words keep
+                        //      kFlZero; an FF run's body words are literal codes). The list gives every
+                        //      record's position, so the passes do not depend on each other ------------
+                        uint32_t w = wbase;
+                        for (uint32_t i = 0;; ++i) {
+                            const bool act = i < nl && w < W1;
+                            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                            const uint32_t e = lo + rl[kFuLoc * lane + min(i, kFuLoc - 1)];
+                            uint32_t t = pk[e];
+                            uint32_t b1 = pk[e + 1];
+                            uint32_t c9 = pk[e + 9];
+                            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                            const bool z = t == 0u, f = t == 0xFFu;
+                            code[(act && !z && w >= W0) ? w - W0 : kFuOut] = (uint16_t)e;
+                            const uint32_t c = f ? c9 : 0u;
+                            if (act && c) {
+                                for (uint32_t j = 1; j <= c; ++j) {
+                                    const uint32_t wi = w + j;
+                                    if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (e + 1 + 8 * j));
+                                }
+                            }
+                            w += act ? 1u + (z ? b1 : 0u) + c : 0u;
+                        }
+                    } else {
+                        // ---- code walk (decode_fill_kernel) ------------------------------------------
+                        const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
+                        uint32_t p = mine ? pos : lim, w = wbase;
+                        for (;;) {
+                            const bool act = p < lim && w < W1;
+                            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                            const uint32_t pp = act ? p : 0u;
+                            uint32_t t = pk[pp];
+                            uint32_t b1 = pk[pp + 1];
+                            uint32_t c9 = pk[pp + 9];
+                            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                            const bool z = t == 0u, f = t == 0xFFu;
+                            code[(act && !z && w >= W0) ? w - W0 : kFuOut] = (uint16_t)pp;
+                            const uint32_t c = f ? c9 : 0u;
+                            if (act && c) {
+                                for (uint32_t i = 1; i <= c; ++i) {
+                                    const uint32_t wi = w + i;
+                                    if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (pp + 1 + 8 * i));
+                                }
+                            }
+                            w = act ? w + 1u + (z ? b1 : 0u) + c : w;
+                            p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
+                        }
+                    }
+                    wave_lds_sync();
+                    FL_T(t7);
+                    FL_ACC(6, t7 - t6);
+                    // ---- expand by output word: coalesced stores -----------------------------------
+                    const uint32_t nw = W1 - W0;
+                    if (a16) {
+                        for (uint32_t i = 2 * lane; i < nw; i += 2 * kWave) {
+                            const uint32_t cc = *reinterpret_cast<const uint32_t*>(code + i);
+                            const uint64_t x0 = fill_word(pk, lut, cc & 0xFFFFu);
+                            const uint64_t x1 = fill_word(pk, lut, cc >> 16);
+                            if (i + 1 < nw) {
+                                const u32x4 vv = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
+                                __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(dst + W0 + i));
+                            } else {
+                                dst[W0 + i] = x0;
+                            }
+                        }
+                        younger += (nw + 2 * kWave - 1) / (2 * kWave);
+                    } else {
+                        for (uint32_t i = lane; i < nw; i += kWave) dst[W0 + i] = fill_word(pk, lut, code[i]);
+                        younger += (nw + kWave - 1) / kWave;
+                    }
+                    FL_T(t8);
+                    FL_ACC(7, t8 - t7);
+                }
+            }
+            if (lane == 0) {
+                out_len[cur.unit] = st == ST_EOF ? 0ull : 8ull * T;
+                status[cur.unit] = st;
+            }
+            younger += 2;  // the two stores above (one wave instruction each)
+        }
+        cur = nxt;
+    }
+#ifdef CPK_FILL_PROF
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ---- size classes ------------------------------------------------
 // A batch's units are split by size before the coding kernels run, so each kernel gets
 // units of the shape it is built for:
@@ -4101,6 +4583,22 @@ static uint32_t fallback_blocks(uint32_t n) {
     return full < 2048u ? full : 2048u;
 }
 
+// Mid-unit decoder (capnp_packed_set_decoder; CPK_DECODE=twopass|fused sets the start value).
+static std::atomic<int>& decoder_setting() {
+    static std::atomic<int> v([] {
+        const char* e = getenv("CPK_DECODE");
+        if (e && std::string(e) == "fused") return (int)CAPNP_PACKED_DECODER_FUSED;
+        if (e && std::string(e) == "twopass") return (int)CAPNP_PACKED_DECODER_TWO_PASS;
+        return (int)CAPNP_PACKED_DECODER_AUTO;
+    }());
+    return v;
+}
+static int decoder_variant() {
+    const int v = decoder_setting().load(std::memory_order_relaxed);
+    return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
+}
+int set_decoder(int v) { return decoder_setting().exchange(v); }
+
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream) {
@@ -4141,11 +4639,20 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                              status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
-    uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
-    decode_index_kernel<false><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(
-        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4, rec);
-    decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_len,
-                                                                       out_cap, status, mid, q + 4, rec);
+    // mid units: the fused single-pass decoder; CPK_DECODE=twopass selects the indexed
+    // two-pass decoder (index pass + fill pass) for same-box A/B runs
+    if (decoder_variant() == CAPNP_PACKED_DECODER_FUSED) {
+        static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);
+        const uint32_t fu_blocks = std::min((n + kFuWaves - 1) / kFuWaves, fu_res);
+        decode_fused_kernel<<<fu_blocks, kFuWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                        out_len, status, mid, q + 4);
+    } else {
+        uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
+        decode_index_kernel<false><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(
+            in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4, rec);
+        decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                           out_len, out_cap, status, mid, q + 4, rec);
+    }
     e = hipGetLastError();
     const hipError_t j = side.join();
     return e != hipSuccess ? e : j;

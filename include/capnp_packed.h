@@ -284,6 +284,20 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
                           uint64_t unit_base, uint64_t seed, uint32_t zero_thresh,
                           void* stream);
 
+/* Decoder selection for the batch decode of mid-size units (a tuning knob, not a
+ * semantic one: every decoder is bit-exact):
+ *   CAPNP_PACKED_DECODER_TWO_PASS  index pass + fill pass (the packed bytes are read twice);
+ *   CAPNP_PACKED_DECODER_FUSED     single pass: per-lane 8-state entry maps, one read;
+ *   CAPNP_PACKED_DECODER_AUTO      the library's default.
+ * The environment variable CPK_DECODE=twopass|fused sets the initial value. Returns the
+ * previous value; applies to batches enqueued after the call (process-wide). */
+enum {
+    CAPNP_PACKED_DECODER_AUTO = 0,
+    CAPNP_PACKED_DECODER_TWO_PASS = 1,
+    CAPNP_PACKED_DECODER_FUSED = 2
+};
+int capnp_packed_set_decoder(int decoder);
+
 #ifdef __cplusplus
 }
 #endif

@@ -88,7 +88,7 @@ def test_no_cpu_fallback_without_device():
 def header_statuses():
     text = open(HEADER).read()
     return {name: int(v) for name, v in re.findall(r"CAPNP_PACKED_(\w+)\s*=\s*(\d+)", text)
-            if name != "ABI_VERSION"}
+            if name != "ABI_VERSION" and not name.startswith("DECODER_")}
 
 
 def test_status_tables_agree():
@@ -103,6 +103,16 @@ def test_status_tables_agree():
     zig = open(os.path.join(REPO, "zig", "packed_ffi.zig")).read()
     zig_enum = dict((n, int(v)) for n, v in re.findall(r"^\s+(\w+) = (\d+),$", zig, flags=re.M))
     assert {k.lower(): v for k, v in st.items()} == zig_enum
+
+
+def test_decoder_selection_round_trips():
+    # capnp_packed_set_decoder is a process-wide knob (no device needed to set it)
+    prev = cp.set_decoder("fused")
+    assert cp.set_decoder("twopass") == "fused"
+    with cp.decoder("fused"):
+        assert cp.set_decoder("fused") == "fused"
+    assert cp.set_decoder(prev) == "twopass"
+    assert cp.lib().capnp_packed_set_decoder(7) == cp.INVALID_ARGUMENT
 
 
 def test_zig_binding_declares_only_header_symbols():

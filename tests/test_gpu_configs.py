@@ -17,6 +17,13 @@ import pyref
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["twopass", "fused"])
+def decoder(request):
+    """Runs the test under each mid-unit decoder (capnp_packed_set_decoder)."""
+    with cp.decoder(request.param):
+        yield request.param
 DEV = "cuda"
 
 
@@ -40,7 +47,7 @@ def test_c1_64_segment_message_single_buffer():
     assert cp.Reader.read_packed_message(packed + b"\x00") == framed
 
 
-def test_c1_batch_of_messages():
+def test_c1_batch_of_messages(decoder):
     """64 C1 messages (different seeds) through the batch entry points."""
     msgs = [pyref.frame(c1_segments(0xC0DE0100 + k)) for k in range(64)]
     ub = len(msgs[0])
@@ -71,7 +78,7 @@ def pareto_sizes(n, seed):
 
 
 @pytest.mark.parametrize("thr", [26, 128, 230])
-def test_c5_skewed_sizes_every_unit(thr):
+def test_c5_skewed_sizes_every_unit(thr, decoder):
     sizes = pareto_sizes(3000, seed=0xC0DE0005 + thr)
     # units around and far beyond the 512-word tile, and both size extremes
     extra = [4088, 4096, 4104, 8192, 12288 + 8, 65536, 262144, 64, 8]
@@ -111,7 +118,7 @@ def test_c5_skewed_sizes_every_unit(thr):
     assert np.array_equal(d_out.cpu().numpy()[:U], host)
 
 
-def test_c5_full_size_1M_units():
+def test_c5_full_size_1M_units(decoder):
     """BASELINE configs[4] at its stated size: 1M units of truncated-Pareto sizes
     64 B..256 KiB (the bench's seed), p = 0.5. decode(encode(x)) == x on device for
     every unit; every unit over 64 KiB and a strided sample of the rest byte-compared

@@ -23,6 +23,13 @@ import oracle
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["twopass", "fused"])
+def decoder(request):
+    """Runs the test under each mid-unit decoder (capnp_packed_set_decoder)."""
+    with cp.decoder(request.param):
+        yield request.param
 DEV = "cuda"
 SENTINEL = 0xA5
 
@@ -39,7 +46,7 @@ def words(rng, n_words, thr):
 
 
 @pytest.mark.parametrize("cls,n_words,thr", CLASSES, ids=[c[0] for c in CLASSES])
-def test_failed_units_leave_their_slot_untouched(cls, n_words, thr):
+def test_failed_units_leave_their_slot_untouched(cls, n_words, thr, decoder):
     rng = np.random.default_rng(0xC0DE + n_words)
     n = 384
     data = [words(rng, n_words, thr) for _ in range(n)]

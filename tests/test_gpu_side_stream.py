@@ -23,6 +23,13 @@ import oracle
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["twopass", "fused"])
+def decoder(request):
+    """Runs the test under each mid-unit decoder (capnp_packed_set_decoder)."""
+    with cp.decoder(request.param):
+        yield request.param
 DEV = "cuda"
 
 
@@ -96,7 +103,7 @@ def test_side_stream_on_caller_stream():
 
 
 @pytest.mark.parametrize("thr", [26, 128, 230])
-def test_back_to_back_batches(thr):
+def test_back_to_back_batches(thr, decoder):
     # three batches, launched without synchronisation in between: each batch resets the
     # shared queue on the side stream after the previous batch's workers
     bs = [Batch(mixed_sizes(n, 10 + k, long_every=le), seed=0xC0DE0200 + k, thr=thr)
@@ -120,7 +127,7 @@ def test_no_long_units_and_only_long_units():
     only.check_oracle(range(64))
 
 
-def test_graph_capture_replay():
+def test_graph_capture_replay(decoder):
     b = Batch(mixed_sizes(1500, 3), seed=0xC0DE0401)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
