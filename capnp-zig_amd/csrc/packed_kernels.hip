@@ -2276,11 +2276,11 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 // resolved exactly (fix) or walked (serial).
 constexpr uint32_t kFuWaves = 4;
 constexpr uint32_t kFuPk = kFlPieces * 16 + 32;  // 64 lanes x L <= 5 pieces + the 32-B 0x7F lookahead
-constexpr uint32_t kFuNone = 0xFFFFu;            // lane entry: no record starts in the lane's block
 constexpr uint32_t kFuFar = 0xFEu;               // map state: exit more than 7 bytes past the block
 constexpr uint32_t kFuIdLo = 0x03020100u, kFuIdHi = 0x07060504u;  // identity map
 constexpr uint32_t kFuOut = 512;   // output words per code pass (the code list)
 constexpr uint32_t kFuLoc = 16;    // records per lane the walk lists (u8 offsets in the lane's block)
+constexpr uint32_t kFuRow = kFuLoc + 1;  // + the slot the records past kFuLoc overwrite
 
 // Exact record walk (lengths of message.zig:152-191) from the tag at window position p to
 // the first record start at or past hi.
@@ -2357,7 +2357,7 @@ __global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const ui
     __shared__ uint8_t tab[512];  // [0, 256): len - 2 of a tag, [256, 512): len - 1 (FF: 0xFF)
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFuWaves * kFuPk];
     __shared__ __attribute__((aligned(16))) uint16_t code_all[kFuWaves * (kFuOut + 8)];  // + a dummy slot
-    __shared__ __attribute__((aligned(16))) uint8_t rl_all[kFuWaves * (kWave * kFuLoc + 16)];  // + a dummy row
+    __shared__ __attribute__((aligned(16))) uint8_t rl_all[kFuWaves * kWave * kFuRow];
     __shared__ uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2372,7 +2372,7 @@ __global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const ui
     uint8_t* const pk = pk_all + wave * kFuPk;
     uint4* const pk4 = reinterpret_cast<uint4*>(pk);
     uint16_t* const code = code_all + wave * (kFuOut + 8);
-    uint8_t* const rl = rl_all + wave * (kWave * kFuLoc + 16);  // lane l's record list at rl[16 l ..]
+    uint8_t* const rl = rl_all + wave * (kWave * kFuRow);  // lane l's record list at rl[kFuRow l ..]
     const uint32_t G = gridDim.x * kFuWaves;
     const uint32_t u0 = blockIdx.x * kFuWaves + wave;
     const uint32_t n_all = n;
@@ -2541,80 +2541,61 @@ __global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const ui
             }
             FL_T(t4);
             FL_ACC(3, t4 - t3);
-            // ---- scan: entry state of every lane ---------------------------------------------
+            // ---- scan: a speculative entry for every lane ------------------------------------
+            // A state the maps could not resolve (several FF bytes, or an exit more than 7 bytes
+            // past the block) is guessed as 7; the record walks below verify every entry.
+            {
+                const uint32_t hm_lo = ((mlo & 0x80808080u) >> 7) * 0xFFu;
+                const uint32_t hm_hi = ((mhi & 0x80808080u) >> 7) * 0xFFu;
+                mlo = (mlo & ~hm_lo) | (0x07070707u & hm_lo);
+                mhi = (mhi & ~hm_hi) | (0x07070707u & hm_hi);
+            }
             const uint32_t e0 = s & 7u;
             uint32_t glo = mlo, ghi = mhi;
             if (lane == 0) glo = ghi = (__builtin_amdgcn_perm(mhi, mlo, e0) & 0xFFu) * 0x01010101u;
             fu_scan(glo, ghi);
-            uint32_t eoff = fu_prev_lane(glo) & 0xFFu;  // entry state
-            if (lane == 0) eoff = e0;
-            uint32_t ent = lane == 0 ? s : (eoff <= 7u ? lo + eoff : kFuNone);
-            // ---- serial: lanes behind an unresolved or far state ---------------------------
-            uint64_t badm = __builtin_amdgcn_ballot_w64(lane > 0 && eoff > 7u);
-            while (badm) {
-                uint32_t kb = (uint32_t)__builtin_ctzll(badm) - 1u;  // entry known, exit not
-                uint32_t mv = __builtin_amdgcn_perm(mhi, mlo, eoff);
-                asm volatile("" : "+v"(mv));  // computed by every lane before lane kb's is read
-                const uint32_t v = readlane(mv, kb) & 0xFFu;
-                uint32_t X = v == kFuFar ? readlane(farx, kb) : fu_walk(pk, readlane(ent, kb), (kb + 1) * blk);
-                badm = 0;
-                for (;;) {  // place the exit X: the lane it enters, or the unit's end
-                    const uint32_t j = X / blk;
-                    if (j >= 64u || X >= end) {  // no record starts in lanes kb+1 ..
-                        if (lane > kb) ent = kFuNone;
-                        break;
-                    }
-                    if (lane > kb && lane < j) ent = kFuNone;  // blocks the record jumps over
-                    const uint32_t f = X - j * blk;
-                    if (lane == j) ent = X;
-                    if (f > 7u) {  // deep into lane j's block: walk it
-                        X = fu_walk(pk, X, (j + 1) * blk);
-                        kb = j;
-                        continue;
-                    }
-                    // restart the scan after lane j: lane j's map applied to f
-                    uint32_t rlo = lane < j ? kFuIdLo : mlo, rhi = lane < j ? kFuIdHi : mhi;
-                    if (lane == j) rlo = rhi = (__builtin_amdgcn_perm(mhi, mlo, f) & 0xFFu) * 0x01010101u;
-                    fu_scan(rlo, rhi);
-                    const uint32_t eb = fu_prev_lane(rlo) & 0xFFu;
-                    if (lane == j) eoff = f;
-                    if (lane > j) {
-                        eoff = eb;
-                        ent = eb <= 7u ? lo + eb : kFuNone;
-                    }
-                    badm = __builtin_amdgcn_ballot_w64(lane > j && eb > 7u);
-                    break;
-                }
-            }
+            uint32_t E = lo + (fu_prev_lane(glo) & 0xFFu);  // entry: the first record start in the block
+            if (lane == 0) E = s;
+            (void)farx;
             FL_T(t5);
             FL_ACC(4, t5 - t4);
-            // ---- walk: the lane's records from its entry (exact), one per pass: words,
-            //      UnexpectedEof, and each record's offset in the lane's block in its list
-            //      (rl: kFuLoc u8 per lane; a lane with more records takes the code walk) ---------
+            // ---- walk + verify: each lane walks its records from its entry (exact), one per pass:
+            //      words, and each record's offset in the lane's block in its list (rl: kFuLoc u8
+            //      per lane; a lane with more records takes the code walk below). A lane's entry is
+            //      right iff it equals the furthest exit of the lanes before it (lane 0's is); the
+            //      lanes whose entry was wrong take that exit and walk again. -----------------------
             const uint32_t lim = min(hi, end);
-            const uint32_t pos = ent == kFuNone ? lim : ent;
-            uint32_t words = 0, ne = 0;
-            bool eof = false;
-            {
-                uint32_t p = pos;
-                for (;;) {  // one record per lane per pass; predicated body, uniform exit
-                    const bool act = p < lim;
-                    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                    const uint32_t pp = act ? p : 0u;
-                    uint32_t t = pk[pp];
-                    uint32_t b1 = pk[pp + 1];
-                    uint32_t c9 = pk[pp + 9];
-                    asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                    const bool z = t == 0u, f = t == 0xFFu;
-                    const uint32_t len = 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u);
-                    rl[(act && ne < kFuLoc) ? kFuLoc * lane + ne : kWave * kFuLoc] = (uint8_t)(pp - lo);
-                    ne += act ? 1u : 0u;
-                    eof = eof || (act && p + len > end);  // message.zig:152-191
-                    words += act ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
-                    p = act ? p + len : p;
+            uint8_t* const rll = rl + kFuRow * lane;
+            uint32_t words = 0, ne = 0, p = E;
+            for (;;) {
+                for (;;) {  // one record per lane per pass
+                    if (__builtin_amdgcn_ballot_w64(p < lim) == 0) break;
+                    if (p < lim) {
+                        uint32_t t = pk[p];
+                        uint32_t b1 = pk[p + 1];
+                        uint32_t c9 = pk[p + 9];
+                        asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                        const bool z = t == 0u, f = t == 0xFFu;
+                        rll[min(ne, kFuLoc)] = (uint8_t)(p - lo);  // entry kFuLoc: the overflow slot
+                        ++ne;
+                        words += 1u + (z ? b1 : 0u) + (f ? c9 : 0u);
+                        p += __popc(t) + 1u + ((z || f) ? 1u + (f ? 8u * c9 : 0u) : 0u);
+                    }
+                }
+                // p: the lane's exit (its entry when no record starts in its block)
+                const uint32_t xm = fu_prev_lane(wave_incl_max(p, lane));
+                const bool bad = lane > 0 && lo < end && E != xm;
+                if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
+                if (bad) {
+                    E = xm;
+                    p = xm;
+                    words = 0;
+                    ne = 0;
                 }
             }
-            const bool any_eof = __builtin_amdgcn_ballot_w64(eof) != 0;
+            const uint32_t pos = min(E, lim);
+            // a record that runs past the unit leaves its lane's exit past the unit's end
+            const bool any_eof = __builtin_amdgcn_ballot_w64(lo < end && p > end) != 0;
             const bool ovf = __builtin_amdgcn_ballot_w64(ne > kFuLoc) != 0;  // a list overflowed: code walk
             FL_T(t6);
             FL_ACC(5, t6 - t5);
@@ -2639,24 +2620,42 @@ __global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const ui
                         //      kFlZero; an FF run's body words are literal codes). The list gives every
                         //      record's position, so the passes do not depend on each other ------------
                         uint32_t w = wbase;
-                        for (uint32_t i = 0;; ++i) {
-                            const bool act = i < nl && w < W1;
-                            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                            const uint32_t e = lo + rl[kFuLoc * lane + min(i, kFuLoc - 1)];
-                            uint32_t t = pk[e];
-                            uint32_t b1 = pk[e + 1];
-                            uint32_t c9 = pk[e + 9];
-                            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                            const bool z = t == 0u, f = t == 0xFFu;
-                            code[(act && !z && w >= W0) ? w - W0 : kFuOut] = (uint16_t)e;
-                            const uint32_t c = f ? c9 : 0u;
-                            if (act && c) {
-                                for (uint32_t j = 1; j <= c; ++j) {
-                                    const uint32_t wi = w + j;
-                                    if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (e + 1 + 8 * j));
+                        uint32_t rn = 0, rs = 0, rw = 0;  // a literal run longer than 3 words: the wave writes it
+                        for (uint32_t i = 0; i < nl; ++i) {
+                            if (__builtin_amdgcn_ballot_w64(w < W1) == 0) break;
+                            if (w < W1) {
+                                const uint32_t e = lo + rll[i];
+                                uint32_t t = pk[e];
+                                uint32_t b1 = pk[e + 1];
+                                uint32_t c9 = pk[e + 9];
+                                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                                const bool z = t == 0u, f = t == 0xFFu;
+                                if (!z && w >= W0) code[w - W0] = (uint16_t)e;
+                                const uint32_t c = f ? c9 : 0u;
+                                if (c) {
+                                    if (c <= 3u || rn != 0) {
+                                        for (uint32_t j = 1; j <= c; ++j) {
+                                            const uint32_t wi = w + j;
+                                            if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (e + 1 + 8 * j));
+                                        }
+                                    } else {
+                                        rn = c;
+                                        rs = e + 9;
+                                        rw = w + 1;
+                                    }
                                 }
+                                w += 1u + (z ? b1 : 0u) + c;
                             }
-                            w += act ? 1u + (z ? b1 : 0u) + c : 0u;
+                        }
+                        uint64_t rm = __builtin_amdgcn_ballot_w64(rn != 0);
+                        while (rm) {  // literal runs: lane i of the wave writes word i, i + 64, ...
+                            const uint32_t l = (uint32_t)__builtin_ctzll(rm);
+                            rm &= rm - 1;
+                            const uint32_t nn = readlane(rn, l), ss = readlane(rs, l), ww = readlane(rw, l);
+                            for (uint32_t j = lane; j < nn; j += kWave) {
+                                const uint32_t wi = ww + j;
+                                if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (ss + 8 * j));
+                            }
                         }
                     } else {
                         // ---- code walk (decode_fill_kernel) ------------------------------------------
