@@ -201,6 +201,9 @@ SIGNATURES = {
     "capnp_packed_frame_connections": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                                       ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                                       ctypes.POINTER(ctypes.c_uint32)]),
+    "capnp_packed_stream_release": (ctypes.c_int, [_vp]),
+    "capnp_packed_stream_queue_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t),
+                                                      ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_set_decoder": (ctypes.c_int, [ctypes.c_int]),
 }
 
@@ -373,7 +376,12 @@ class Message:
         """message.zig:699-969 Message.validate(options), run by validate_batch on the
         device over this message's segments (re-framed: header + segments, the bytes
         Message.init parsed). Raises the reference's error; returns the traversal words
-        consumed. Arguments left None take ValidationOptions' defaults (:331-335)."""
+        consumed. Arguments left None take ValidationOptions' defaults (:331-335).
+        An empty segment list raises EmptyMessage (:700), as after deinit(). Segments are
+        whole words when they come from Message.init / init_packed; a hand-built segment
+        whose length is not a multiple of 8 cannot be framed and raises InvalidMessageSize."""
+        if len(self.segments) == 0:
+            raise EmptyMessage("Message.validate: no segments")
         framed = np.frombuffer(frame_segments(self.segments), dtype=np.uint8)
         d_in = torch.from_numpy(framed.copy()).to(device)
         off = torch.zeros(1, dtype=torch.int64, device=device)
@@ -618,6 +626,20 @@ class decoder:
         return False
 
 
+def stream_release(stream=None) -> None:
+    """Free the library's context of a stream (side stream, events, queues); see
+    capnp_packed_stream_release. Synchronises the stream."""
+    _raise(lib().capnp_packed_stream_release(_stream(stream)), "stream_release")
+
+
+def stream_queue_info(stream=None):
+    """(bytes of the stream's queue, replaced queues kept for captured graphs)."""
+    b, k = ctypes.c_size_t(), ctypes.c_uint32()
+    _raise(lib().capnp_packed_stream_queue_info(_stream(stream), ctypes.byref(b), ctypes.byref(k)),
+           "stream_queue_info")
+    return b.value, k.value
+
+
 def _ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
@@ -739,8 +761,11 @@ def validate_batch(d_in, in_off, in_len, status, words=None, segment_count_limit
                    stream=None) -> None:
     """Message.validate (message.zig:699-969) of a batch of framed messages (the bytes
     Message.init takes): status[i] = 0 or the reference's first error for message i;
-    words[i] (optional int64) = traversal words the walk consumed (0 on error)."""
+    words[i] (optional int64) = traversal words the walk consumed (0 on error).
+    Any nesting limit is accepted; the device applies at most 2^18 (the C-ABI takes a u32,
+    so larger values are clamped here first)."""
     n = _units(in_off, in_len, status, words)
+    nesting_limit = min(int(nesting_limit), 0xFFFFFFFF)
     _raise(lib().capnp_packed_validate_batch(_ptr(d_in), _ptr(in_off), _ptr(in_len), n, segment_count_limit,
                                              traversal_limit_words, nesting_limit, _ptr(status), _ptr(words),
                                              _stream(stream)), "validate_batch")

@@ -279,6 +279,34 @@ int capnp_packed_set_decoder(int decoder) {
     return cpk::set_decoder(decoder);
 }
 
+int capnp_packed_stream_release(void* stream) {
+    int st = ensure_device();
+    if (st) return st;
+    hipError_t e = cpk::release_stream(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "stream release");
+}
+
+int capnp_packed_stream_queue_info(void* stream, size_t* bytes, uint32_t* kept) {
+    if (!bytes || !kept) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output");
+    *bytes = 0;
+    *kept = 0;
+    int st = ensure_device();
+    if (st) return st;
+    cpk::stream_queue_info(static_cast<hipStream_t>(stream), bytes, kept);
+    return CAPNP_PACKED_OK;
+}
+
+// The kernels address the workspace as u32 counters, 16-B table entries and 64-B
+// record stores at 256-B offsets: it must be 256-B aligned (hipMalloc's alignment).
+static int check_ws(const void* ws, size_t bytes, uint32_t n) {
+    if (!ws) return CAPNP_PACKED_OK;
+    if (reinterpret_cast<uintptr_t>(ws) & 255)
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "workspace not 256-B aligned");
+    if (bytes < cpk::queue_bytes(n))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "workspace smaller than capnp_packed_batch_workspace_bytes(n)");
+    return CAPNP_PACKED_OK;
+}
+
 int capnp_packed_encode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                  uint32_t n, uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_cap,
                                  uint64_t* d_out_len, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
@@ -286,8 +314,7 @@ int capnp_packed_encode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, 
     int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
     if (st || n == 0) return st;
     if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
-    if (d_workspace && workspace_bytes < cpk::queue_bytes(n))
-        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "workspace smaller than capnp_packed_batch_workspace_bytes(n)");
+    if ((st = check_ws(d_workspace, workspace_bytes, n))) return st;
     hipError_t e = cpk::launch_encode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
                                       d_status, true, d_workspace, workspace_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "encode launch");
@@ -316,8 +343,7 @@ int capnp_packed_decode_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, 
     int st = check_batch(d_in, d_in_off, d_in_len, n, d_out_len, d_status);
     if (st || n == 0) return st;
     if (!d_out_off || !d_out_cap) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output slot arrays");
-    if (d_workspace && workspace_bytes < cpk::queue_bytes(n))
-        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "workspace smaller than capnp_packed_batch_workspace_bytes(n)");
+    if ((st = check_ws(d_workspace, workspace_bytes, n))) return st;
     hipError_t e = cpk::launch_decode(d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
                                       d_status, true, d_workspace, workspace_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "decode launch");
@@ -405,8 +431,6 @@ int capnp_packed_validate_batch(const uint8_t* d_in, const uint64_t* d_in_off, c
                                 uint32_t nesting_limit, int32_t* d_status, uint64_t* d_words, void* stream) {
     if (n == 0) return CAPNP_PACKED_OK;
     if (!d_in_off || !d_in_len || !d_status) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null batch pointer");
-    if (nesting_limit > 64)
-        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "nesting_limit above 64 (the device stack depth)");
     int st = ensure_device();
     if (st) return st;
     hipError_t e = cpk::launch_validate(d_in, d_in_off, d_in_len, n, segment_count_limit, traversal_limit_words,

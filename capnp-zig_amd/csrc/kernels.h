@@ -22,6 +22,8 @@ size_t queue_bytes(uint32_t n);
 
 // capnp_packed_set_decoder: returns the previous setting
 int set_decoder(int decoder);
+hipError_t release_stream(hipStream_t stream);
+void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept);
 
 // Reader.readPackedMessage over a batch of reader streams (reader.zig:84-156).
 hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,

@@ -155,6 +155,15 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // the previous lane's v (wave_shr:1); lane 0 gets ident
 __device__ __forceinline__ uint32_t wave_prev_lane(uint32_t v, uint32_t ident) { return dpp_mov<0x138, 0xF>(v, ident); }
 
+// Lane l - 1's v (lane 0: 0), read with every lane active: the asm pins the DPP move (and
+// the computation of v) in front of any branch on the lane, since a DPP read of a lane the
+// EXEC mask excludes returns that lane's stale register.
+__device__ __forceinline__ uint32_t fu_prev_lane(uint32_t v) {
+    uint32_t r = dpp_mov<0x138, 0xF>(v, 0u);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+
 // inclusive min over lanes >= this lane
 __device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v, uint32_t lane) {
 #pragma unroll
@@ -1983,8 +1992,11 @@ constexpr uint32_t kFlMaxL = 5;                   // pieces per lane (kFlPieces 
 // bytes q+1 .. q+8 its packed bytes (a mixed record, or an FF record's first word,
 // whose tag 0xFF selects all 8 bytes), kFlLit | q for a literal word at q+1 .. q+8
 // (an FF run's body), or kFlZero.
+// A zero run's first word is kFlZeroHead; the rest of the run and an FF run's body are
+// left as kFlZero by the code walk and resolved from the last head before them (fl_bodies).
 constexpr uint32_t kFlLit = 0x2000u;
 constexpr uint32_t kFlZero = 0xFFFFu;
+constexpr uint32_t kFlZeroHead = 0xFFFEu;
 constexpr uint32_t kFlPos = 0x1FFFu;
 static_assert(kFlPk < kFlPos, "codes hold window positions");
 
@@ -2027,7 +2039,36 @@ __device__ __forceinline__ uint64_t fill_word(const uint8_t* pk, const uint64_t*
     const uint32_t t = (code & kFlLit) ? 0xFFu : (uint32_t)(lo >> sh) & 0xFFu;
     const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));  // bytes q+1 .. q+8
     const uint64_t w = perm64(pay, lut[t]);
-    return code == kFlZero ? 0ull : w;
+    return code >= kFlZeroHead ? 0ull : w;
+}
+
+// Codes of the words the code walk left as kFlZero (a record's words after its first): lane l
+// takes codes [8l, 8l + 8) of the pass, the last head before each (an exclusive max-scan of
+// (index + 1) << 16 | code over the lanes) decides it. After a zero head it stays a zero word;
+// after an FF head at q it is the literal word k words on, kFlLit | (q + 1 + 8k); after a
+// literal code kFlLit | q (an FF body continued from the previous pass) it is kFlLit | (q + 8k).
+// message.zig:101-141 (the words of one 00 / FF record).
+__device__ __forceinline__ void fl_bodies(uint16_t* code, uint32_t nw, uint32_t lane) {
+    uint4 cv = reinterpret_cast<const uint4*>(code)[lane];
+    uint32_t c[8] = {cv.x & 0xFFFFu, cv.x >> 16, cv.y & 0xFFFFu, cv.y >> 16,
+                     cv.z & 0xFFFFu, cv.z >> 16, cv.w & 0xFFFFu, cv.w >> 16};
+    uint32_t lh = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lh = c[i] != kFlZero ? ((8u * lane + i + 1u) << 16) | c[i] : lh;
+    uint32_t h = fu_prev_lane(wave_incl_max(lh, lane));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t idx = 8u * lane + i;
+        if (c[i] != kFlZero) {
+            h = ((idx + 1u) << 16) | c[i];
+        } else if (h != 0 && idx < nw) {
+            const uint32_t hc = h & 0xFFFFu, k = idx + 1u - (h >> 16);
+            const uint32_t b = (hc & kFlLit) ? (hc & kFlPos) : hc + 1u;
+            c[i] = hc == kFlZeroHead ? kFlZero : (kFlLit | (b + 8u * k));
+        }
+    }
+    cv = make_uint4(c[0] | (c[1] << 16), c[2] | (c[3] << 16), c[4] | (c[5] << 16), c[6] | (c[7] << 16));
+    reinterpret_cast<uint4*>(code)[lane] = cv;
 }
 
 __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uint8_t* __restrict__ in,
@@ -2187,6 +2228,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                 wave_lds_sync();
                 const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
                 uint32_t p = mine ? pos : jend, w = wbase;
+                bool runs = false;  // a record of more than one word in this pass
                 for (;;) {  // one record per lane per pass; predicated body, uniform exit
                     const bool act = p < jend && w < W1;
                     if (__builtin_amdgcn_ballot_w64(act) == 0) break;
@@ -2196,23 +2238,26 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                     uint32_t c9 = pk[pp + 9];
                     asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
                     const bool z = t == 0u, f = t == 0xFFu;
-                    // message.zig:101-141: 00 -> zero word(s) (the list starts as kFlZero), FF ->
-                    // its first word (tag 0xFF selects the 8 bytes) + c literal words, other
-                    // tags -> scatter of popc(t) bytes
-                    code[(act && !z && w >= W0) ? w - W0 : kFlOut] = (uint16_t)pp;
                     const uint32_t c = f ? c9 : 0u;
-                    if (act && c) {  // FF run body: literal word i at bytes pp+2+8i .. pp+9+8i
-                        for (uint32_t i = 1; i <= c; ++i) {
-                            const uint32_t wi = w + i;
-                            if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (pp + 1 + 8 * i));
-                        }
-                    }
-                    w = act ? w + 1u + (z ? b1 : 0u) + c : w;
+                    const uint32_t nx = (z ? b1 : 0u) + c;  // words after the first
+                    // message.zig:101-141: 00 -> a zero head, FF -> its first word (tag 0xFF
+                    // selects the 8 bytes), other tags -> scatter of popc(t) bytes; the words
+                    // after a record's first stay kFlZero for fl_bodies. An FF body that started
+                    // in an earlier pass continues at word 0 from its literal code there.
+                    const bool head = act && w >= W0, cont = act && f && w < W0 && w + nx >= W0;
+                    const uint32_t cd = z ? kFlZeroHead : (w >= W0 ? pp : (kFlLit | (pp + 1u + 8u * (W0 - w))));
+                    code[head ? w - W0 : (cont ? 0u : kFlOut)] = (uint16_t)cd;
+                    runs |= act && nx != 0;
+                    w = act ? w + 1u + nx : w;
                     p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
                 }
                 FL_T(t4);
                 FL_ACC(3, t4 - t3);
                 wave_lds_sync();
+                if (__builtin_amdgcn_ballot_w64(runs) != 0) {
+                    fl_bodies(code, W1 - W0, lane);
+                    wave_lds_sync();
+                }
                 // ---- expand by output word: coalesced stores straight from registers ----------
                 const uint32_t nw = W1 - W0;
                 if (a16) {
@@ -2312,15 +2357,6 @@ __device__ __forceinline__ void fu_scan(uint32_t& lo, uint32_t& hi) {
     CPK_FU_STEP(0x142, 0xA);
     CPK_FU_STEP(0x143, 0xC);
 #undef CPK_FU_STEP
-}
-
-// Lane l - 1's v (lane 0: 0), read with every lane active: the asm pins the DPP move (and
-// the computation of v) in front of any branch on the lane, since a DPP read of a lane the
-// EXEC mask excludes returns that lane's stale register.
-__device__ __forceinline__ uint32_t fu_prev_lane(uint32_t v) {
-    uint32_t r = dpp_mov<0x138, 0xF>(v, 0u);
-    asm volatile("" : "+v"(r));
-    return r;
 }
 
 // The map of one dword of a lane's block (two byte pairs): d -> src[d], src = [TA[b1],
@@ -3760,14 +3796,22 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
 //   pointers (pleft of pw, from byte `cur` of segment `seg`) and the elements after it
 //   (eleft, each dw data words then pw pointers), at the nesting value the reference
 //   passes to validatePointer for them. Pushing a frame spends a nesting level, so a lane
-//   never holds more than nesting_limit (<= kVdDepth) frames. The first kVdLds live in
-//   LDS, deeper ones in the lane's private scratch.
+//   never holds more than nesting_limit frames. The first kVdLds live in LDS, deeper ones
+//   (up to kVdDepth) in the lane's private scratch. A frame keeps its nesting value in 6
+//   bits, relative to base = max(nesting_limit - 64, 0): a message that needs a frame
+//   below base (only with nesting_limit > 64) is handed, untouched, to a deep list, and the
+//   DEEP instance of the kernel validates the listed messages with the frames in global
+//   scratch (depth_cap frames per lane, the nesting value in a u32 beside each).
 // - Segment offsets: the first kVdSegs segments' byte offsets are kept in LDS from the
 //   header parse; one more (the last sought) in registers; any other is sought again by
 //   reading the segment table.
 // Visiting order, limit consumption and every check follow the reference line by line,
 // so a message's status is the first error the reference raises.
-constexpr uint32_t kVdDepth = 64;  // supported nesting limit (the reference default)
+constexpr uint32_t kVdDepth = 64;  // frames per lane in LDS + private scratch (the reference default limit)
+// Largest nesting limit the device applies (a larger one is clamped to it): 2^18 pointer
+// levels, far past the depth at which the reference's recursive validatePointer exhausts
+// its thread stack. It bounds the DEEP kernel's frame stack and every far-pointer chain.
+constexpr uint32_t kVdMaxNest = 1u << 18;
 #ifndef CPK_VD_LDS
 #define CPK_VD_LDS 8
 #endif
@@ -3802,23 +3846,43 @@ __device__ __forceinline__ int64_t ptr_offset_words(uint64_t w) {  // message.zi
     return (raw & 0x20000000u) ? (int64_t)raw - ((int64_t)1 << 30) : (int64_t)raw;
 }
 
+// Deep-path arguments (VdDeep): the list of deferred messages and its count; for the DEEP
+// instance also the global frame stack (frame i of global lane g at [i * lanes + g]) with the
+// frames' nesting values, its depth and the lanes of the grid that take messages.
+struct VdDeep {
+    uint32_t* list = nullptr;
+    uint32_t* count = nullptr;
+    uint4* stk = nullptr;
+    uint32_t* nest = nullptr;
+    uint32_t depth_cap = 0;
+    uint32_t lanes = 0;
+};
+
+template <bool DEEP>
 __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restrict__ in,
                                                          const uint64_t* __restrict__ in_off,
                                                          const uint64_t* __restrict__ in_len, uint32_t n,
                                                          uint32_t per_wave, uint64_t seg_limit, uint64_t trav_limit,
                                                          uint32_t nest_limit, int32_t* __restrict__ status,
-                                                         uint64_t* __restrict__ words) {
-    __shared__ uint4 stack_all[kVdLds * kWave];         // frame f < kVdLds of lane l at [f * 64 + l]
+                                                         uint64_t* __restrict__ words, VdDeep dp) {
+    __shared__ uint4 stack_all[DEEP ? 1 : kVdLds * kWave];  // frame f < kVdLds of lane l at [f * 64 + l]
     __shared__ uint32_t segp_all[(kVdSegs + 1) * kWave];  // segment i's start (i <= kVdSegs) at [i * 64 + l]
-    uint4 deep[kVdDepth - kVdLds];                       // frames kVdLds.. (private scratch)
+    uint4 deep[DEEP ? 1 : kVdDepth - kVdLds];            // frames kVdLds.. (private scratch)
     const uint32_t lane = lane_id();
-    uint4* const stk = stack_all + lane;
+    uint4* const stk = stack_all + (DEEP ? 0 : lane);
     uint32_t* const segp = segp_all + lane;
+    const uint64_t glane = (uint64_t)blockIdx.x * kWave + lane;
+    if (DEEP) {  // the deferred messages, spread over the grid
+        n = *dp.count;
+        per_wave = (n + gridDim.x - 1) / gridDim.x;
+    }
+    // nesting values in the frames are relative to base (6 bits; DEEP: absolute, in dp.nest)
+    const uint32_t base = nest_limit > kVdDepth ? nest_limit - kVdDepth : 0u;
     const uint64_t first = (uint64_t)blockIdx.x * per_wave;
     const uint64_t last = first + per_wave < n ? first + per_wave : n;
     uint64_t cursor = first;  // wave-uniform
 
-    uint32_t kind = VK_IDLE;
+    uint32_t kind = (DEEP && glane >= dp.lanes) ? VK_EXIT : VK_IDLE;
     uint64_t msg = 0;
     const uint8_t* d = in;
     const uint8_t* laddr = in;  // the pending read
@@ -3835,20 +3899,42 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
     uint32_t tseg = 0;  // the pending inline-composite tag: segment, position, list word count
     uint64_t tpos = 0, twc = 0;
 
+    const uint64_t glanes = dp.lanes;  // DEEP: the frame stack's lane stride
     auto frame_store = [&](uint32_t i, uint4 f) {
-        if (i < kVdLds) stk[kWave * i] = f;
+        if (DEEP) dp.stk[(uint64_t)i * glanes + glane] = f;
+        else if (i < kVdLds) stk[kWave * i] = f;
         else deep[i - kVdLds] = f;
     };
-    auto frame_load = [&](uint32_t i) { return i < kVdLds ? stk[kWave * i] : deep[i - kVdLds]; };
-    auto push = [&](uint32_t seg, uint64_t cur, uint32_t pleft, uint32_t pw, uint32_t eleft, uint32_t dw,
-                    uint32_t nest) {
-        frame_store(depth, make_uint4((uint32_t)cur, eleft, pleft | (pw << 16), dw | (seg << 16) | (nest << 26)));
-        ++depth;
+    auto frame_load = [&](uint32_t i) {
+        if (DEEP) return dp.stk[(uint64_t)i * glanes + glane];
+        return i < kVdLds ? stk[kWave * i] : deep[i - kVdLds];
+    };
+    auto frame_nest = [&](uint32_t i, const uint4& f) {
+        return DEEP ? dp.nest[(uint64_t)i * glanes + glane] : (f.w >> 26) + base;
     };
     auto finish = [&](int32_t st) {
         status[msg] = st;
         if (words) words[msg] = st == ST_OK ? trav_limit - rem : 0ull;
         kind = VK_IDLE;
+    };
+    // false: the message was deferred to the deep list (nothing written for it here)
+    auto push = [&](uint32_t seg, uint64_t cur, uint32_t pleft, uint32_t pw, uint32_t eleft, uint32_t dw,
+                    uint32_t nest) {
+        if (DEEP) {
+            if (depth >= dp.depth_cap) {  // cannot happen: a frame spends a level and >= 1 word
+                finish(ST_NEST);
+                return false;
+            }
+            dp.nest[(uint64_t)depth * glanes + glane] = nest;
+        } else if (nest < base) {
+            dp.list[atomicAdd(dp.count, 1u)] = (uint32_t)msg;
+            kind = VK_IDLE;
+            return false;
+        }
+        frame_store(depth, make_uint4((uint32_t)cur, eleft, pleft | (pw << 16),
+                                      dw | (seg << 16) | (DEEP ? 0u : (nest - base) << 26)));
+        ++depth;
+        return true;
     };
     auto consume = [&](uint64_t w) {  // :710-713
         if (w > rem) return false;
@@ -3896,7 +3982,7 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
             if (f.z & 0xFFFFu) {
                 pseg = (f.w >> 16) & 0x3FFu;
                 ppos = f.x;
-                pnest = f.w >> 26;
+                pnest = frame_nest(depth - 1, f);
                 f.x += 8;
                 f.z -= 1;
                 frame_store(depth - 1, f);
@@ -3943,7 +4029,7 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
         seg_lookup(s, off, slen);
         if (co > slen || bytes > slen - co) return finish(ST_OOB);
         if (!consume((bytes + 7) / 8)) return finish(ST_TRAV);  // listContentWords (:81-86)
-        if (es == 6 && wc) push(s, co, 1, 1, (uint32_t)(wc - 1), 0, nest);
+        if (es == 6 && wc && !push(s, co, 1, 1, (uint32_t)(wc - 1), 0, nest)) return;
         next();
     };
     // inline-composite elements from a tag (:940-968 with layout A, :846-868, :911-926)
@@ -3953,7 +4039,8 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
         seg_lookup(s, off, slen);
         if (eo > slen || total_words * 8 > slen - eo) return finish(ST_OOB);
         if (!consume(total_words)) return finish(ST_TRAV);
-        if (pw && count) push(s, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest);
+        if (pw && count && !push(s, eo + 8 * dw, (uint32_t)pw, (uint32_t)pw, (uint32_t)(count - 1), (uint32_t)dw, nest))
+            return;
         next();
     };
 
@@ -3965,7 +4052,7 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
                 if (kind == VK_IDLE) {
                     const uint64_t id = cursor + __popcll(idle & ((1ull << lane) - 1));
                     if (id < last) {
-                        msg = id;
+                        msg = DEEP ? dp.list[id] : id;
                         kind = VK_META;
                     } else {
                         kind = VK_EXIT;
@@ -4066,7 +4153,7 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
                         break;
                     }
                     if (!consume(ds + pc)) { finish(ST_TRAV); break; }
-                    if (pc) push(pseg, (uint64_t)so_s + 8 * ds, (uint32_t)pc, (uint32_t)pc, 0, 0, nest);
+                    if (pc && !push(pseg, (uint64_t)so_s + 8 * ds, (uint32_t)pc, (uint32_t)pc, 0, 0, nest)) break;
                     next();
                     break;
                 }
@@ -4359,8 +4446,10 @@ static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) 
 // events and long-unit queue, so batches on independent caller streams never wait
 // on each other, and a graph captured from one stream shares nothing with eager
 // work on another. The context's mutex keeps one caller's record/wait pairs and
-// queue reset together. A queue that has to grow is replaced, never freed (a
-// captured graph may still reference it); growing is refused during a capture.
+// queue reset together. A queue that has to grow is replaced by one of at least twice its
+// size (so a stream sees O(log n) replacements): the old one is freed after the stream
+// drains, unless a hipGraph capture used it (a captured graph may still reference it; it is
+// then kept until capnp_packed_stream_release). Growing is refused during a capture.
 // Callers that pass their own workspace (capnp_packed_*_batch_ws) use it as the
 // queue instead, so nothing of the library's is baked into their graphs.
 struct StreamCtx {
@@ -4369,7 +4458,15 @@ struct StreamCtx {
     hipEvent_t fork = nullptr, join = nullptr;
     uint32_t* q = nullptr;  // class workspace (queue_bytes): kQHead counters, lists, tile / window table
     uint64_t qcap = 0;
-    std::vector<uint32_t*> retired;  // replaced queues (kept: graphs may reference them)
+    bool q_captured = false;         // q was used inside a hipGraph capture
+    std::vector<uint32_t*> retired;  // replaced queues a capture used (graphs may reference them)
+    ~StreamCtx() {
+        for (uint32_t* r : retired) (void)hipFree(r);
+        if (q) (void)hipFree(q);
+        if (s) (void)hipStreamDestroy(s);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+    }
 };
 static std::mutex g_ctx_mu;
 static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
@@ -4463,15 +4560,31 @@ class SideLaunch {
             if (ws_bytes_ < queue_bytes(n)) return nullptr;
             q = static_cast<uint32_t*>(ws_);
         } else {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(main_, &cs) != hipSuccess) return nullptr;
+            const bool capturing = cs != hipStreamCaptureStatusNone;
             if (ctx_->qcap < n) {
-                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-                if (hipStreamIsCapturing(main_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+                if (capturing) return nullptr;
+                uint64_t cap = 2 * ctx_->qcap;
+                cap = cap < n ? n : cap > 0xFFFFFFFFull ? 0xFFFFFFFFull : cap;
                 uint32_t* nq = nullptr;
-                if (hipMalloc(reinterpret_cast<void**>(&nq), queue_bytes(n)) != hipSuccess) return nullptr;
-                if (ctx_->q) ctx_->retired.push_back(ctx_->q);
+                if (hipMalloc(reinterpret_cast<void**>(&nq), queue_bytes((uint32_t)cap)) != hipSuccess) return nullptr;
+                if (ctx_->q) {
+                    if (ctx_->q_captured) {
+                        ctx_->retired.push_back(ctx_->q);
+                    } else {  // only this stream's batches used it (the side stream joins back)
+                        if (hipStreamSynchronize(main_) != hipSuccess) {
+                            (void)hipFree(nq);
+                            return nullptr;
+                        }
+                        (void)hipFree(ctx_->q);
+                    }
+                }
                 ctx_->q = nq;
-                ctx_->qcap = n;
+                ctx_->qcap = cap;
+                ctx_->q_captured = false;
             }
+            ctx_->q_captured |= capturing;
             q = ctx_->q;
         }
         if (hipMemsetAsync(q, 0, kQHead * sizeof(uint32_t), main_) != hipSuccess) return nullptr;
@@ -4495,6 +4608,41 @@ class SideLaunch {
     hipStream_t side_ = nullptr;
     bool ok_ = false, forked_ = false;
 };
+
+// Drop the library's context of a caller stream (its side stream, events and queues, also
+// those captured graphs used): after the stream's work is done and before it is destroyed.
+hipError_t release_stream(hipStream_t stream) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::unique_ptr<StreamCtx> c;
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        auto it = g_ctx.find({dev, reinterpret_cast<uintptr_t>(stream)});
+        if (it == g_ctx.end()) return hipSuccess;
+        c = std::move(it->second);
+        g_ctx.erase(it);
+    }
+    std::lock_guard<std::mutex> g(c->mu);  // no batch of this stream is being enqueued
+    e = hipStreamSynchronize(stream);
+    if (e == hipSuccess && c->s) e = hipStreamSynchronize(c->s);
+    return e;  // ~StreamCtx frees the rest
+}
+
+// The per-stream queue the library holds for `stream`: its bytes, and how many replaced
+// queues it keeps because a capture used them (tests: growth stays bounded).
+void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept) {
+    *bytes = 0;
+    *kept = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    auto it = g_ctx.find({dev, reinterpret_cast<uintptr_t>(stream)});
+    if (it == g_ctx.end()) return;
+    std::lock_guard<std::mutex> g2(it->second->mu);
+    *bytes = it->second->q ? queue_bytes((uint32_t)it->second->qcap) : 0;
+    *kept = (uint32_t)it->second->retired.size();
+}
 
 hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
@@ -4716,16 +4864,51 @@ hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, validate_kernel, kWave, 0) != hipSuccess || per <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, validate_kernel<false>, kWave, 0) != hipSuccess || per <= 0)
             per = 8;
         return (uint32_t)(cus * per);
     }();
     const uint32_t full = (n + kWave - 1) / kWave;
     const uint32_t blocks = full < resident ? full : resident;
     const uint32_t per_wave = (uint32_t)(((uint64_t)n + blocks - 1) / blocks);
-    validate_kernel<<<blocks, kWave, 0, stream>>>(in, in_off, in_len, n, per_wave, seg_limit, trav_limit, nest_limit,
-                                                 status, words);
-    return hipGetLastError();
+    if (nest_limit > kVdMaxNest) nest_limit = kVdMaxNest;
+    VdDeep dp;
+    const bool deep = nest_limit > kVdDepth;
+    void* lst = nullptr;
+    if (deep) {  // messages needing more than 64 frames go to a list for the DEEP kernel
+        hipError_t e = hipMallocAsync(&lst, 4ull * n + 16, stream);
+        if (e == hipSuccess) e = hipMemsetAsync(lst, 0, 16, stream);
+        if (e != hipSuccess) return e;
+        dp.count = static_cast<uint32_t*>(lst);
+        dp.list = dp.count + 4;
+    }
+    validate_kernel<false><<<blocks, kWave, 0, stream>>>(in, in_off, in_len, n, per_wave, seg_limit, trav_limit,
+                                                         nest_limit, status, words, dp);
+    if (!deep) return hipGetLastError();
+    // Frames of the DEEP kernel: a message holds at most min(nesting_limit, traversal limit)
+    // of them (each spends a nesting level and at least one traversal word); lanes sized so
+    // the stacks take at most kVdDeepBytes (at least one lane), at most 64 waves.
+    constexpr uint64_t kVdDeepBytes = 256ull << 20;
+    const uint64_t cap = trav_limit < nest_limit ? (trav_limit ? trav_limit : 1) : nest_limit;
+    const uint64_t per_lane = cap * (sizeof(uint4) + sizeof(uint32_t));
+    uint64_t lanes = kVdDeepBytes / per_lane;
+    lanes = lanes < 1 ? 1 : lanes > 64ull * kWave ? 64ull * kWave : lanes;
+    void* stk = nullptr;
+    hipError_t e = hipMallocAsync(&stk, lanes * per_lane, stream);
+    if (e != hipSuccess) {
+        (void)hipFreeAsync(lst, stream);
+        return e;
+    }
+    dp.stk = static_cast<uint4*>(stk);
+    dp.nest = reinterpret_cast<uint32_t*>(dp.stk + lanes * cap);
+    dp.depth_cap = (uint32_t)cap;
+    dp.lanes = (uint32_t)lanes;
+    validate_kernel<true><<<(uint32_t)((lanes + kWave - 1) / kWave), kWave, 0, stream>>>(
+        in, in_off, in_len, n, 0, seg_limit, trav_limit, nest_limit, status, words, dp);
+    e = hipGetLastError();
+    (void)hipFreeAsync(stk, stream);
+    (void)hipFreeAsync(lst, stream);
+    return e;
 }
 
 hipError_t launch_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,

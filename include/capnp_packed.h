@@ -133,10 +133,12 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
  * long unit lists, the per-block class counts, the long-unit tile / window table, and
  * 704 B per unit of piece records for the indexed decoder, kept out of the caller's
  * output slots). The plain calls
- * use a queue the library keeps per caller stream (made or grown on a batch larger
- * than any earlier one on that stream; growing is refused with DEVICE_ERROR inside
- * a hipGraph capture, and an old queue is never freed, so graphs that captured it
- * stay valid). The *_ws calls take the caller's device workspace instead: nothing
+ * use a queue the library keeps per caller stream (made on the first batch, grown to at
+ * least twice its size on a batch larger than it holds; growing is refused with
+ * DEVICE_ERROR inside a hipGraph capture). A replaced queue is freed once the stream has
+ * drained, unless a capture used it: graphs that captured it stay valid, and it is kept
+ * until capnp_packed_stream_release. The *_ws calls take the caller's device workspace
+ * instead (256-B aligned, as hipMalloc returns; INVALID_ARGUMENT otherwise): nothing
  * of the library's is captured, and a graph of them may replay beside any work.
  * ------------------------------------------------------------------------ */
 
@@ -148,6 +150,16 @@ int capnp_packed_encode_batch(const uint8_t* d_in, const uint64_t* d_in_off, con
 
 /* Bytes of device workspace the *_batch_ws calls need for n units. */
 size_t capnp_packed_batch_workspace_bytes(uint32_t n);
+
+/* Free what the library keeps for a caller stream (its side stream, events and queues,
+ * also queues a captured graph used). Call after the stream's work is done, before the
+ * stream is destroyed, and only when no graph captured from it will replay again. The
+ * next batch on the stream starts a new context. Synchronises the stream. */
+int capnp_packed_stream_release(void* stream);
+
+/* The queue the library holds for a caller stream: its size in bytes (0: none) and how
+ * many replaced queues it keeps because a hipGraph capture used them. */
+int capnp_packed_stream_queue_info(void* stream, size_t* bytes, uint32_t* kept);
 
 /* capnp_packed_encode_batch with a caller-owned device workspace of at least
  * capnp_packed_batch_workspace_bytes(n) bytes (NULL = the library's per-stream
@@ -257,9 +269,13 @@ int capnp_packed_message_init_batch(const uint8_t* d_in, const uint64_t* d_in_of
  * limits and error order. d_status[i] = the first error the reference's recursion
  * would raise, or OK; d_words[i] (may be NULL) = traversal words consumed (OK only).
  * The reference defaults are segment_count_limit 512, traversal_limit_words 8 Mi,
- * nesting_limit 64; nesting limits above 64 (the device stack depth) fail the
- * call with INVALID_ARGUMENT, and a message of 4 GiB or more gets INVALID_ARGUMENT
- * as its status. Allocates nothing; capturable in a hipGraph. */
+ * nesting_limit 64. Any nesting_limit is accepted: up to 64 the call allocates nothing
+ * and is capturable in a hipGraph; above 64, messages that need more than 64 stack frames
+ * are validated by a second kernel with its frames in global memory, allocated
+ * stream-ordered on `stream` (hipMallocAsync: 4n + 16 B and at most ~256 MiB of frame
+ * stacks, freed stream-ordered). A nesting_limit above 2^18 is applied as 2^18 (far
+ * deeper than the reference's recursive validate can go before its thread stack runs
+ * out). A message of 4 GiB or more gets INVALID_ARGUMENT as its status. */
 int capnp_packed_validate_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint64_t* d_in_len,
                                 uint32_t n, uint64_t segment_count_limit, uint64_t traversal_limit_words,
                                 uint32_t nesting_limit, int32_t* d_status, uint64_t* d_words, void* stream);

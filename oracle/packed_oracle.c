@@ -233,7 +233,7 @@ int oracle_message_init(const uint8_t* data, size_t n, uint32_t max_segs,
 /* ------------------------------------------------------------------------
  * message.zig:699-969 Message.validate (and the helpers it calls, :11-18
  * decodeOffsetWords, :65-86 listContentBytes/Words, :279-285 decodeFarPointer,
- * :420-444 readWord/resolveFarLandingPad, :586-697 resolveInlineCompositeList,
+ * :420-437 readWord/resolveFarLandingPad, :563-609 resolveInlineCompositeList,
  * message/bounds.zig:10-13 checkBounds), recursive as in the reference.
  * ------------------------------------------------------------------------ */
 enum {
@@ -274,7 +274,7 @@ static int v_consume(vmsg_t* m, uint64_t words) { /* :710-713 */
 
 static int v_pointer(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint64_t nesting);
 
-/* pointers of `count` elements of (dw + pw) words at elements_offset (:846-859, :956-967) */
+/* pointers of `count` elements of (dw + pw) words at elements_offset (:855-866, :913-926, :956-967) */
 static int v_elements(vmsg_t* m, uint32_t seg, uint64_t elements_offset, uint64_t count, uint64_t dw, uint64_t pw,
                       uint64_t nesting) {
     if (pw == 0 || count == 0) return V_OK;
@@ -290,7 +290,7 @@ static int v_elements(vmsg_t* m, uint32_t seg, uint64_t elements_offset, uint64_
     return V_OK;
 }
 
-/* :940-969 validateInlineCompositeTag */
+/* :929-968 validateInlineCompositeTag */
 static int v_ic_tag(vmsg_t* m, uint32_t seg, uint64_t elements_offset, uint64_t tag, uint64_t nesting) {
     int64_t cs = v_offset_words(tag);
     if (cs < 0) return V_ICP;
@@ -305,7 +305,7 @@ static int v_ic_tag(vmsg_t* m, uint32_t seg, uint64_t elements_offset, uint64_t 
     return v_elements(m, seg, elements_offset, count, dw, pw, nesting);
 }
 
-/* :761-799 validateStructPointer */
+/* :774-812 validateStructPointer */
 static int v_struct(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, int has_ov, uint64_t ov, uint64_t nesting) {
     uint64_t ds = (word >> 32) & 0xFFFF, pc = word >> 48, so;
     if (has_ov) {
@@ -340,7 +340,8 @@ static int v_list_bytes(uint64_t es, uint64_t count, uint64_t* bytes) { /* :65-7
     }
 }
 
-/* :586-627 resolveInlineCompositeList, list-pointer case (the only one validate reaches) */
+/* :899-927 validateInlineCompositeList, with :563-609 resolveInlineCompositeList's list-pointer case
+   (the only one validate reaches) */
 static int v_ic_list(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint64_t nesting) {
     int64_t t = (int64_t)pos + 8 + v_offset_words(word) * 8;
     if (t < 0) return V_OOB;
@@ -355,16 +356,16 @@ static int v_ic_list(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint6
     uint64_t elements_offset = tag_pos + 8;
     r = v_bounds(m, seg, elements_offset, word_count * 8);
     if (r) return r;
-    r = v_consume(m, word_count); /* :910-912 */
+    r = v_consume(m, word_count); /* :909 */
     if (r) return r;
     return v_elements(m, seg, elements_offset, count, dw, pw, nesting);
 }
 
-/* :801-893 validateListPointer */
+/* :814-897 validateListPointer */
 static int v_list(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, int has_ov, uint64_t ov, uint64_t nesting) {
     uint64_t es = (word >> 32) & 7;
     if (es == 7 && !has_ov) return v_ic_list(m, seg, pos, word, nesting);
-    if (es == 7) { /* layout B double-far inline composite (:815-857) */
+    if (es == 7) { /* layout B double-far inline composite (:827-869) */
         uint64_t word_count = word >> 35, tag_pos = ov, tag = 0;
         int r = v_read(m, seg, tag_pos, &tag);
         if (r) return r;
@@ -403,7 +404,7 @@ static int v_list(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, int has_
     return V_OK;
 }
 
-/* :734-759 validateFarPointer (with :427-435 resolveFarLandingPad) */
+/* :736-772 validateFarPointer (with :430-437 resolveFarLandingPad) */
 static int v_far(vmsg_t* m, uint64_t word, uint64_t nesting) {
     int dbl = (word >> 2) & 1;
     uint64_t pad_off = (word >> 3) & 0x1FFFFFFF;
@@ -432,7 +433,7 @@ static int v_far(vmsg_t* m, uint64_t word, uint64_t nesting) {
     return V_FAR;
 }
 
-/* :715-732 validatePointer */
+/* :715-734 validatePointer */
 static int v_pointer(vmsg_t* m, uint32_t seg, uint64_t pos, uint64_t word, uint64_t nesting) {
     if (word == 0) return V_OK;
     if (nesting == 0) return V_NEST;

@@ -235,3 +235,47 @@ def deep_chain(depth: int) -> bytes:
         b.set(0, pos, struct_ptr(at - pos - 1, 1 if last else 0, 0 if last else 1))
         pos = at
     return b.framed()
+
+
+def deep_mixed(rng, depth: int, n_segments: int = 3) -> bytes:
+    """A spine of `depth` pointer levels of mixed kinds: structs (extra null pointers and
+    data words beside the one that goes on), pointer lists and inline-composite lists (the
+    spine through one element), each link near or through a single far pointer (which
+    spends one more nesting level, validateFarPointer :736-752). The spine ends in a struct
+    with one data word."""
+    b = Builder(n_segments)
+    b.alloc(0, 1)
+    seg, pos = 0, 0
+    for d in range(depth):
+        last = d == depth - 1
+        t = seg if rng.random() < 0.6 else int(rng.integers(0, n_segments))
+        kind = "end" if last else str(rng.choice(["struct", "ptrlist", "composite"]))
+        if kind in ("end", "struct"):
+            dw = 1 if last else int(rng.integers(0, 2))
+            pw = 0 if last else int(rng.integers(1, 3))
+            content = b.alloc(t, dw + pw)
+            for i in range(dw):
+                b.set(t, content + i, int(rng.integers(0, 1 << 63)))
+            near = lambda off, dw=dw, pw=pw: struct_ptr(off, dw, pw)
+            nxt = content + dw + (int(rng.integers(0, pw)) if pw else 0)
+        elif kind == "ptrlist":
+            count = int(rng.integers(1, 3))
+            content = b.alloc(t, count)
+            near = lambda off, count=count: list_ptr(off, 6, count)
+            nxt = content + int(rng.integers(0, count))
+        else:
+            count, dw = int(rng.integers(1, 3)), int(rng.integers(0, 2))
+            wc = count * (dw + 1)
+            tag_at = b.alloc(t, 1 + wc)
+            b.set(t, tag_at, struct_ptr(count, dw, 1))
+            content = tag_at
+            near = lambda off, wc=wc: list_ptr(off, 7, wc)
+            nxt = tag_at + 1 + int(rng.integers(0, count)) * (dw + 1) + dw
+        if t == seg:
+            b.set(seg, pos, near(content - pos - 1))
+        else:  # single far: the landing pad is a near pointer in the target segment
+            pad = b.alloc(t, 1)
+            b.set(t, pad, near(content - pad - 1))
+            b.set(seg, pos, far_ptr(False, pad, t))
+        seg, pos = t, nxt
+    return b.framed()

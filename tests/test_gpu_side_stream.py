@@ -203,6 +203,78 @@ def test_workspace_too_small_is_rejected():
         b.run(ws=ws)
 
 
+def test_misaligned_workspace_is_rejected():
+    b = Batch(mixed_sizes(100, 8), seed=0xC0DE0432)
+    ws = cp.workspace(b.n + 64, device=DEV)
+    with pytest.raises(cp.InvalidArgument):
+        b.run(ws=ws[16:])  # 128 B past the 256-B aligned base
+    b.run(ws=ws)
+    torch.cuda.synchronize()
+    b.check_roundtrip()
+
+
+def test_queue_growth_is_bounded_and_released():
+    """Growing batches on one stream: the library's queue grows geometrically, replaced
+    queues are freed (none was captured), device memory stays bounded, and
+    capnp_packed_stream_release drops the context."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    wb = cp.lib().capnp_packed_batch_workspace_bytes
+    sizes_all = mixed_sizes(4200, 9, long_every=50, huge_every=997)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    grows, last = 0, 0
+    with torch.cuda.stream(s):
+        for n in range(200, 4200, 97):
+            b = Batch(sizes_all[:n], seed=0xC0DE0440 + n)
+            b.run(stream=s)
+            qb, kept = cp.stream_queue_info(s)
+            assert kept == 0 and wb(n) <= qb <= wb(2 * n + 1)
+            grows += qb != last
+            last = qb
+    s.synchronize()
+    b.check_roundtrip()
+    assert grows <= 6  # 200 -> 4200 units at >= 2x per growth: at most 5 growths after the first
+    del b
+    torch.cuda.empty_cache()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert free0 - free1 <= wb(2 * 4200) + (64 << 20), (free0, free1)
+    cp.stream_release(s)
+    assert cp.stream_queue_info(s) == (0, 0)
+    # the stream works again after a release (a new context)
+    b = Batch(mixed_sizes(300, 10), seed=0xC0DE0450)
+    with torch.cuda.stream(s):
+        b.run(stream=s)
+    s.synchronize()
+    b.check_roundtrip()
+    cp.stream_release(s)
+
+
+def test_captured_queue_is_kept_until_release():
+    small = Batch(mixed_sizes(600, 11), seed=0xC0DE0461)
+    big = Batch(mixed_sizes(5000, 12), seed=0xC0DE0462)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        small.run(stream=s)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        small.run()
+    with torch.cuda.stream(s):
+        big.run(stream=s)  # grows: the captured queue is kept
+    s.synchronize()
+    assert cp.stream_queue_info(s)[1] == 1
+    small.reset(0xC0DE0463)
+    g.replay()
+    torch.cuda.synchronize()
+    small.check_roundtrip()
+    big.check_roundtrip()
+    del g
+    cp.stream_release(s)
+    assert cp.stream_queue_info(s) == (0, 0)
+
+
 def test_tile_table_overflow_goes_serial():
     # Long-unit encode is tile-parallel through a tile table of n + 65536 tiles
     # (long_tiles_kernel). Three units of 30000 tiles (123 MB each) need 90000 > 65539:

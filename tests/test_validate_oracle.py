@@ -115,3 +115,38 @@ def test_generator_read_count_matches_walk():
         v = Counting(segs, 1 << 40)
         v.pointer(0, 0, v.word(0, 0), 64)
         assert Counting.n == t.reads
+
+
+def test_reference_messages_validate_on_the_oracle():
+    """The reference's real messages (capnp testdata, interop fixtures) and the unpacked
+    forms of their packed twins: valid under the default limits, the twins identical to
+    the framed files, and the limit edges the GPU tests compare at behave as expected."""
+    import os
+    fx = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fixtures")
+    rd = lambda n: open(os.path.join(fx, n), "rb").read()
+    expect = {"binary": 348, "segmented": 0, "fixture_single.bin": 34, "fixture_far.bin": 34}
+    for name, words in expect.items():
+        assert oracle.validate(rd(name)) == (0, words)
+    for packed, twin in (("packed", "binary"), ("segmented-packed", "segmented"),
+                         ("fixture_single_packed.bin", "fixture_single.bin"),
+                         ("fixture_far_packed.bin", "fixture_far.bin")):
+        st, u = oracle.unpack(rd(packed))
+        assert st == oracle.OK and u == rd(twin)
+    m = rd("binary")
+    assert oracle.validate(m, traversal_limit_words=347)[0] == CODES["TraversalLimitExceeded"]
+    assert oracle.validate(m, nesting_limit=4)[0] == CODES["NestingLimitExceeded"]
+    assert oracle.validate(m, nesting_limit=5) == (0, 348)
+    # segmented's root is a double far whose pad holds a struct tag: validateFarPointer
+    # reads it as an inline-composite tag of count 0 (:765-767) and stops
+    assert oracle.validate(rd("segmented"), segment_count_limit=124)[0] == CODES["SegmentCountLimitExceeded"]
+
+
+def test_deep_nesting_on_the_oracle():
+    import numpy as np
+    for d in (64, 65, 200):
+        assert oracle.validate(msggen.deep_chain(d), nesting_limit=d) == (0, d)
+        assert oracle.validate(msggen.deep_chain(d), nesting_limit=d - 1)[0] == CODES["NestingLimitExceeded"]
+    rng = np.random.default_rng(5)
+    m = msggen.deep_mixed(rng, 100)
+    st, w = oracle.validate(m, nesting_limit=1000)
+    assert st == 0 and w > 100

@@ -103,7 +103,10 @@ pub extern "capnp_packed" fn capnp_packed_validate_batch(
 ) c_int;
 /// Class workspace for the *_batch_ws calls (graph-safe batches with no shared state): unit
 /// lists, the long-unit tile / window table and the decoder's piece records (~750 B per unit).
+/// d_ws must be 256-B aligned (hipMalloc's alignment); a misaligned one is InvalidArgument.
 pub extern "capnp_packed" fn capnp_packed_batch_workspace_bytes(n: u32) usize;
+/// Free the library's context of a caller stream (before destroying the stream).
+pub extern "capnp_packed" fn capnp_packed_stream_release(stream: ?*anyopaque) c_int;
 pub extern "capnp_packed" fn capnp_packed_encode_batch_ws(
     d_in: [*]const u8, d_in_off: [*]const u64, d_in_len: [*]const u64, n: u32,
     d_out: [*]u8, d_out_off: [*]const u64, d_out_cap: [*]const u64,
@@ -138,6 +141,10 @@ pub const Error = error{
     UnexpectedEof,
     Overflow,
     OutOfMemory,
+    // frameConnections: the `frames` buffer is full (grow it and call again)
+    OutOfSpace,
+    // a slice argument of the wrong length
+    InvalidArgument,
     PackedDeviceError,
     NoDevice,
     // Reader.readPackedMessage (reader.zig:84-156)
@@ -168,6 +175,7 @@ fn check(status: c_int) Error!void {
         .overflow => error.Overflow,
         .out_of_space => error.OutOfMemory, // capacity is sized by us; unreachable in practice
         .no_device => error.NoDevice,
+        .invalid_argument => error.InvalidArgument,
         .end_of_stream => error.EndOfStream,
         .invalid_segment_count => error.InvalidSegmentCount,
         .segment_count_limit_exceeded => error.SegmentCountLimitExceeded,
@@ -250,19 +258,34 @@ pub fn readPackedMessageBuffered(allocator: std.mem.Allocator, buffered: []const
 /// call: `frames` receives every popped frame; frame i is
 /// frames[frame_off[i]..][0..frame_len[i]] of connection frame_conn[i]. Per connection,
 /// consumed[c] bytes leave its buffer and status[c] is .end_of_stream (wait for more
-/// bytes) or the error that closes it. error.OutOfSpace: grow `frames` and call again.
+/// bytes) or the error that closes it. error.OutOfSpace: grow `frames` (or the table) and
+/// call again. in_len, slot_guess, consumed and status must hold in_off.len entries, and
+/// table.len / table.conn table.off.len entries (error.InvalidArgument otherwise: the
+/// native side writes that many).
 pub const FrameTable = struct { off: []u64, len: []u64, conn: []u32 };
 pub fn frameConnections(
     buffered: []const u8, in_off: []const u64, in_len: []const u64, slot_guess: []u64,
     frames: []u8, table: FrameTable, consumed: []u64, status: []i32,
 ) Error!u32 {
+    const n = in_off.len;
+    if (in_len.len != n or slot_guess.len != n or consumed.len != n or status.len != n) return error.InvalidArgument;
+    if (table.len.len != table.off.len or table.conn.len != table.off.len) return error.InvalidArgument;
+    if (n > std.math.maxInt(u32) or table.off.len > std.math.maxInt(u32)) return error.InvalidArgument;
     var nf: u32 = 0;
-    try check(capnp_packed_frame_connections(
-        buffered.ptr, buffered.len, in_off.ptr, in_len.ptr, @intCast(in_off.len), slot_guess.ptr,
+    const st = capnp_packed_frame_connections(
+        buffered.ptr, buffered.len, in_off.ptr, in_len.ptr, @intCast(n), slot_guess.ptr,
         frames.ptr, frames.len, table.off.ptr, table.len.ptr, table.conn.ptr, @intCast(table.off.len),
         consumed.ptr, status.ptr, &nf,
-    ));
+    );
+    if (st == @intFromEnum(Status.out_of_space)) return error.OutOfSpace;
+    try check(st);
     return nf;
+}
+
+/// ValidationOptions.nesting_limit (usize, message.zig:334) as the C-ABI's u32: the device
+/// applies at most 2^18 levels anyway (capnp_packed.h), so clamping loses nothing.
+pub fn nestingLimitArg(nesting_limit: usize) u32 {
+    return @intCast(@min(nesting_limit, std.math.maxInt(u32)));
 }
 
 /// A validate_batch per-message status as the error Message.validate would return.
