@@ -271,15 +271,23 @@ def estimate_unpacked_size(packed) -> int:
     return n.value
 
 
-def unpack_packed(packed) -> bytes:
-    """unpackPacked (message.zig:88-145). Raises UnexpectedEof on truncation."""
+def unpack_packed(packed, size_hint=None) -> bytes:
+    """unpackPacked (message.zig:88-145). Raises UnexpectedEof on truncation.
+    One device decode into a buffer of `size_hint` bytes (default 4 x the packed length):
+    a message that needs more ends OUT_OF_SPACE with its size, and is decoded again into
+    a buffer of exactly that size (the reference sizes first, message.zig:90)."""
     packed = bytes(packed)
-    size = estimate_unpacked_size(packed)
-    out = ctypes.create_string_buffer(max(1, size))
-    n = _sz()
-    st = lib().capnp_packed_decode(_cbuf(packed), len(packed), out, size, ctypes.byref(n))
+    cap = max(4096, 4 * len(packed)) if size_hint is None else int(size_hint)
+    for _ in range(2):
+        out = ctypes.create_string_buffer(max(1, cap))
+        n = _sz()
+        st = lib().capnp_packed_decode(_cbuf(packed), len(packed), out, cap, ctypes.byref(n))
+        if st == OUT_OF_SPACE and n.value > cap:
+            cap = n.value
+            continue
+        _raise(st, "unpackPacked")
+        return out.raw[:n.value]
     _raise(st, "unpackPacked")
-    return out.raw[:n.value]
 
 
 # ---------------------------------------------------------------------------

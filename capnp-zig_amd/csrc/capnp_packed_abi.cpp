@@ -67,7 +67,10 @@ int ensure_device() {
     return CAPNP_PACKED_OK;
 }
 
-// Device context for the single-buffer host entry points.
+// Device context for the single-buffer host entry points: grow-only device buffers and
+// pinned host staging (the caller's pageable bytes are copied into pinned memory, so the
+// H2D / D2H copies run as DMA at full PCIe rate), one stream, the meta block's host copy
+// in pinned memory too.
 struct HostCtx {
     std::mutex mu;
     hipStream_t stream = nullptr;
@@ -75,7 +78,12 @@ struct HostCtx {
     size_t in_cap = 0;
     uint8_t* d_out = nullptr;
     size_t out_cap = 0;
-    uint64_t* d_meta = nullptr;  // in_off[2], out_off[2], len, status(as u64)
+    uint8_t* h_in = nullptr;  // pinned staging
+    size_t h_in_cap = 0;
+    uint8_t* h_out = nullptr;
+    size_t h_out_cap = 0;
+    uint64_t* d_meta = nullptr;  // in_off, in_len, out_off, out_cap, out_len, status (as u64), consumed
+    uint64_t* h_meta = nullptr;
 
     int init() {
         if (stream) return CAPNP_PACKED_OK;
@@ -83,17 +91,32 @@ struct HostCtx {
         if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
         e = hipMalloc(&d_meta, 8 * sizeof(uint64_t));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(meta)");
+        e = hipHostMalloc(reinterpret_cast<void**>(&h_meta), 8 * sizeof(uint64_t), hipHostMallocDefault);
+        if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(meta)");
         return CAPNP_PACKED_OK;
     }
+    static size_t grow(size_t need) { return need < 65536 ? 65536 : need + need / 2; }
     int reserve(uint8_t** p, size_t* cap, size_t need) {
         if (need <= *cap && *p) return CAPNP_PACKED_OK;
         if (need > (SIZE_MAX / 3) * 2) return fail(CAPNP_PACKED_OUT_OF_SPACE, "workspace size overflows size_t");
-        size_t want = need < 4096 ? 4096 : need + need / 2;
+        const size_t want = grow(need);
         if (*p) (void)hipFree(*p);
         *p = nullptr;
         *cap = 0;
         hipError_t e = hipMalloc(p, want);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+        *cap = want;
+        return CAPNP_PACKED_OK;
+    }
+    int reserve_host(uint8_t** p, size_t* cap, size_t need) {
+        if (need <= *cap && *p) return CAPNP_PACKED_OK;
+        if (need > (SIZE_MAX / 3) * 2) return fail(CAPNP_PACKED_OUT_OF_SPACE, "staging size overflows size_t");
+        const size_t want = grow(need);
+        if (*p) (void)hipHostFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(p), want, hipHostMallocDefault);
+        if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(staging)");
         *cap = want;
         return CAPNP_PACKED_OK;
     }
@@ -134,21 +157,33 @@ struct FrameCtx {
 
 FrameCtx g_fr;
 
+// Largest unpacked size of n packed bytes: a 2-byte zero-run record expands to 256 words.
+uint64_t unpack_bound(size_t n) { return n > (UINT64_MAX / 1024) ? UINT64_MAX : 1024ull * n; }
+
 // Run one unit through a batch kernel. kind: 0 encode, 1 decode, 2 decoded size, 3 encoded size,
-// 4 read message (reader.zig:84-156; *used_out = packed bytes consumed).
+// 4 read message (reader.zig:84-156; *used_out = packed bytes consumed). The input crosses
+// PCIe once (pinned staging), the kernels run with an output slot of `slot` bytes, and the
+// output comes back only when the unit is OK; *len_out is out_len (for OUT_OF_SPACE: the
+// size the unit needs).
 int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out,
                uint64_t* used_out = nullptr) {
     int st = g_ctx.init();
     if (st) return st;
     if (n > SIZE_MAX - 16 || slot > SIZE_MAX - 16) return fail(CAPNP_PACKED_OUT_OF_SPACE, "buffer size overflows size_t");
     if ((st = g_ctx.reserve(&g_ctx.d_in, &g_ctx.in_cap, n + 16))) return st;
+    if ((st = g_ctx.reserve_host(&g_ctx.h_in, &g_ctx.h_in_cap, n + 16))) return st;
     const bool write = (kind == 0 || kind == 1 || kind == 4);
     if (write && (st = g_ctx.reserve(&g_ctx.d_out, &g_ctx.out_cap, slot + 16))) return st;
-    uint64_t meta[7] = {0, n, 0, slot, 0, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status, consumed
+    uint64_t* const hm = g_ctx.h_meta;
+    const uint64_t meta[7] = {0, n, 0, slot, 0, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status, consumed
+    std::memcpy(hm, meta, sizeof(meta));
     hipStream_t s = g_ctx.stream;
     hipError_t e = hipSuccess;
-    if (n) e = hipMemcpyAsync(g_ctx.d_in, in, n, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(g_ctx.d_meta, meta, sizeof(meta), hipMemcpyHostToDevice, s);
+    if (n) {
+        std::memcpy(g_ctx.h_in, in, n);
+        e = hipMemcpyAsync(g_ctx.d_in, g_ctx.h_in, n, hipMemcpyHostToDevice, s);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(g_ctx.d_meta, hm, sizeof(meta), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(H2D)");
     uint64_t* m = g_ctx.d_meta;
     int32_t* d_status = reinterpret_cast<int32_t*>(m + 5);
@@ -161,16 +196,20 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
         e = cpk::launch_decode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, nullptr, 0,
                                s);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
-    e = hipMemcpyAsync(meta, g_ctx.d_meta, sizeof(meta), hipMemcpyDeviceToHost, s);
+    e = hipMemcpyAsync(hm, g_ctx.d_meta, sizeof(meta), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H)");
     int32_t status;
-    std::memcpy(&status, &meta[5], sizeof(status));
-    *len_out = meta[4];
-    if (used_out) *used_out = meta[6];
-    if (status == CAPNP_PACKED_OK && write && meta[4]) {
-        e = hipMemcpy(out, g_ctx.d_out, meta[4], hipMemcpyDeviceToHost);
+    std::memcpy(&status, &hm[5], sizeof(status));
+    *len_out = hm[4];
+    if (used_out) *used_out = hm[6];
+    if (status == CAPNP_PACKED_OK && write && hm[4]) {
+        const size_t len = (size_t)hm[4];
+        if ((st = g_ctx.reserve_host(&g_ctx.h_out, &g_ctx.h_out_cap, len))) return st;
+        e = hipMemcpyAsync(g_ctx.h_out, g_ctx.d_out, len, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpy(D2H out)");
+        std::memcpy(out, g_ctx.h_out, len);
     }
     if (status != CAPNP_PACKED_OK) g_last_error = capnp_packed_status_name(status);
     return status;
@@ -258,16 +297,13 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
     int st = ensure_device();
     if (st) return st;
     std::lock_guard<std::mutex> lock(g_ctx.mu);
-    uint64_t need = 0;
-    st = run_single(2, in, n, nullptr, 0, &need);  // message.zig:90 size pass first
-    if (st != CAPNP_PACKED_OK) return st;
-    if (need > cap) {
-        *out_len = (size_t)need;
-        return fail(CAPNP_PACKED_OUT_OF_SPACE, "OutOfSpace");
-    }
+    // one H2D and one decode into a slot of the caller's capacity (never more than n packed
+    // bytes can produce): the decoders size every unit before writing it (message.zig:90),
+    // so a unit that does not fit ends OUT_OF_SPACE with its size in out_len
+    const uint64_t bound = unpack_bound(n);
     uint64_t len = 0;
-    st = run_single(1, in, n, out, (size_t)need, &len);
-    *out_len = (size_t)len;
+    st = run_single(1, in, n, out, (size_t)(cap < bound ? cap : bound), &len);
+    *out_len = (st == CAPNP_PACKED_OK || st == CAPNP_PACKED_OUT_OF_SPACE) ? (size_t)len : 0;
     return st;
 }
 

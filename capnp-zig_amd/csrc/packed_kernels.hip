@@ -2784,11 +2784,16 @@ constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
 
 __device__ __forceinline__ uint32_t* q_blocks(uint32_t* q, uint32_t n) { return q + kQHead + 3ull * n; }
 
-template <int KIND>  // 0: encode, 1: decode
+template <int KIND>  // 0: encode, 1: decode, 2: decoded size (no output: long by packed length alone)
 __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
                                                uint32_t u) {
     const uint64_t off = in_off[u], len = in_len[u];
+    if (KIND == 2) {
+        const uint64_t s = reinterpret_cast<uintptr_t>(in + off) & 15;
+        if (len > 0 && ((s + len + 15) >> 4) > kFlPieces) return len > kQHuge ? CL_HUGE : CL_LONG;
+        return CL_MID;
+    }
     if (KIND == 0) {
         if (encode_tiled_unit(in, off, len)) return len > kQHuge ? CL_HUGE : CL_LONG;
         const bool valid = !(reinterpret_cast<uintptr_t>(in + off) & 7) && !(len & 7);
@@ -3323,10 +3328,10 @@ __global__ __launch_bounds__(kWvBlock) void window_resolve_kernel(const uint8_t*
                     e->wb = rwb;
                 }
             }
-            if (lane == 0) {
+            if (lane == 0) {  // out_cap null: the size pass (estimateUnpackedSize)
                 const uint64_t U = 8 * wacc;
                 out_len[unit] = st == ST_OK ? U : 0;
-                status[unit] = st != ST_OK ? st : (U > out_cap[unit] ? ST_SPACE : ST_OK);
+                status[unit] = st != ST_OK ? st : (out_cap && U > out_cap[unit] ? ST_SPACE : ST_OK);
             }
         }
     }
@@ -4750,8 +4755,37 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (!write) {  // size pass: the size-only index walk, then the lane walk for units it declined
-        launch_index<true>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, stream);
+    if (!write) {  // size pass (estimateUnpackedSize, message.zig:152-191)
+        // Units of at most kFlPieces pieces: the size-only index walk (a lane per unit). Longer
+        // units: window-parallel on the side stream (long_windows / window_spec /
+        // window_resolve, which yield out_len without any output), those the window table
+        // cannot hold by the size-only walk too; units of 2 GiB or more (the walk declines
+        // them) by the lane walk after the join.
+        SideLaunch side(stream, ws, ws_bytes);
+        uint32_t* const q = side.queue(n);
+        if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
+        launch_classes<2>(in, in_off, in_len, n, nullptr, nullptr, nullptr, q, status, stream);
+        hipError_t e = side.fork();
+        if (e != hipSuccess) return e;
+        static const uint32_t spec_res = resident_blocks(window_spec_kernel, kWvBlock, 4);
+        static const uint32_t res_res = resident_blocks(window_resolve_kernel, kWvBlock, 2);
+        const uint64_t wcap = win_cap(n);
+        const uint32_t win_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, spec_res);
+        const uint32_t res_blocks = std::min((n + kWvWaves - 1) / kWvWaves, res_res);
+        const hipStream_t ss = side.stream();
+        const uint32_t ix_blocks = (n + kWave - 1) / kWave;
+        long_windows_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
+        window_spec_kernel<<<win_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, q);
+        window_resolve_kernel<<<res_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, nullptr, out_len, status, q);
+        decode_index_kernel<true><<<ix_blocks, kWave, 0, ss>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
+                                                               out_len, status, nullptr, q + serial_off(n), q + 5);
+        decode_index_kernel<true><<<ix_blocks, kWave, 0, stream>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
+                                                                   out_len, status, nullptr, q + kQHead + 2ull * n,
+                                                                   q + 4);
+        e = hipGetLastError();
+        const hipError_t j = side.join();
+        if (e == hipSuccess) e = j;
+        if (e != hipSuccess) return e;
         decode_lane_kernel<false, true><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(
             in, in_off, in_len, n, out, out_off, out_cap, out_len, status);
         return hipGetLastError();
@@ -4786,8 +4820,8 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                              status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
-    // mid units: the fused single-pass decoder; CPK_DECODE=twopass selects the indexed
-    // two-pass decoder (index pass + fill pass) for same-box A/B runs
+    // mid units: the indexed two-pass decoder (index pass + fill pass), or the fused
+    // single-pass decoder when selected (capnp_packed_set_decoder / CPK_DECODE=fused)
     if (decoder_variant() == CAPNP_PACKED_DECODER_FUSED) {
         static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);
         const uint32_t fu_blocks = std::min((n + kFuWaves - 1) / kFuWaves, fu_res);

@@ -98,8 +98,11 @@ int capnp_packed_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
 int capnp_packed_decoded_size(const uint8_t* in, size_t n, size_t* out_size);
 
 /* Replaces `fn unpackPacked(allocator, packed) ![]u8` (message.zig:88-145).
- * Errors are raised before any output byte is written, as in the reference
- * (size pass first). On OUT_OF_SPACE, *out_len is the required size. */
+ * One host-to-device copy and one device decode into a slot of min(cap, 1024 n) bytes:
+ * the decoders size the unit before writing it, so errors are raised before any output
+ * byte is written, as in the reference (size pass first), and out is untouched on any
+ * error. On OUT_OF_SPACE, *out_len is the required size: a caller may pass a guessed
+ * capacity and call again with the exact one. */
 int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 
 /* ------------------------------------------------------------------------

@@ -40,16 +40,20 @@ def main():
                "cpu_pack_us": t_us(lambda: oracle.pack(data)),
                "cpu_unpack_us": t_us(lambda: oracle.unpack(packed)),
                "gpu_pack_us": t_us(lambda: cp.pack_packed(data)),
-               "gpu_unpack_us": t_us(lambda: cp.unpack_packed(packed))}
+               "gpu_unpack_us": t_us(lambda: cp.unpack_packed(packed)),
+               "cpu_size_us": t_us(lambda: oracle.decoded_size(packed)),
+               "gpu_size_us": t_us(lambda: cp.estimate_unpacked_size(packed))}
         rows.append({k: (round(v, 2) if isinstance(v, float) else v) for k, v in row.items()})
         print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
         size *= 4
     out = {"zero_thresh": thr, "rows": rows}
-    for op in ("pack", "unpack"):
+    for op in ("pack", "unpack", "size"):
         win = [r["bytes"] for r in rows if r[f"gpu_{op}_us"] < r[f"cpu_{op}_us"]]
         out[f"{op}_gpu_faster_from_bytes"] = min(win) if win else None
-    out["note"] = ("one unit per call; GPU = single-buffer C-ABI (pageable host buffers, one device "
-                   "context, H2D + launches + D2H + sync); CPU = oracle, one thread")
+    out["note"] = ("one unit per call; GPU = single-buffer C-ABI (caller's pageable buffers staged through "
+                   "pinned memory, one device context, one H2D + launches + D2H + sync; unpack = one "
+                   "capnp_packed_decode into a 4x guess, size = capnp_packed_decoded_size); CPU = oracle, "
+                   "one thread")
     print(json.dumps(out))
 
 

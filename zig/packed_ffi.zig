@@ -216,15 +216,27 @@ pub fn estimateUnpackedSize(packed_bytes: []const u8) Error!usize {
 }
 
 /// message.zig:88 `fn unpackPacked(allocator, packed) ![]u8`. Like the reference,
-/// truncated input fails with UnexpectedEof before any output is produced.
+/// truncated input fails with UnexpectedEof before any output is produced. One device
+/// call into a buffer of 4x the packed size; a message that expands more reports its size
+/// (OUT_OF_SPACE) and is decoded again into a buffer of exactly that size.
 pub fn unpackPacked(allocator: std.mem.Allocator, packed_bytes: []const u8) Error![]u8 {
-    const total = try estimateUnpackedSize(packed_bytes);
-    const out = try allocator.alloc(u8, total);
-    errdefer allocator.free(out);
-    var len: usize = 0;
-    try check(capnp_packed_decode(packed_bytes.ptr, packed_bytes.len, out.ptr, out.len, &len));
-    std.debug.assert(len == total);
-    return out;
+    var cap: usize = @max(4096, 4 * packed_bytes.len);
+    var attempt: u32 = 0;
+    while (true) : (attempt += 1) {
+        const out = try allocator.alloc(u8, cap);
+        var len: usize = 0;
+        const st = capnp_packed_decode(packed_bytes.ptr, packed_bytes.len, out.ptr, out.len, &len);
+        if (st == @intFromEnum(Status.out_of_space) and len > cap and attempt == 0) {
+            allocator.free(out);
+            cap = len;
+            continue;
+        }
+        check(st) catch |err| {
+            allocator.free(out);
+            return err;
+        };
+        return allocator.realloc(out, len);
+    }
 }
 
 pub const ReadResult = struct { framed: []u8, consumed: usize };
