@@ -447,9 +447,13 @@ def skewed_leg(args, dev, n=1 << 20, reps=10):
     ok = bool((pst == 0).all().item() and (ust == 0).all().item() and torch.equal(ulen, sizes)
               and torch.equal(d_out, d_in))
     big = sizes > 4096
-    return {"units": n, "unpacked_bytes": U, "units_over_4KiB": int(big.sum().item()),
+    P = int(plen.sum().item())
+    alg = U + P + META_BYTES_PER_UNIT * n  # per direction, as the headline's roofline
+    return {"units": n, "unpacked_bytes": U, "packed_bytes": P, "units_over_4KiB": int(big.sum().item()),
             "bytes_in_units_over_4KiB": int(sizes[big].sum().item()),
-            "encode_ms": round(em, 4), "decode_ms": round(dm, 4),
+            "encode_ms": round(em, 4), "decode_ms": round(dm, 4), "alg_bytes": alg,
+            "encode_frac": round(alg / (em * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "decode_frac": round(alg / (dm * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "GiB_s": round(U / ((em + dm) * 1e-3) / 2 ** 30, 2),
             "packed_ratio": round(int(plen.sum().item()) / U, 4), "bit_exact_roundtrip": ok,
             "note": "SURVEY config C5: truncated Pareto unit sizes 64 B..256 KiB, p = zero_thresh/256"}
@@ -564,8 +568,13 @@ def message_leg(args, dev, reps=10, segs=4, seg_words=127):
     t_init = timed(lambda: cp.message_init_batch(d_out, f_off, f_len, segs, cnt, so, sl, mst, stream=stream))
     ok = ok and bool(torch.equal(d_out, framed) and (mst == 0).all().item() and (cnt == segs).all().item()
                      and (sl == sb).all().item())
-    return {"messages": n, "segments_per_message": segs, "framed_bytes": fb,
+    P = int(plen.sum().item())
+    # encode: the segment words + headers out of the pool, P written, per-message metadata
+    # (segment pointer / length / first / count and the slot arrays) ~ 44 B + 20 B per segment
+    alg = n * fb + P + (META_BYTES_PER_UNIT + 20 * segs) * n
+    return {"messages": n, "segments_per_message": segs, "framed_bytes": fb, "packed_bytes": P,
             "fused_encode_ms": round(t_fused, 4), "tobytes_copy_plus_encode_ms": round(t_unfused, 4),
+            "alg_bytes": alg, "encode_frac": round(alg / (t_fused * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "fused_GiB_s": round(n * fb / (t_fused * 1e-3) / 2 ** 30, 2),
             "message_init_ms": round(t_init, 4), "bit_exact": ok,
             "note": "GiB/s of framed bytes; fused = encode_message_batch from segment lists (no framed copy)"}
@@ -600,8 +609,10 @@ def read_message_leg(args, dev, reps=10):
     ms = ev[0].elapsed_time(ev[1]) / reps
     ok = bool((wl.ust == 0).all().item() and torch.equal(used, wl.plen) and torch.equal(wl.d_out, wl.d_in))
     P = int(wl.plen.sum().item())
+    alg = n * ub + P + META_BYTES_PER_UNIT * n + 8 * n  # + consumed (8 B per stream)
     return {"ms": round(ms, 4), "GiB_s": round(n * ub / (ms * 1e-3) / 2 ** 30, 2),
-            "alg_GB_s": round((n * ub + P + 8 * n + 48 * n) / (ms * 1e-3) / 1e9, 1),
+            "alg_bytes": alg, "alg_GB_s": round(alg / (ms * 1e-3) / 1e9, 1),
+            "decode_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "messages": n, "framed_bytes": ub, "bit_exact": ok,
             "note": "GiB/s of framed (unpacked) bytes; header pass + framed-length walk + indexed decode"}
 
@@ -717,8 +728,29 @@ def launch_ranks(args):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    return max(rcs, key=abs)
+    # poll every rank: when one fails, the others would block in their collectives, so
+    # they are terminated (then killed after a grace period) and the failure is returned
+    failed = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            break
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.time() + 15
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return failed
 
 
 def dry_run(args, world, rank):
@@ -766,6 +798,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run and os.environ.get("CPK_DRY_RUN_FAIL_RANK") == str(rank):
+        sys.exit(3)  # test hook (tests/test_bench_launcher.py): a rank that dies before the rendezvous
     if args.dry_run:
         if args.units == 1 << 20:
             args.units = 64

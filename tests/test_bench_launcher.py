@@ -41,6 +41,19 @@ def test_launcher_single_rank():
     assert res["n_gpus"] == 1 and len(res["packed_totals"]) == 1
 
 
+def test_launcher_stops_the_other_ranks_when_one_fails():
+    # rank 1 exits before the rendezvous: rank 0 would wait in it for 30 minutes; the
+    # launcher notices, terminates rank 0 and returns rank 1's status
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CPK_DRY_RUN_FAIL_RANK"] = "1"
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--gpus", "2", "--units", "8"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 3, out.stderr[-2000:]
+    assert time.time() - t0 < 90
+
+
 @pytest.mark.gpu
 def test_same_gpu_rehearsal_two_ranks():
     # the N-rank GPU step (bench.py --gpus 2 --same-gpu): both ranks code their own units
