@@ -5,21 +5,38 @@
 //   decode  message.zig:88-145 (unpackPacked) with the size pass of :152-191
 //
 // Execution model. No MFMA: this is byte compaction, HBM-bound.
-//   encode  one 64-lane wave per unit of <= 512 words (encode_kernel): the unit is
-//           staged in the wave's LDS slice with coalesced 16-B loads; lane j owns
-//           words [8j, 8j+8); zero-byte tags come from SWAR + a multiply gather;
-//           greedy 256-capped zero / literal runs are resolved with wave max/min
-//           scans of break positions; a wave sum scan gives each lane its output
-//           offset; lanes OR their records into an LDS byte stream that is written
-//           back with coalesced stores. Longer units: encode_tiled_kernel, tile by
-//           tile with run carries, on a side stream beside the main grid.
-//   decode  the record chain (tag -> record length -> next tag) is serial. Pass 1
-//           (decode_index_kernel) walks every unit's chain once, lane per unit,
-//           with quad-coalesced loads into an LDS ring, and leaves one u16 record
-//           per 16-B piece; pass 2 (decode_fill_kernel, wave per unit) starts every
-//           lane at its own pieces' first tag, lists the source of each output word
-//           and expands with coalesced stores. Units the fill pass cannot stage go
-//           to decode_wave_kernel (wave per unit, windowed) on the side stream.
+// Every batch is first split into size classes (class_count / class_scan /
+// class_scatter): small units (lane per unit), mid units (wave per unit)
+// and long units (> one 512-word tile / > 5 KiB packed), which run on a side stream of
+// the caller's stream, beside the main grid.
+//   encode  small: encode_small_kernel, lane per unit. Mid: one 64-lane wave per unit of
+//           <= 512 words (encode_kernel): the unit is staged in the wave's LDS slice
+//           with coalesced 16-B loads; lane j owns words [8j, 8j+8); zero-byte tags come
+//           from SWAR + a multiply gather; greedy 256-capped zero / literal runs are
+//           resolved with wave max/min scans of break positions; a wave sum scan gives
+//           each lane its output offset; lanes OR their records into an LDS byte stream
+//           written back with coalesced stores. Long: tile-parallel (long_tiles_kernel,
+//           tile_encode_kernel: each 512-word tile coded by its own wave from the run
+//           carries it reads back from the input, sizes then writes); units the tile
+//           table cannot hold go to encode_tiled_kernel (tile by tile, one wave).
+//   decode  the record chain (tag -> record length -> next tag) is serial. Small:
+//           decode_small_kernel, lane per unit. Mid: pass 1 (decode_index_kernel) walks
+//           every unit's chain once, lane per unit, with quad-coalesced loads into an LDS
+//           ring, and leaves one u16 record per 16-B piece; pass 2 (decode_fill_kernel,
+//           wave per unit) starts every lane at its own pieces' first tag, lists the
+//           source of each output word (runs' later words filled by a wave scan) and
+//           expands with coalesced stores. Opt-in alternative for mid units: the fused
+//           single-pass decoder (decode_fused_kernel). Long: window-parallel
+//           (long_windows / window_spec / window_resolve / window_fill: 4608-B windows
+//           speculated from every entry state, resolved in order per unit, expanded in
+//           parallel); units the window table cannot hold go to decode_wave_kernel
+//           (wave per unit, window by window). The size pass (estimateUnpackedSize) is
+//           the index walk without records for mid units and window_spec / window_resolve
+//           for long ones.
+//   also    Reader.readPackedMessage batched (read_header_kernel + gated index / fill
+//           passes), framing fused with encode (encode_message_kernel), Message.init
+//           (message_init_kernel), Message.validate (validate_kernel), synthetic data
+//           (generate_kernel) and the offsets scan.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
