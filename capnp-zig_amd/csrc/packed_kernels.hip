@@ -2307,7 +2307,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 }
 
 // ---------------------------------------------------------------------------
-// DECODE, fused single pass (round 3; DESIGN.md §2.3): the packed bytes cross HBM once
+// DECODE, fused single pass (round 3; DESIGN.md §2.3a): the packed bytes cross HBM once
 // and no piece records exist. One wave per unit, persistent grid, the next unit's pieces
 // prefetched into registers while this one is decoded (as decode_fill_kernel).
 //   stage  the unit's pieces go to the wave's LDS window at their 16-B aligned positions
@@ -2326,16 +2326,17 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 //   fix    a lane with unknown states and exactly one FF byte in its block: every unknown
 //          state reached that byte as a tag, so its exit is the exact walk from the FF
 //          record's landing (a landing more than 7 bytes past the block is "far": 0xFE);
-//   scan   a DPP prefix composition of the maps (6 steps, two v_perm each) gives every
-//          lane its entry state; lane 0's entry is s (a 0x7F tag at s - 8 when s >= 8);
-//   serial the first lane whose entry is unknown follows a lane whose own state there is
-//          far (its exit is known) or unresolved (several FF bytes: an exact walk from its
-//          entry); the scan restarts after the exit's lane (p = 0.5: ~0.4 per unit);
-//   count  each lane walks its records from its entry (exact): words and UnexpectedEof
-//          (a record running past the unit) before any output, as unpackPacked;
-//   codes, expansion: decode_fill_kernel's code walk and expansion.
-// Exactness does not depend on the data: every state the maps cannot carry is either
-// resolved exactly (fix) or walked (serial).
+//   scan   unknown / far states are replaced by a guess (7), and a DPP prefix composition
+//          of the maps (6 steps, two v_perm each) gives every lane a speculative entry;
+//          lane 0's entry is s (a 0x7F tag at s - 8 when s >= 8);
+//   count  each lane walks its records from its entry (exact lengths), listing their
+//          positions; an exclusive max-scan of the lanes' exits checks every entry against
+//          the left neighbour's exit, and lanes whose entry was wrong walk again from the
+//          corrected one until no lane changes (exact: lane 0's entry is known, and each
+//          round fixes at least the first wrong lane). Then words and UnexpectedEof (a
+//          record running past the unit) before any output, as unpackPacked;
+//   codes, expansion: codes from the listed records, decode_fill_kernel's expansion.
+// Exactness does not depend on the data: guesses only cost re-walks.
 constexpr uint32_t kFuWaves = 4;
 constexpr uint32_t kFuPk = kFlPieces * 16 + 32;  // 64 lanes x L <= 5 pieces + the 32-B 0x7F lookahead
 constexpr uint32_t kFuFar = 0xFEu;               // map state: exit more than 7 bytes past the block
