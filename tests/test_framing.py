@@ -55,3 +55,14 @@ def test_empty_builder_has_one_segment():
 def test_message_init_errors(data, exc):
     with pytest.raises(exc):
         cp.Message.init(data)
+
+
+def test_validate_of_message_without_segments_is_empty_message():
+    # message.zig:700: validate on a message with no segments (e.g. after deinit) raises
+    # EmptyMessage before any device work
+    m = cp.Message.init(open(os.path.join(FIX, "fixture_single.bin"), "rb").read())
+    m.deinit()
+    with pytest.raises(cp.EmptyMessage):
+        m.validate()
+    with pytest.raises(cp.EmptyMessage):
+        cp.Message([], None).validate()
