@@ -2009,11 +2009,10 @@ constexpr uint32_t kFlMaxL = 5;                   // pieces per lane (kFlPieces 
 // bytes q+1 .. q+8 its packed bytes (a mixed record, or an FF record's first word,
 // whose tag 0xFF selects all 8 bytes), kFlLit | q for a literal word at q+1 .. q+8
 // (an FF run's body), or kFlZero.
-// A zero run's first word is kFlZeroHead; the rest of the run and an FF run's body are
-// left as kFlZero by the code walk and resolved from the last head before them (fl_bodies).
+// The body of an FF run whose record starts in the pass is left as kFlZero by the code
+// walk and filled in afterwards from the FF head before it (fl_bodies).
 constexpr uint32_t kFlLit = 0x2000u;
 constexpr uint32_t kFlZero = 0xFFFFu;
-constexpr uint32_t kFlZeroHead = 0xFFFEu;
 constexpr uint32_t kFlPos = 0x1FFFu;
 static_assert(kFlPk < kFlPos, "codes hold window positions");
 
@@ -2056,36 +2055,37 @@ __device__ __forceinline__ uint64_t fill_word(const uint8_t* pk, const uint64_t*
     const uint32_t t = (code & kFlLit) ? 0xFFu : (uint32_t)(lo >> sh) & 0xFFu;
     const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));  // bytes q+1 .. q+8
     const uint64_t w = perm64(pay, lut[t]);
-    return code >= kFlZeroHead ? 0ull : w;
+    return code == kFlZero ? 0ull : w;
 }
 
-// Codes of the words the code walk left as kFlZero (a record's words after its first): lane l
-// takes codes [8l, 8l + 8) of the pass, the last head before each (an exclusive max-scan of
-// (index + 1) << 16 | code over the lanes) decides it. After a zero head it stays a zero word;
-// after an FF head at q it is the literal word k words on, kFlLit | (q + 1 + 8k); after a
-// literal code kFlLit | q (an FF body continued from the previous pass) it is kFlLit | (q + 8k).
-// message.zig:101-141 (the words of one 00 / FF record).
-__device__ __forceinline__ void fl_bodies(uint16_t* code, uint32_t nw, uint32_t lane) {
-    uint4 cv = reinterpret_cast<const uint4*>(code)[lane];
-    uint32_t c[8] = {cv.x & 0xFFFFu, cv.x >> 16, cv.y & 0xFFFFu, cv.y >> 16,
-                     cv.z & 0xFFFFu, cv.z >> 16, cv.w & 0xFFFFu, cv.w >> 16};
+// FF run bodies of a code pass (message.zig:112-128): the code walk writes only each
+// record's first word, so a body's c literal words are still kFlZero, like the words of a
+// zero run. Lane l takes codes [8l, 8l + 8): the last written code before each (an
+// exclusive max-scan of (index + 1) << 16 | code over the lanes) decides it: after an FF
+// head at q (tag byte 0xFF, count c = byte q + 9) the word k words on, k <= c, is the
+// literal kFlLit | (q + 1 + 8k); any other kFlZero word is a zero word.
+__device__ __forceinline__ void fl_bodies(const uint8_t* pk, uint16_t* code, uint32_t nw, uint32_t lane) {
+    uint16_t* const c = code + 8 * lane;  // read from LDS one at a time: few live registers
     uint32_t lh = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) lh = c[i] != kFlZero ? ((8u * lane + i + 1u) << 16) | c[i] : lh;
-    uint32_t h = fu_prev_lane(wave_incl_max(lh, lane));
-#pragma unroll
+#pragma unroll 1
     for (int i = 0; i < 8; ++i) {
-        const uint32_t idx = 8u * lane + i;
-        if (c[i] != kFlZero) {
-            h = ((idx + 1u) << 16) | c[i];
-        } else if (h != 0 && idx < nw) {
-            const uint32_t hc = h & 0xFFFFu, k = idx + 1u - (h >> 16);
-            const uint32_t b = (hc & kFlLit) ? (hc & kFlPos) : hc + 1u;
-            c[i] = hc == kFlZeroHead ? kFlZero : (kFlLit | (b + 8u * k));
+        const uint32_t ci = c[i];
+        lh = ci != kFlZero ? ((8u * lane + i + 1u) << 16) | ci : lh;
+    }
+    uint32_t h = fu_prev_lane(wave_incl_max(lh, lane));
+    uint32_t body = 0;  // the FF head's count c (0: no body)
+    if (h != 0 && !(h & kFlLit)) body = pk[h & kFlPos] == 0xFFu ? pk[(h & kFlPos) + 9] : 0u;
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t idx = 8u * lane + i, ci = c[i];
+        if (ci != kFlZero) {
+            h = ((idx + 1u) << 16) | ci;
+            body = !(ci & kFlLit) && pk[ci] == 0xFFu ? pk[ci + 9] : 0u;
+        } else if (idx < nw) {
+            const uint32_t k = idx + 1u - (h >> 16);
+            if (k <= body) c[i] = (uint16_t)(kFlLit | ((h & kFlPos) + 1u + 8u * k));
         }
     }
-    cv = make_uint4(c[0] | (c[1] << 16), c[2] | (c[3] << 16), c[4] | (c[5] << 16), c[6] | (c[7] << 16));
-    reinterpret_cast<uint4*>(code)[lane] = cv;
 }
 
 __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uint8_t* __restrict__ in,
@@ -2245,7 +2245,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                 wave_lds_sync();
                 const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
                 uint32_t p = mine ? pos : jend, w = wbase;
-                bool runs = false;  // a record of more than one word in this pass
+                bool runs = false;  // an FF body starts in this pass (fl_bodies)
                 for (;;) {  // one record per lane per pass; predicated body, uniform exit
                     const bool act = p < jend && w < W1;
                     if (__builtin_amdgcn_ballot_w64(act) == 0) break;
@@ -2255,24 +2255,24 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                     uint32_t c9 = pk[pp + 9];
                     asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
                     const bool z = t == 0u, f = t == 0xFFu;
+                    // message.zig:101-141: 00 -> zero word(s) (the list starts as kFlZero), FF ->
+                    // its first word (tag 0xFF selects the 8 bytes) + c literal words (fl_bodies),
+                    // other tags -> scatter of popc(t) bytes
+                    code[(act && !z && w >= W0) ? w - W0 : kFlOut] = (uint16_t)pp;
                     const uint32_t c = f ? c9 : 0u;
-                    const uint32_t nx = (z ? b1 : 0u) + c;  // words after the first
-                    // message.zig:101-141: 00 -> a zero head, FF -> its first word (tag 0xFF
-                    // selects the 8 bytes), other tags -> scatter of popc(t) bytes; the words
-                    // after a record's first stay kFlZero for fl_bodies. An FF body that started
-                    // in an earlier pass continues at word 0 from its literal code there.
-                    const bool head = act && w >= W0, cont = act && f && w < W0 && w + nx >= W0;
-                    const uint32_t cd = z ? kFlZeroHead : (w >= W0 ? pp : (kFlLit | (pp + 1u + 8u * (W0 - w))));
-                    code[head ? w - W0 : (cont ? 0u : kFlOut)] = (uint16_t)cd;
-                    runs |= act && nx != 0;
-                    w = act ? w + 1u + nx : w;
+                    runs |= act && c != 0u;
+                    if (act && c && w < W0) {  // a body continued from an earlier pass (rare)
+                        for (uint32_t i = W0 - w; i <= c && w + i < W1; ++i)
+                            code[w + i - W0] = (uint16_t)(kFlLit | (pp + 1 + 8 * i));
+                    }
+                    w = act ? w + 1u + (z ? b1 : 0u) + c : w;
                     p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
                 }
                 FL_T(t4);
                 FL_ACC(3, t4 - t3);
                 wave_lds_sync();
                 if (__builtin_amdgcn_ballot_w64(runs) != 0) {
-                    fl_bodies(code, W1 - W0, lane);
+                    fl_bodies(pk, code, W1 - W0, lane);
                     wave_lds_sync();
                 }
                 // ---- expand by output word: coalesced stores straight from registers ----------
