@@ -123,16 +123,20 @@ pub extern "capnp_packed" fn capnp_packed_lengths_to_offsets(
     d_scratch: ?*anyopaque, scratch_bytes: usize, stream: ?*anyopaque,
 ) c_int;
 
-/// Single-buffer crossover (DESIGN.md §6.1, profiles/r02_crossover.json, MI355X + EPYC 9575F
-/// host): one packPacked / unpackPacked call through the single-buffer C-ABI (H2D, kernels,
-/// D2H, sync: ~75 us fixed) against the Zig body's algorithm on one core.
-///   pack:   the device is faster from 64 KiB (184 vs 270 us; 16 MiB: 25 vs 93 ms).
-///   unpack: the device is never faster for ONE buffer: a unit is decoded by one wave
-///           (the chain of records is serial), 16 MiB: 605 vs 45 ms.
+/// Single-buffer crossover (DESIGN.md §6.1, profiles/r03_crossover.json, MI355X + EPYC 9575F
+/// host, p = 0.5): one packPacked / unpackPacked call through the single-buffer C-ABI
+/// (pinned staging, one H2D, kernels, D2H, sync: ~75-100 us fixed) against the Zig body's
+/// algorithm on one core, caller-owned buffers on both sides.
+///   pack:   the device is faster from 64 KiB (99 vs 262 us; 16 MiB: 1.6 vs 80 ms).
+///   unpack: the device is faster from 64 KiB unpacked (41 KB packed: 122 vs 126 us; 164 KB
+///           packed: 164 vs 631 us; 16 MiB: 2.7 vs 43 ms). The threshold below is on the
+///           packed length (what unpackPacked sees): 64 KiB packed is ~100 KiB unpacked here,
+///           ahead of the crossover, and zero-heavy messages (more output per packed byte)
+///           favour the device further.
 /// Below these sizes the patched message.zig keeps its own body; batches (many units per
-/// call, capnp_packed_*_batch) are where the device pays off.
+/// call, capnp_packed_*_batch) are where the device pays off most.
 pub const gpu_pack_min_bytes: usize = 64 * 1024;
-pub const gpu_unpack_min_bytes: usize = std.math.maxInt(usize);
+pub const gpu_unpack_min_bytes: usize = 64 * 1024;
 
 /// The reference's error names, plus the two the device can add. `NoDevice`
 /// lets the patched message.zig fall back to its own Zig body.
