@@ -3632,6 +3632,10 @@ constexpr uint32_t kSdRing = 80;  // LDS bytes per lane: the 64-B ring + 16 B (f
 // (the slot is 8-B aligned; gfx950 global stores accept that), or the even word alone
 // when only it fits.
 __device__ __forceinline__ void store_pair(uint64_t* dst, uint32_t w, uint32_t capw, uint64_t even, uint64_t odd) {
+#ifdef CPK_DIAG_NOSTORE
+    if (odd == 0x0123456789ABCDEFull) dst[0] = even;  // diagnostic build: (almost) no output stores
+    return;
+#endif
     if (w < capw) {
         const u32x4 v = {(uint32_t)even, (uint32_t)(even >> 32), (uint32_t)odd, (uint32_t)(odd >> 32)};
         *reinterpret_cast<u32x4*>(dst + w - 1u) = v;
@@ -3799,6 +3803,211 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             }
         }
     }
+}
+
+// unpackPacked (message.zig:88-145) for small units, a GROUP of units per wave (round 3,
+// DESIGN.md §2.6). decode_small_kernel's lanes each stream their own unit: every load and
+// store of a wave goes to 64 different units, 16 B each, and the partly written lines those
+// stores leave behind make HBM traffic 2-3x the bytes (C5 PMC: 428 MB written for ~130 MB of
+// output). Here a wave takes up to 64 consecutive units of the small list whose packed pieces
+// fit kSgP bytes of LDS and whose capacities fit kSgW words:
+//   1. meta: lane i reads entry i's offsets / lengths (one coalesced load per array); wave
+//      scans of the pieces and capacity words give each unit its LDS offsets;
+//   2. load: the group's 16-B pieces, flattened (piece j -> its unit by a binary search of
+//      the piece prefix in LDS), 64 per instruction, contiguous within each unit;
+//   3. decode: lane i walks unit i's records from LDS (one record per pass on every lane,
+//      predicated as decode_small_kernel), writing its words into its LDS output slot;
+//   4. store: the OK units' words, flattened by 16-B pairs the same way, so the stores of a
+//      wave write whole runs of each unit's slot.
+// A unit is written only when it decodes OK within its capacity: small units are
+// all-or-nothing too (message.zig:90 raises before any output), like mid and long units.
+// Opt-in (CPK_SMALL=group): measured slower than decode_small_kernel, because a group's
+// decode phase waits for its longest unit (C5's sizes are heavy-tailed) while the lane
+// kernel refills each lane as its unit ends.
+constexpr uint32_t kSgWaves = 4;
+constexpr uint32_t kSgP = 4096;   // packed bytes (16-B pieces, from each unit's aligned base) per group
+constexpr uint32_t kSgW = 1024;   // output capacity words per group (8 KiB: any one small unit fits)
+constexpr uint32_t kSgPad = 32;   // read slack past the last piece (a record's count byte, a word's tail)
+static_assert(kSgW * 8 >= kSmDecCap && kSgP >= 16 * ((kSmDecP + 30) / 16), "one small unit fits a group");
+
+// index of the last entry of the wave-ordered prefix table pfx[0..cnt) that is <= j
+__device__ __forceinline__ uint32_t sg_find(const uint32_t* pfx, uint32_t cnt, uint32_t j) {
+    uint32_t lo = 0, hi = cnt;  // pfx[lo] <= j < pfx[hi] (pfx[cnt] = +inf)
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const bool le = mid < cnt && pfx[mid] <= j;
+        lo = (le && mid > lo) ? mid : lo;
+        hi = (!le && mid < hi) ? mid : hi;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
+    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+    const uint32_t* q) {
+    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t pin_all[kSgWaves][kSgP + kSgPad];
+    __shared__ __attribute__((aligned(16))) uint64_t pout_all[kSgWaves][kSgW];
+    __shared__ uint32_t pfx_all[kSgWaves][2][kWave];  // exclusive prefix: pieces, output pairs
+    for (uint32_t i = threadIdx.x; i < 256; i += kSgWaves * kWave) lut[i] = expand_selector(i);
+    __syncthreads();
+    const uint32_t count = q[3];
+    const uint32_t* const list = q + kQHead + n;
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const pin = pin_all[wave];
+    uint64_t* const pout = pout_all[wave];
+    uint32_t* const ppf = pfx_all[wave][0];
+    uint32_t* const opf = pfx_all[wave][1];
+    // a contiguous range of the small list per wave (batch order within the class)
+    const uint32_t gw = blockIdx.x * kSgWaves + wave, GW = gridDim.x * kSgWaves;
+    const uint32_t per = (count + GW - 1) / GW;
+    uint64_t cursor = (uint64_t)gw * per;
+    const uint64_t last = min((uint64_t)count, cursor + per);
+#ifdef CPK_FILL_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    while (cursor < last) {  // wave-uniform
+        FL_T(t0);
+        // ---- 1. meta of the next (up to) 64 entries -----------------------------------------
+        const bool valid = cursor + lane < last;
+        uint32_t unit = 0, P = 0, s = 0, np = 0, capw = 0;
+        uint64_t src = 0, dst = 0, cap = 0;
+        if (valid) {
+            unit = list[cursor + lane];
+            const uint64_t off = in_off[unit];
+            P = (uint32_t)in_len[unit];  // <= kSmDecP
+            cap = out_cap[unit];         // <= kSmDecCap
+            dst = reinterpret_cast<uint64_t>(out + out_off[unit]);
+            src = reinterpret_cast<uint64_t>(in + off);
+            s = (uint32_t)(src & 15);
+            np = P ? (s + P + 15) >> 4 : 0u;
+            capw = (uint32_t)(cap >> 3);
+        }
+        const uint32_t ip = wave_incl_sum(valid ? np : 0u, lane);
+        const uint32_t iw = wave_incl_sum(valid ? capw : 0u, lane);
+        const bool fits = valid && 16u * ip <= kSgP && iw <= kSgW;  // prefix-monotone
+        const uint32_t g = (uint32_t)__popcll(__ballot(fits));     // >= 1: one small unit always fits
+        const bool mine = lane < g;
+        const uint32_t pb = ip - np, wb = iw - capw;  // this unit's first piece / output word
+        const uint32_t NP = readlane(ip, g - 1);
+        wave_lds_sync();  // the previous group's LDS reads are done
+        ppf[lane] = mine ? pb : 0xFFFFFFFFu;
+        wave_lds_sync();
+        FL_T(t1);
+        FL_ACC(0, t1 - t0);
+        // ---- 2. load the group's pieces, flattened ------------------------------------------
+        // piece j of the group: its unit k (binary search of the piece prefix), then 16 B from
+        // the unit's aligned base (all lanes take part in the bpermutes; past NP they re-load
+        // the last piece and store nothing)
+        auto piece = [&](uint32_t j) {
+            const uint32_t jj = j < NP ? j : NP - 1;
+            const uint32_t k = sg_find(ppf, g, jj);
+            const uint64_t base = (uint64_t)__shfl((long long)src, (int)k, kWave) & ~15ull;
+            const uint32_t pk0 = (uint32_t)__shfl((int)pb, (int)k, kWave);
+            return *reinterpret_cast<const uint4*>(base + 16ull * (jj - pk0));
+        };
+        for (uint32_t j0 = 0; j0 < NP; j0 += 2 * kWave) {  // two loads in flight per lane
+            const uint32_t ja = j0 + lane, jb = j0 + kWave + lane;
+            const uint4 va = piece(ja);
+            const uint4 vb = piece(jb);
+            if (ja < NP) *reinterpret_cast<uint4*>(pin + 16 * ja) = va;
+            if (jb < NP) *reinterpret_cast<uint4*>(pin + 16 * jb) = vb;
+        }
+        wave_lds_sync();
+        FL_T(t2);
+        FL_ACC(1, t2 - t1);
+        // ---- 3. decode: lane i walks unit i -------------------------------------------------
+        const uint8_t* const b = pin + (mine ? 16 * pb : 0u);
+        uint64_t* const o = pout + (mine ? wb : 0u);
+        uint32_t pos = s, end = s + P, lit = 0, wo = 0;
+        int32_t st = ST_OK;
+        bool act = mine && P > 0;
+        if (mine && (dst & 7)) {
+            st = ST_ARG;
+            act = false;
+        }
+        for (;;) {  // one record per lane per pass; predicated body, uniform exit
+            const bool go = act && (lit != 0 || pos < end);
+            if (__ballot(go) == 0) break;
+            const bool isl = lit != 0;
+            const uint32_t p0 = go ? pos : 0u;
+            const uint32_t qq = isl ? p0 - 1 : p0;  // a literal word reads as if after an FF tag at pos - 1
+            uint32_t t = b[p0];
+            uint32_t b1 = b[p0 + 1];
+            uint32_t c9 = b[p0 + 9];
+            const uint32_t a = (qq + 1) & ~7u;
+            uint64_t lo = *reinterpret_cast<const uint64_t*>(b + a);
+            uint64_t hi = *reinterpret_cast<const uint64_t*>(b + a + 8);
+            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9), "+v"(lo), "+v"(hi));  // one LDS round trip
+            const uint32_t sh = ((qq + 1) & 7) * 8;
+            const uint64_t pay = (lo >> sh) | ((hi << 1) << (63 - sh));  // bytes qq+1 .. qq+8
+            const bool z = !isl && t == 0u, f = !isl && t == 0xFFu;
+            // message.zig:101-141: 00 c -> c+1 zero words; FF w c -> w, then c literal words;
+            // other tags -> popc(t) bytes scattered to the set bits
+            const uint32_t len = isl ? 8u : 1u + __popc(t) + (uint32_t)(z | f);
+            const bool eof = go && !isl && (pos + len > end || (f && pos + 10u + 8u * c9 > end));
+            const bool ok = go && !eof;
+            const uint64_t word = perm64(pay, lut[isl ? 0xFFu : t]);  // lut[0] = zero word
+            if (ok && wo < capw) o[wo] = word;
+            const uint32_t zr = (ok && z) ? b1 : 0u;  // the zero run's further words
+            for (uint32_t j = 1; j <= zr; ++j)
+                if (wo + j < capw) o[wo + j] = 0ull;
+            pos = ok ? pos + len : pos;
+            lit = ok ? (isl ? lit - 1u : (f ? c9 : 0u)) : lit;
+            wo = ok ? wo + 1u + zr : wo;
+            if (eof) {
+                st = ST_EOF;
+                act = false;
+            }
+        }
+        if (mine && st == ST_OK && wo > capw) st = ST_SPACE;
+        FL_T(t3);
+        FL_ACC(2, t3 - t2);
+        // ---- 4. store the OK units' words, flattened by 16-B pairs -----------------------------
+        const uint32_t npair = (mine && st == ST_OK) ? (wo + 1) >> 1 : 0u;
+        const uint32_t ipr = wave_incl_sum(npair, lane);
+        const uint32_t NPR = readlane(ipr, g - 1);
+        opf[lane] = mine ? ipr - npair : 0xFFFFFFFFu;
+        wave_lds_sync();  // step 3's output words and the pair prefix are visible
+        const uint32_t NPR64 = (NPR + kWave - 1) / kWave * kWave;  // wave-uniform trip count
+        for (uint32_t j = lane; j < NPR64; j += kWave) {
+            const uint32_t jj = j < NPR ? j : (NPR ? NPR - 1 : 0u);
+            const uint32_t k = sg_find(opf, g, jj);
+            const uint64_t d = (uint64_t)__shfl((long long)dst, (int)k, kWave);
+            const uint32_t k0 = (uint32_t)__shfl((int)(ipr - npair), (int)k, kWave);
+            const uint32_t kw = (uint32_t)__shfl((int)wo, (int)k, kWave);
+            const uint32_t kb = (uint32_t)__shfl((int)wb, (int)k, kWave);
+            if (j < NPR) {
+                const uint32_t w = 2 * (jj - k0);
+                uint64_t* const gd = reinterpret_cast<uint64_t*>(d) + w;
+                const uint64_t x0 = pout[kb + w];
+                if (w + 1 < kw) {
+                    const uint64_t x1 = pout[kb + w + 1];
+                    const u32x4 vv = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
+                    *reinterpret_cast<u32x4*>(gd) = vv;
+                } else {
+                    *gd = x0;
+                }
+            }
+        }
+        if (mine) {
+            out_len[unit] = st == ST_OK || st == ST_SPACE ? 8ull * wo : 0ull;
+            status[unit] = st;
+        }
+        cursor += g;
+        FL_T(t4);
+        FL_ACC(3, t4 - t3);
+        FL_ACC(4, g);
+        FL_ACC(5, 1);
+    }
+#ifdef CPK_FILL_PROF
+    if (lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -4763,6 +4972,15 @@ static std::atomic<int>& decoder_setting() {
     }());
     return v;
 }
+// Small-unit decoder: 1 the lane-streaming kernel (default), 0 the group-staged kernel
+// (CPK_SMALL=group: all-or-nothing for small units too, but slower).
+static int small_variant() {
+    static const int v = [] {
+        const char* e = getenv("CPK_SMALL");
+        return (e && std::string(e) == "group") ? 0 : 1;
+    }();
+    return v;
+}
 static int decoder_variant() {
     const int v = decoder_setting().load(std::memory_order_relaxed);
     return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
@@ -4811,7 +5029,12 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     // index pass, fill pass; the fallback owns the long units from the start
     // (decode_long_unit): it goes first, on the side stream, beside passes 1 and 2
     static const uint32_t sm_res = resident_blocks(decode_small_kernel, kSmBlock, 8);
-    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
+    static const double sm_frac = [] {  // dev knob (same-box A/B): share of the resident grid
+        const char* e = getenv("CPK_SM_FRAC");
+        return e ? atof(e) : 1.0;
+    }();
+    const uint32_t sm_cap = std::max(1u, (uint32_t)(sm_res * sm_frac));
+    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_cap);
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
@@ -4835,8 +5058,15 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     window_fill_kernel<<<wfill_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, status, q);
     decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status, q);
-    decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
-                                                             status, q);
+    if (small_variant() == 0) {
+        static const uint32_t sg_res = resident_blocks(decode_small_group_kernel, kSgWaves * kWave, 3);
+        decode_small_group_kernel<<<std::min((n + kSgWaves * kWave - 1) / (kSgWaves * kWave), sg_res),
+                                    kSgWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                   out_len, status, q);
+    } else {
+        decode_small_kernel<<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                 out_len, status, q);
+    }
     const uint32_t* const mid = q + kQHead + 2ull * n;
     // mid units: the indexed two-pass decoder (index pass + fill pass), or the fused
     // single-pass decoder when selected (capnp_packed_set_decoder / CPK_DECODE=fused)

@@ -4,8 +4,9 @@ returns UnexpectedEof / no output before it writes a byte): a mid or long unit w
 status is UNEXPECTED_EOF or OUT_OF_SPACE leaves its output slot exactly as it was.
 Small units (<= 512 packed bytes into <= 8-KiB slots, decoded a lane each in one
 streaming pass) are the documented exception: a failed one may hold
-a prefix of its output, never a byte past its out_cap; a size walk before them cost
-C5 decode 0.70 -> 0.83 ms.
+a prefix of its output, never a byte past its out_cap. The group-staged small decoder
+(CPK_SMALL=group) is all-or-nothing for them too; test_small_group_decoder_all_or_nothing
+runs it in a child process (the choice is read once per process).
 
 Units of each size class are decoded from a dense packed stream
 (unaligned unit starts) into slots pre-filled with a sentinel byte:
@@ -47,6 +48,22 @@ def words(rng, n_words, thr):
 
 @pytest.mark.parametrize("cls,n_words,thr", CLASSES, ids=[c[0] for c in CLASSES])
 def test_failed_units_leave_their_slot_untouched(cls, n_words, thr, decoder):
+    check_class(cls, n_words, thr, strict=False)
+
+
+def test_small_group_decoder_all_or_nothing():
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, CPK_SMALL="group")
+    paths = [os.path.dirname(os.path.abspath(__file__))] + [p for p in sys.path if p]
+    code = ("import sys; sys.path[:0] = %r; import test_gpu_decode_contract as t; "
+            "t.check_class('small', 32, 128, strict=True); t.check_class('small', 16, 230, strict=True)" % paths)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-3000:]
+
+
+def check_class(cls, n_words, thr, strict):
     rng = np.random.default_rng(0xC0DE + n_words)
     n = 384
     data = [words(rng, n_words, thr) for _ in range(n)]
@@ -91,7 +108,7 @@ def test_failed_units_leave_their_slot_untouched(cls, n_words, thr, decoder):
             assert ol[i] == len(ref)
             assert s[:len(ref)].tobytes() == ref, (cls, i)
             assert (s[len(ref):] == SENTINEL).all(), (cls, i, "bytes past out_len written")
-        elif cls == "small":
+        elif cls == "small" and not strict:
             assert (s[caps[i]:] == SENTINEL).all(), (cls, i, int(want), "bytes past out_cap written")
         else:
             assert (s == SENTINEL).all(), (cls, i, int(want), "failed unit wrote into its slot")
