@@ -205,6 +205,7 @@ SIGNATURES = {
     "capnp_packed_stream_queue_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t),
                                                       ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_set_decoder": (ctypes.c_int, [ctypes.c_int]),
+    "capnp_packed_set_all_or_nothing": (ctypes.c_int, [ctypes.c_int]),
 }
 
 # capnp_packed_set_decoder values (include/capnp_packed.h)
@@ -620,6 +621,12 @@ def set_decoder(name: str) -> str:
     if prev < 0 or prev not in DECODERS.values():
         _raise(prev, "set_decoder")
     return {v: k for k, v in DECODERS.items()}[prev]
+
+
+def set_all_or_nothing(on: bool) -> bool:
+    """Small decode units all-or-nothing too (capnp_packed_set_all_or_nothing); returns the
+    previous setting."""
+    return bool(lib().capnp_packed_set_all_or_nothing(1 if on else 0))
 
 
 class decoder:

@@ -315,6 +315,8 @@ int capnp_packed_set_decoder(int decoder) {
     return cpk::set_decoder(decoder);
 }
 
+int capnp_packed_set_all_or_nothing(int on) { return cpk::set_all_or_nothing(on); }
+
 int capnp_packed_stream_release(void* stream) {
     int st = ensure_device();
     if (st) return st;

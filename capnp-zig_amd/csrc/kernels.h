@@ -22,6 +22,7 @@ size_t queue_bytes(uint32_t n);
 
 // capnp_packed_set_decoder: returns the previous setting
 int set_decoder(int decoder);
+int set_all_or_nothing(int on);
 hipError_t release_stream(hipStream_t stream);
 void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept);
 

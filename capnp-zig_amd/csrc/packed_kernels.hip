@@ -1772,8 +1772,13 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 //            status is not OK on entry.
 constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2;
 
+#ifdef CPK_IX_WAVES  // dev A/B: pin the index pass's occupancy (waves per SIMD)
+#define CPK_IX_ATTR __attribute__((amdgpu_waves_per_eu(CPK_IX_WAVES, CPK_IX_WAVES)))
+#else
+#define CPK_IX_ATTR
+#endif
 template <bool SIZE_ONLY, int RD = kRdNone>
-__global__ __launch_bounds__(kWave) void decode_index_kernel(
+__global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
@@ -4972,15 +4977,18 @@ static std::atomic<int>& decoder_setting() {
     }());
     return v;
 }
-// Small-unit decoder: 1 the lane-streaming kernel (default), 0 the group-staged kernel
-// (CPK_SMALL=group: all-or-nothing for small units too, but slower).
-static int small_variant() {
-    static const int v = [] {
+// Small-unit decoder (capnp_packed_set_all_or_nothing; CPK_SMALL=group sets the start
+// value): 1 the lane-streaming kernel (default: a failed small unit may keep a prefix),
+// 0 the group-staged kernel (all-or-nothing for small units too, slower).
+static std::atomic<int>& small_setting() {
+    static std::atomic<int> v([] {
         const char* e = getenv("CPK_SMALL");
         return (e && std::string(e) == "group") ? 0 : 1;
-    }();
+    }());
     return v;
 }
+static int small_variant() { return small_setting().load(std::memory_order_relaxed); }
+int set_all_or_nothing(int on) { return small_setting().exchange(on ? 0 : 1) == 0 ? 1 : 0; }
 static int decoder_variant() {
     const int v = decoder_setting().load(std::memory_order_relaxed);
     return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;

@@ -113,6 +113,8 @@ def test_decoder_selection_round_trips():
         assert cp.set_decoder("fused") == "fused"
     assert cp.set_decoder(prev) == "twopass"
     assert cp.lib().capnp_packed_set_decoder(7) == cp.INVALID_ARGUMENT
+    assert cp.set_all_or_nothing(True) is False
+    assert cp.set_all_or_nothing(False) is True
 
 
 def test_zig_binding_declares_only_header_symbols():

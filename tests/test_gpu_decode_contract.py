@@ -4,9 +4,8 @@ returns UnexpectedEof / no output before it writes a byte): a mid or long unit w
 status is UNEXPECTED_EOF or OUT_OF_SPACE leaves its output slot exactly as it was.
 Small units (<= 512 packed bytes into <= 8-KiB slots, decoded a lane each in one
 streaming pass) are the documented exception: a failed one may hold
-a prefix of its output, never a byte past its out_cap. The group-staged small decoder
-(CPK_SMALL=group) is all-or-nothing for them too; test_small_group_decoder_all_or_nothing
-runs it in a child process (the choice is read once per process).
+a prefix of its output, never a byte past its out_cap; with
+capnp_packed_set_all_or_nothing(1) they are all-or-nothing too (the group-staged decoder).
 
 Units of each size class are decoded from a dense packed stream
 (unaligned unit starts) into slots pre-filled with a sentinel byte:
@@ -51,16 +50,13 @@ def test_failed_units_leave_their_slot_untouched(cls, n_words, thr, decoder):
     check_class(cls, n_words, thr, strict=False)
 
 
-def test_small_group_decoder_all_or_nothing():
-    import os
-    import subprocess
-    import sys
-    env = dict(os.environ, CPK_SMALL="group")
-    paths = [os.path.dirname(os.path.abspath(__file__))] + [p for p in sys.path if p]
-    code = ("import sys; sys.path[:0] = %r; import test_gpu_decode_contract as t; "
-            "t.check_class('small', 32, 128, strict=True); t.check_class('small', 16, 230, strict=True)" % paths)
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
-    assert out.returncode == 0, out.stderr[-3000:]
+def test_small_units_all_or_nothing_when_asked():
+    prev = cp.set_all_or_nothing(True)
+    try:
+        check_class("small", 32, 128, strict=True)
+        check_class("small", 16, 230, strict=True)
+    finally:
+        cp.set_all_or_nothing(prev)
 
 
 def check_class(cls, n_words, thr, strict):

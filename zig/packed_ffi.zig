@@ -105,6 +105,8 @@ pub extern "capnp_packed" fn capnp_packed_validate_batch(
 /// lists, the long-unit tile / window table and the decoder's piece records (~750 B per unit).
 /// d_ws must be 256-B aligned (hipMalloc's alignment); a misaligned one is InvalidArgument.
 pub extern "capnp_packed" fn capnp_packed_batch_workspace_bytes(n: u32) usize;
+/// Small decode units all-or-nothing too (process-wide); returns the previous setting.
+pub extern "capnp_packed" fn capnp_packed_set_all_or_nothing(on: c_int) c_int;
 /// Free the library's context of a caller stream (before destroying the stream).
 pub extern "capnp_packed" fn capnp_packed_stream_release(stream: ?*anyopaque) c_int;
 pub extern "capnp_packed" fn capnp_packed_encode_batch_ws(
