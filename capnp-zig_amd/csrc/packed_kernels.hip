@@ -1231,7 +1231,7 @@ __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __re
     uint64_t capw = 0;
     if (WRITE) {
         uint8_t* o = out + out_off[unit];
-        if (reinterpret_cast<uintptr_t>(o) & 7) {
+        if (P > 0 && (reinterpret_cast<uintptr_t>(o) & 7)) {  // an empty unit writes nothing
             out_len[unit] = 0;
             status[unit] = ST_ARG;
             return;
@@ -1816,7 +1816,7 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
         if (!SIZE_ONLY) {
             dstb = out + out_off[unit];
             cap = out_cap[unit];
-            if (reinterpret_cast<uintptr_t>(dstb) & 7) st = ST_ARG;
+            if (P64 > 0 && (reinterpret_cast<uintptr_t>(dstb) & 7)) st = ST_ARG;  // an empty unit writes nothing
         }
     }
     const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
@@ -3753,8 +3753,8 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             cap = m_cap;
             capw = (uint32_t)(m_cap >> 3);
             wo = 0;
-            if (reinterpret_cast<uintptr_t>(o) & 7) finish(ST_ARG);
-            else if (m_len == 0) finish(ST_OK);
+            if (m_len == 0) finish(ST_OK);  // an empty unit writes nothing: any slot will do
+            else if (reinterpret_cast<uintptr_t>(o) & 7) finish(ST_ARG);
             else kind = SM_FIRST;
         } else if (kind == SM_FIRST) {
             kind = SM_RUN;  // its first pieces enter the ring next turn
@@ -3931,7 +3931,7 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
         uint32_t pos = s, end = s + P, lit = 0, wo = 0;
         int32_t st = ST_OK;
         bool act = mine && P > 0;
-        if (mine && (dst & 7)) {
+        if (mine && P > 0 && (dst & 7)) {
             st = ST_ARG;
             act = false;
         }
