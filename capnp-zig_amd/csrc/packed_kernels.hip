@@ -91,6 +91,8 @@ enum : int32_t {
 };
 // internal status between decode passes: the unit goes to a full (fallback) decoder
 constexpr int32_t kStNeedFull = 0x7FFF0001;
+constexpr int32_t kStNeedWalk = 0x7FFF0002;  // read-message: the one-pass walk could not take the unit
+constexpr int32_t kStNeedGate = 0x7FFF0003;  // read-message: walked (consumed known), records next
 // status of a long unit between its listing and its worker's result
 constexpr int32_t kStPending = CAPNP_PACKED_DEVICE_ERROR;
 
@@ -1764,13 +1766,17 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 //
 // RD selects the Reader.readPackedMessage passes (reader.zig:84-156; launch_read_message):
 //   kRdNone  unpackPacked / estimateUnpackedSize as above;
-//   kRdWalk  size-only walk that stops at the first record boundary where the decoded
-//            words reach out_len[unit] / 8 (the framed length read_header_kernel
-//            derived) and writes the bytes it took to consumed[unit]; units whose
-//            status is not OK on entry are left alone;
-//   kRdGate  the write pass over in_len = consumed, again skipping units whose
-//            status is not OK on entry.
-constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2;
+//   kRdOne   (round 3) the write pass of a whole read in one walk: records and the framed-length
+//            stop together (the bytes a message can take are bounded by 10 per word, so a
+//            stream of any length is walked only that far); a unit whose bound does not fit
+//            the fill pass is left kStNeedWalk for the two passes below;
+//   kRdWalk  size-only walk of the kStNeedWalk units that stops at the first record boundary
+//            where the decoded words reach out_len[unit] / 8 (the framed length
+//            read_header_kernel derived) and writes the bytes it took to consumed[unit]
+//            (status kStNeedGate when it reached the framed length exactly);
+//   kRdGate  the write pass over in_len = consumed of the kStNeedGate units.
+// A unit's status on entry says which pass owns it, so no pass redoes another's work.
+constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2, kRdOne = 3;
 
 #ifdef CPK_IX_WAVES  // dev A/B: pin the index pass's occupancy (waves per SIMD)
 #define CPK_IX_ATTR __attribute__((amdgpu_waves_per_eu(CPK_IX_WAVES, CPK_IX_WAVES)))
@@ -1786,6 +1792,8 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
     const uint32_t* __restrict__ list_count = nullptr, uint8_t* __restrict__ rec = nullptr) {
     static_assert(RD != kRdWalk || SIZE_ONLY, "the read walk writes no output");
     static_assert(RD != kRdGate || !SIZE_ONLY, "the gated pass is the write pass");
+    static_assert(RD != kRdOne || !SIZE_ONLY, "the one-pass read writes records");
+    constexpr bool kStop = RD == kRdWalk || RD == kRdOne;  // the walk stops at the framed length
     constexpr uint32_t kRing = 80;  // [0, 16): block k-1's last piece, [16, 80): block k
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWave * kRing];
     const uint32_t lane = lane_id();
@@ -1801,17 +1809,22 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
     uint64_t P64 = 0, cap = 0;
     uint8_t* dstb = nullptr;
     int32_t st = ST_OK;
-    bool gated = false;       // RD: an earlier pass already settled this unit
-    uint64_t lim_w = ~0ull;   // kRdWalk: words of the framed message
+    bool gated = false;       // RD: another pass owns this unit (or settled it)
+    uint64_t lim_w = ~0ull;   // kStop: words of the framed message
     if (valid) {
-        if (RD != kRdNone) gated = status[unit] != ST_OK;
+        if (RD != kRdNone)
+            gated = status[unit] != (RD == kRdWalk ? kStNeedWalk : RD == kRdGate ? kStNeedGate : ST_OK);
         src = in + in_off[unit];
         P64 = in_len[unit];
-        if (RD == kRdWalk) {
+        if (kStop) {
             lim_w = out_len[unit] >> 3;
             // a message of <= 8 Mi + 257 words takes < 2^31 packed bytes (<= 10 B per word),
             // so the walk always stops before this clamp
             if (P64 > kIxSizeMax - 1) P64 = kIxSizeMax - 1;
+            // kRdOne: the message's bytes are within 10 per framed word (FF record: 10 bytes for
+            // its first word, 8 per literal word; others fewer), so the stream past that is
+            // never walked
+            if (RD == kRdOne && P64 > 10 * lim_w) P64 = 10 * lim_w;
         }
         if (!SIZE_ONLY) {
             dstb = out + out_off[unit];
@@ -1827,7 +1840,7 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
         const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && (rec || cap >= 64 * ((nr + 8) / 8)));
         if (!fits) {
             take = false;
-            st = kStNeedFull;
+            st = RD == kRdOne ? kStNeedWalk : kStNeedFull;
         }
     }
     const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
@@ -1896,7 +1909,7 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
         uint64_t cnt = 0;   // words of the records of piece 4k-1+i (16-bit field i)
         for (;;) {  // one record per lane per pass; branch-free body, uniform exit
             // a finished or failed lane has pos = kIxDead; a read walk stops at the framed length
-            const bool act = pos < lim && (RD != kRdWalk || wrun < lim_w);
+            const bool act = pos < lim && (!kStop || wrun < lim_w);
             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
             // ring offset o = pos + 16 - ob: block k-1's last piece at [0, 16), block k at
             // [16, 80); any pos (kIxDead, or past lim) reads inside the lane's ring
@@ -1915,9 +1928,12 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
             const uint32_t wd = 1u + (z ? b1 : 0u) + (f ? c9 : 0u);  // <= 256: a piece sums to <= 2048
             cnt += (uint64_t)(ok ? wd : 0u) << (o & 48u);            // field o >> 4
             pos = eof ? kIxDead : (ok ? pos + len : pos);
-            if (RD == kRdWalk) wrun += ok ? wd : 0u;
+            if (kStop) wrun += ok ? wd : 0u;
         }
-        if (RD == kRdWalk && __builtin_amdgcn_ballot_w64(pos < end && wrun < lim_w) == 0) break;  // all stopped
+        // every lane stopped (at its framed length, the stream's end or an error)
+        const bool stop = kStop && __builtin_amdgcn_ballot_w64(pos < end && wrun < lim_w) == 0;
+        if (RD == kRdWalk && stop) break;
+        const bool last = k == maxr || stop;  // kRdOne: the record queue is flushed before the break
         words += (cnt & 0xFFFFu) + ((cnt >> 16) & 0xFFFFu) + ((cnt >> 32) & 0xFFFFu) + (cnt >> 48);
         if (!SIZE_ONLY) {
             const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
@@ -1926,7 +1942,7 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
                                ((uint64_t)(__builtin_ctz(hi | 0x10000u) & 15u) << 32) |
                                ((uint64_t)(__builtin_ctz((hi >> 16) | 0x10000u) & 15u) << 48);
             const uint64_t rec = e | (cnt << 4);  // records 4k .. 4k+3 (pieces 4k-1 .. 4k+2)
-            if ((k & 1) || k == maxr) {
+            if ((k & 1) || last) {
                 // records 8g .. 8g+7 (16 B) go to queue entry g % 4 (a uniform switch: no
                 // register indexing); every 8 rounds, and after the last, the queue is stored
                 // as 64 contiguous bytes per lane (4 store instructions, which the vmcnt waits
@@ -1941,7 +1957,7 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
                     case 2: rq2 = v; break;
                     default: rq3 = v; break;
                 }
-                if ((g & 3) == 3 || k == maxr) {
+                if ((g & 3) == 3 || last) {
                     const uint32_t fb = g >> 2;
                     uint8_t* const q = (take && fb < nflush) ? ixp + 64 * fb : cpk_sink64;
                     // transposed through the ring's first 64 B (round k+1 keeps only its last
@@ -1968,17 +1984,38 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
                 rec0 = rec;
             }
         }
+        if (stop) break;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!valid || gated) return;  // gated: status and out_len of an earlier pass stand
-    if (RD == kRdWalk) {
+    if (RD == kRdOne && st == kStNeedWalk) {
+        status[unit] = kStNeedWalk;  // out_len (the framed length) stays for kRdWalk
+        return;
+    }
+    if (RD == kRdOne && st == ST_ARG) {  // a misaligned output slot: nothing consumed
+        out_len[unit] = 0;
+        consumed[unit] = 0;
+        status[unit] = ST_ARG;
+        return;
+    }
+    if (kStop) {
         // reader.zig:91-93 / 146-153: the walk ended at the framed length (OK), past it
         // (InvalidPackedMessage), or the stream ended first (EndOfStream, also for a
         // record cut short: readByte / readNoEof)
         const int32_t rs = (st != ST_OK || wrun < lim_w) ? ST_EOS : (wrun != lim_w ? ST_OVERSHOOT : ST_OK);
-        status[unit] = rs;
         consumed[unit] = rs == ST_OK ? (uint64_t)(pos - s) : 0ull;
-        if (rs != ST_OK) out_len[unit] = 0;
+        if (rs != ST_OK) {
+            out_len[unit] = 0;
+            status[unit] = rs;
+            return;
+        }
+        if (RD == kRdWalk) {
+            status[unit] = kStNeedGate;
+            return;
+        }
+        // kRdOne: records written; the framed length is the decoded size
+        out_len[unit] = 8 * words;
+        status[unit] = 8 * words > cap ? ST_SPACE : ST_OK;
         return;
     }
     if (st == kStNeedFull) {
@@ -4470,15 +4507,17 @@ __global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restri
 // Reader.readPackedMessage, batched (reader.zig:84-156)
 // ---------------------------------------------------------------------------
 // Unit i is one reader's buffered packed stream; one message is decoded from its
-// front. Four passes (launch_read_message):
+// front (launch_read_message):
 //   1. read_header_kernel: lane per unit, decodes records until the segment table
 //      is complete (one record for a 1-segment message) and writes the framed
 //      length to out_len, or the header error to status;
-//   2. decode_index_kernel<true, kRdWalk>: the coalesced tag walk, stopped at the
-//      framed length; writes consumed (packed bytes of the message) and the
-//      EndOfStream / InvalidPackedMessage outcome;
-//   3. + 4. the indexed decoder (index pass kRdGate, fill pass, full-path fallback)
-//      over in_len = consumed, skipping units with a non-OK status.
+//   2. decode_index_kernel<false, kRdOne>: the coalesced tag walk, stopped at the framed
+//      length, writing the piece records as it goes; writes consumed (packed bytes of the
+//      message) and the EndOfStream / InvalidPackedMessage / OutOfSpace outcome. Units
+//      whose bytes the fill pass could not stage go on (kStNeedWalk) to
+//   3. decode_index_kernel<true, kRdWalk> (the walk alone) and decode_index_kernel<false,
+//      kRdGate> (the records over in_len = consumed), as round 2 did for every unit;
+//   4. the fill pass and the full-path fallback over in_len = consumed, for OK units.
 constexpr uint64_t kMaxTotalWords = 8ull * 1024 * 1024;  // reader.zig:6
 constexpr uint64_t kMaxSegments = 512;                   // message.zig:310
 constexpr uint64_t kHdrMaxWords = 257;                   // (1 + 512 + pad) u32 = 257 words
@@ -5132,6 +5171,10 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
     const uint32_t wv = (n + kWave - 1) / kWave;
     read_header_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
                                                                          status);
+    // one walk for the units the fill pass can take: records and the stop at the framed length
+    decode_index_kernel<false, kRdOne><<<wv, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                  out_len, status, consumed);
+    // the rest (kStNeedWalk): the walk to the framed length, then the gated write pass
     decode_index_kernel<true, kRdWalk><<<wv, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                   out_len, status, consumed);
     // the message's own bytes from here on: in_len = consumed
