@@ -86,6 +86,10 @@ def main():
     res["copy_U_GBps"] = round(2 * U / (res.get("copy_U_ms", 1e9) * 1e-3) / 1e9, 1)
     res["fill_U_GBps"] = round(U / (res.get("fill_U_ms", 1e9) * 1e-3) / 1e9, 1)
     ok = bool((ust == 0).all().item()) if ("decode_ms" in res and not a.no_store) else None
+    if "decoded_size_ms" in res:
+        cp.decoded_size_batch(d_pk, pk_off, plen, ulen, ust)
+        torch.cuda.synchronize()
+        res["size_ok"] = bool(torch.equal(ulen, in_len)) and bool((ust == 0).all().item())
     cp.decode_batch(d_pk, pk_off, plen, d_out, in_off, in_len, ulen, ust)
     torch.cuda.synchronize()
     res["roundtrip_ok"] = bool(torch.equal(d_out, d_in)) and ok is not False
