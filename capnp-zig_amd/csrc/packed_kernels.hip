@@ -3141,15 +3141,36 @@ __device__ __forceinline__ TileTab tile_tab(uint32_t* q, uint32_t n) {
 // q[5]: serial units; q[8..9]: tiles reserved (u64); q[10]: serial take cursor
 __device__ __forceinline__ unsigned long long* q_tiles(uint32_t* q) { return reinterpret_cast<unsigned long long*>(q + 8); }
 
+// Consecutive ranges of a shared counter for a wave's lanes (k each, 0: none), in lane order,
+// with ONE atomic per wave: ~10K long units each adding to the one counter serialised at its L2
+// channel while the small-unit kernel loaded the memory system (config C5: 0.21 ms).
+__device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, uint64_t k) {
+    const uint32_t lane = lane_id();
+    uint64_t incl = k;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint64_t o = __shfl_up(incl, d, kWave);
+        if (lane >= (uint32_t)d) incl += o;
+    }
+    const uint64_t total = __shfl(incl, kWave - 1, kWave);
+    uint64_t b = 0;
+    if (lane == 0 && total != 0) b = atomicAdd(ctr, (unsigned long long)total);
+    b = __shfl(b, 0, kWave);
+    return b + incl - k;
+}
+
 __global__ __launch_bounds__(256) void long_tiles_kernel(const uint64_t* __restrict__ in_len, uint32_t n, uint32_t* q) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nh = q[2], nl = q[0];
-    if (i >= nl + nh) return;
-    const uint32_t unit = i < nh ? q[kQHead + n - 1 - i] : q[kQHead + (i - nh)];
     const TileTab t = tile_tab(q, n);
-    const uint64_t k = ((in_len[unit] >> 3) + kEncMaxWords - 1) / kEncMaxWords;  // >= 2 tiles
-    uint64_t base = t.cap;
-    if (k <= t.cap) base = atomicAdd(q_tiles(q), (unsigned long long)k);
+    // as long_windows_kernel: wave-uniform trips, one reservation per wave
+    for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~(kWave - 1)); i0 < nl + nh; i0 += gridDim.x * 256) {
+    const uint32_t i = i0 + lane_id();
+    const bool v = i < nl + nh;
+    const uint32_t unit = !v ? 0u : (i < nh ? q[kQHead + n - 1 - i] : q[kQHead + (i - nh)]);
+    const uint64_t k = v ? ((in_len[unit] >> 3) + kEncMaxWords - 1) / kEncMaxWords : 0ull;  // >= 2 tiles
+    const uint64_t r = wave_reserve(q_tiles(q), (v && k <= t.cap) ? k : 0ull);
+    if (!v) continue;
+    const uint64_t base = k <= t.cap ? r : t.cap;
     if (base + k <= t.cap) {
         for (uint64_t j = 0; j < k; ++j) {
             t.unit[base + j] = unit;
@@ -3158,6 +3179,7 @@ __global__ __launch_bounds__(256) void long_tiles_kernel(const uint64_t* __restr
     } else {
         for (uint64_t j = base; j < t.cap; ++j) t.unit[j] = kTileSkip;  // reserved past the end: unused
         t.serial[atomicAdd(q + 5, 1u)] = unit;
+    }
     }
 }
 
@@ -3329,16 +3351,20 @@ __device__ __forceinline__ WinEnt* win_tab(uint32_t* q, uint32_t n) {
 
 __global__ __launch_bounds__(256) void long_windows_kernel(const uint64_t* __restrict__ in_len, uint32_t n,
                                                            uint32_t* q) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nh = q[2], nl = q[0];
-    if (i >= nl + nh) return;
-    const uint64_t slot = i < nh ? kQHead + n - 1 - i : kQHead + (i - nh);
-    const uint32_t unit = q[slot];
     WinEnt* const e = win_tab(q, n);
     const uint64_t cap = win_cap(n);
-    const uint64_t k = (in_len[unit] + kWvWin - 1) / kWvWin;  // >= 1 (P > 0)
-    uint64_t base = cap;
-    if (k <= cap) base = atomicAdd(q_tiles(q), (unsigned long long)k);
+    // a small grid (list_blocks) striding over the long list, wave-uniform trips; the windows
+    // are reserved with one atomic per wave (wave_reserve)
+    for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~(kWave - 1)); i0 < nl + nh; i0 += gridDim.x * 256) {
+    const uint32_t i = i0 + lane_id();
+    const bool v = i < nl + nh;
+    const uint64_t slot = !v ? 0ull : (i < nh ? kQHead + n - 1 - i : kQHead + (i - nh));
+    const uint32_t unit = v ? q[slot] : 0u;
+    const uint64_t k = v ? (in_len[unit] + kWvWin - 1) / kWvWin : 0ull;  // >= 1 (P > 0)
+    const uint64_t r = wave_reserve(q_tiles(q), (v && k <= cap) ? k : 0ull);
+    if (!v) continue;
+    const uint64_t base = k <= cap ? r : cap;
     if (base + k <= cap) {
         for (uint64_t j = 0; j < k; ++j) {
             e[base + j].unit = unit;
@@ -3349,6 +3375,7 @@ __global__ __launch_bounds__(256) void long_windows_kernel(const uint64_t* __res
         for (uint64_t j = base; j < cap; ++j) e[j].unit = kTileSkip;  // reserved past the end: unused
         q[serial_off(n) + atomicAdd(q + 5, 1u)] = unit;  // the serial list
         q[slot] = kTileSkip;
+    }
     }
 }
 
@@ -4847,6 +4874,10 @@ __global__ __launch_bounds__(256) void scan_apply_kernel(uint64_t* __restrict__ 
 namespace cpk {
 
 static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) / kWavesPerBlock; }
+// Grid of the long-list kernels (long_tiles_kernel, long_windows_kernel): at most 64 blocks
+// striding over the long list, so they start beside a persistent small-unit grid (a block per
+// 256 units of the batch waited ~0.2 ms for slots on config C5, delaying the long-unit chain).
+static inline uint32_t list_blocks(uint32_t n) { return std::min((n + 255u) / 256u, 64u); }
 
 // Side stream for the long-unit kernels (encode_tiled_kernel, the decode fallback).
 // They select their units by a test on the unit's own lengths, so they need nothing
@@ -5080,7 +5111,7 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     const hipStream_t ss = side.stream();
     const uint32_t* const mid = q + kQHead + 2ull * n;
     static const uint32_t tiles_res = resident_blocks(tile_encode_kernel<kTilesWrite, true>, kBlock, 4);
-    long_tiles_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
+    long_tiles_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
     if (write) {
         tile_encode_kernel<kTilesSize, true><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
                                                                              out_cap, out_len, status, q);
@@ -5194,7 +5225,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
         const uint32_t res_blocks = std::min((n + kWvWaves - 1) / kWvWaves, res_res);
         const hipStream_t ss = side.stream();
         const uint32_t ix_blocks = (n + kWave - 1) / kWave;
-        long_windows_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
+        long_windows_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
         window_spec_kernel<<<win_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, q);
         window_resolve_kernel<<<res_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, nullptr, out_len, status, q);
         decode_index_kernel<true><<<ix_blocks, kWave, 0, ss>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
@@ -5247,7 +5278,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const uint32_t res_blocks = std::min((n + kWvWaves - 1) / kWvWaves, res_res);  // up to a wave per long unit
     const uint32_t wfill_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, fill_res);
     const hipStream_t ss = side.stream();
-    long_windows_kernel<<<(n + 255) / 256, 256, 0, ss>>>(in_len, n, q);
+    long_windows_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
     window_spec_kernel<<<win_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, q);
     window_resolve_kernel<<<res_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out_cap, out_len, status, q);
     window_fill_kernel<<<wfill_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, status, q);
