@@ -3833,22 +3833,13 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
 // as the others, a literal word as if it followed an FF tag) -- while pieces k + 4 and
 // k + 5 are in flight into registers; they enter the ring at the start of the next turn.
 // A truncated record is UnexpectedEof with nothing more written.
+// Output (round 3): lanes write to different units, so a lane's own 16-B store is a memory
+// transaction of its own, and those scattered partial-line writes also slowed every kernel
+// beside this one. Each lane stages its words in LDS by absolutely aligned
+// 64-B chunks; after each record pass the wave stores the chunks completed in it, a quad of
+// lanes per chunk (16 chunks of 64 contiguous bytes per store instruction). A unit's partial
+// first and last chunks, and chunks a zero run completes, are stored by their lane.
 constexpr uint32_t kSdRing = 80;  // LDS bytes per lane: the 64-B ring + 16 B (fewer bank conflicts)
-// Words w-1 (even, held back) and w (odd) of an output slot of capw words: one 16-B store
-// (the slot is 8-B aligned; gfx950 global stores accept that), or the even word alone
-// when only it fits.
-__device__ __forceinline__ void store_pair(uint64_t* dst, uint32_t w, uint32_t capw, uint64_t even, uint64_t odd) {
-#ifdef CPK_DIAG_NOSTORE
-    if (odd == 0x0123456789ABCDEFull) dst[0] = even;  // diagnostic build: (almost) no output stores
-    return;
-#endif
-    if (w < capw) {
-        const u32x4 v = {(uint32_t)even, (uint32_t)(even >> 32), (uint32_t)odd, (uint32_t)(odd >> 32)};
-        *reinterpret_cast<u32x4*>(dst + w - 1u) = v;
-    } else if (w - 1u < capw) {
-        dst[w - 1u] = even;
-    }
-}
 __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len, uint32_t n,
@@ -3859,6 +3850,13 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
                                                                 int32_t* __restrict__ status, const uint32_t* q) {
     __shared__ uint64_t lut[256];
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kSmBlock * kSdRing];
+    // each lane's output words by absolutely aligned 8-word (64-B) chunks; a full chunk is
+    // stored by a quad of the wave (4 x 16 B), 16 chunks per store instruction
+    __shared__ __attribute__((aligned(16))) uint64_t ostage_all[kSmBlock * 8];
+    __shared__ __attribute__((aligned(16))) uint64_t ctab_all[(kSmBlock / kWave) * 16 * 2];
+    uint64_t* const ostage = ostage_all + threadIdx.x * 8;
+    uint64_t* const ctab = ctab_all + (threadIdx.x >> 6) * 32;
+    const uint32_t wbase_t = threadIdx.x & ~(kWave - 1);
     lut[threadIdx.x] = expand_selector(threadIdx.x);
     __syncthreads();
     const uint32_t count = q[3];
@@ -3877,10 +3875,44 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
     uint32_t end = 0, pos = 0, k = 0, np = 0, lit = 0;  // aligned space: bytes [s, end); span start piece
     uint4 d0, d1, d2, d3;                                // pieces in flight
     uint64_t* dst = nullptr;
-    uint64_t pend = 0;  // output word at an even index, stored with the next one
     uint32_t capw = 0, wo = 0;
     uint64_t cap = 0;
 
+    constexpr uint32_t SW = 8;
+    uint32_t ph = 0;      // the slot's first word's position in its aligned chunk
+    bool rdy = false;     // a full chunk waits for the wave's flush
+    uint64_t* rdst = nullptr;
+    // the lane itself stores the staged words [lo, hi] (slot word indices) of the chunk ending at e
+    auto flush = [&](uint32_t e, uint32_t lo, uint32_t hi) {
+        const int32_t cb = (int32_t)e - (int32_t)(SW - 1);
+#pragma unroll
+        for (uint32_t pp = 0; pp < SW / 2; ++pp) {
+            const int32_t w0 = cb + 2 * (int32_t)pp, w1 = w0 + 1;
+            const bool v0 = w0 >= (int32_t)lo && w0 <= (int32_t)hi, v1 = w1 >= (int32_t)lo && w1 <= (int32_t)hi;
+            if (v0 | v1) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(ostage + 2 * pp);
+                if (v0 && v1) *reinterpret_cast<u32x4*>(dst + w0) = v;
+                else if (v0) dst[w0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                else dst[w1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+            }
+        }
+    };
+    // word w of the slot, staged at its chunk position; a full chunk is left to the wave's
+    // flush when `defer` (nothing else is staged by this lane before it), else stored at once
+    auto put = [&](uint32_t w, uint64_t word, bool defer) {
+        if (w < capw) {
+            const uint32_t j = (ph + w) & (SW - 1);
+            ostage[j] = word;
+            if (j == SW - 1) {
+                if (defer && w >= SW - 1) {
+                    rdy = true;
+                    rdst = dst + (w - (SW - 1));
+                } else {
+                    flush(w, w >= SW - 1 ? w - (SW - 1) : 0u, w);
+                }
+            }
+        }
+    };
     auto finish = [&](int32_t st) {
         if (st == ST_OK) {
             out_len[unit] = 8ull * wo;
@@ -3954,6 +3986,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             cap = m_cap;
             capw = (uint32_t)(m_cap >> 3);
             wo = 0;
+            ph = (uint32_t)(reinterpret_cast<uintptr_t>(o) >> 3) & (SW - 1);
             if (m_len == 0) finish(ST_OK);  // an empty unit writes nothing: any slot will do
             else if (reinterpret_cast<uintptr_t>(o) & 7) finish(ST_ARG);
             else kind = SM_FIRST;
@@ -3983,26 +4016,50 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             const bool eof = go && !isl && (pos + len > end || (f && pos + 10u + 8u * c9 > end));
             const bool ok = go && !eof;
             const uint64_t word = perm64(pay, lut[isl ? 0xFFu : t]);  // lut[0] = zero word
-            // Output words go out in pairs: an even-index word waits in `pend` and is stored
-            // with its odd neighbour as one 16-B store (lanes write to different units, so
-            // each lane's store is its own transaction: 8-B stores cost the kernel half its
-            // time). A word at capw or beyond is not stored.
-            if (ok && (wo & 1u)) store_pair(dst, wo, capw, pend, word);
-            pend = (ok && !(wo & 1u)) ? word : pend;
+            // Output words are staged in LDS by aligned 64-B chunks (put); a word at capw or
+            // beyond is not stored.
             const uint32_t zr = (ok && z) ? b1 : 0u;  // the zero run's further words
-            for (uint32_t j = 1; j <= zr; ++j) {
-                if ((wo + j) & 1u) store_pair(dst, wo + j, capw, pend, 0ull);
-                else pend = 0ull;
-            }
+            if (ok) put(wo, word, zr == 0u);
+            for (uint32_t j = 1; j <= zr; ++j) put(wo + j, 0ull, false);
             pos = ok ? pos + len : pos;
             lit = ok ? (isl ? lit - 1u : (f ? c9 : 0u)) : lit;
             wo = ok ? wo + 1u + zr : wo;
             if (eof) finish(ST_EOF);
             act = act && !eof;
+            // the wave stores the full chunks of this pass: quad i takes the i-th ready lane's
+            const uint64_t rm = __ballot(rdy);
+            if (rm) {
+                const uint32_t nr = (uint32_t)__popcll(rm);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u));
+                for (uint32_t g = 0; g < nr; g += 16) {
+                    wave_lds_sync();
+                    if (rdy && rank >= g && rank < g + 16) {
+                        ctab[2 * (rank - g)] = reinterpret_cast<uint64_t>(rdst);
+                        ctab[2 * (rank - g) + 1] = lane;
+                    }
+                    wave_lds_sync();
+                    const uint32_t qd = lane >> 2;
+                    if (g + qd < nr) {
+                        uint64_t* const cd = reinterpret_cast<uint64_t*>(ctab[2 * qd]);
+                        const uint32_t sl = (uint32_t)ctab[2 * qd + 1];
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(ostage_all + (wbase_t + sl) * 8 + 2 * (lane & 3));
+                        *reinterpret_cast<u32x4*>(cd + 2 * (lane & 3)) = v;
+                    }
+                }
+                rdy = false;
+            }
         }
         if (act) {  // still running: done, or the next span
             if (pos >= end && lit == 0) {
-                if ((wo & 1u) && wo - 1u < capw) dst[wo - 1u] = pend;  // the last word waiting
+                // the last staged chunk, if its last word is not the chunk's last (a unit that
+                // overran its slot stopped staging at word capw - 1)
+                const uint32_t lw = min(wo, capw);  // words staged
+                if (lw > 0 && ((ph + lw - 1u) & (SW - 1)) != SW - 1) {
+                    const uint32_t e = lw - 1u + (SW - 1 - ((ph + lw - 1u) & (SW - 1)));
+                    const uint32_t c0 = e + 1u >= SW ? e + 1u - SW : 0u;  // the chunk's first slot word
+                    flush(e, c0, lw - 1u);
+                }
                 finish(ST_OK);
             } else {
                 k += 2;
