@@ -51,7 +51,13 @@ static void sink_put(sink_t* s, uint8_t b) {
     s->len++;
 }
 
+/* appendSlice: one copy when the slice fits the capacity (literal runs, mixed words' bytes) */
 static void sink_put_n(sink_t* s, const uint8_t* p, size_t n) {
+    if (s->out && s->len + n <= s->cap) {
+        memcpy(s->out + s->len, p, n);
+        s->len += n;
+        return;
+    }
     for (size_t i = 0; i < n; ++i) sink_put(s, p[i]);
 }
 
