@@ -3840,6 +3840,11 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
 // lanes per chunk (16 chunks of 64 contiguous bytes per store instruction). A unit's partial
 // first and last chunks, and chunks a zero run completes, are stored by their lane.
 constexpr uint32_t kSdRing = 80;  // LDS bytes per lane: the 64-B ring + 16 B (fewer bank conflicts)
+#ifndef CPK_SD_CHUNK
+#define CPK_SD_CHUNK 8
+#endif
+constexpr uint32_t kSdChunk = CPK_SD_CHUNK;         // output words per staged chunk (64 B)
+constexpr uint32_t kSdGroup = 2 * kWave / kSdChunk; // chunks per cooperative store instruction
 __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
                                                                 const uint64_t* __restrict__ in_len, uint32_t n,
@@ -3852,10 +3857,10 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kSmBlock * kSdRing];
     // each lane's output words by absolutely aligned 8-word (64-B) chunks; a full chunk is
     // stored by a quad of the wave (4 x 16 B), 16 chunks per store instruction
-    __shared__ __attribute__((aligned(16))) uint64_t ostage_all[kSmBlock * 8];
-    __shared__ __attribute__((aligned(16))) uint64_t ctab_all[(kSmBlock / kWave) * 16 * 2];
-    uint64_t* const ostage = ostage_all + threadIdx.x * 8;
-    uint64_t* const ctab = ctab_all + (threadIdx.x >> 6) * 32;
+    __shared__ __attribute__((aligned(16))) uint64_t ostage_all[kSmBlock * kSdChunk];
+    __shared__ __attribute__((aligned(16))) uint64_t ctab_all[(kSmBlock / kWave) * kSdGroup * 2];
+    uint64_t* const ostage = ostage_all + threadIdx.x * kSdChunk;
+    uint64_t* const ctab = ctab_all + (threadIdx.x >> 6) * (2 * kSdGroup);
     const uint32_t wbase_t = threadIdx.x & ~(kWave - 1);
     lut[threadIdx.x] = expand_selector(threadIdx.x);
     __syncthreads();
@@ -3878,7 +3883,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
     uint32_t capw = 0, wo = 0;
     uint64_t cap = 0;
 
-    constexpr uint32_t SW = 8;
+    constexpr uint32_t SW = kSdChunk;
     uint32_t ph = 0;      // the slot's first word's position in its aligned chunk
     bool rdy = false;     // a full chunk waits for the wave's flush
     uint64_t* rdst = nullptr;
@@ -4032,19 +4037,20 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
                 const uint32_t nr = (uint32_t)__popcll(rm);
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u));
-                for (uint32_t g = 0; g < nr; g += 16) {
+                for (uint32_t g = 0; g < nr; g += kSdGroup) {
                     wave_lds_sync();
-                    if (rdy && rank >= g && rank < g + 16) {
+                    if (rdy && rank >= g && rank < g + kSdGroup) {
                         ctab[2 * (rank - g)] = reinterpret_cast<uint64_t>(rdst);
                         ctab[2 * (rank - g) + 1] = lane;
                     }
                     wave_lds_sync();
-                    const uint32_t qd = lane >> 2;
+                    const uint32_t qd = lane / (kSdChunk / 2);  // the chunk this lane stores 16 B of
+                    const uint32_t qi = lane % (kSdChunk / 2);
                     if (g + qd < nr) {
                         uint64_t* const cd = reinterpret_cast<uint64_t*>(ctab[2 * qd]);
                         const uint32_t sl = (uint32_t)ctab[2 * qd + 1];
-                        const u32x4 v = *reinterpret_cast<const u32x4*>(ostage_all + (wbase_t + sl) * 8 + 2 * (lane & 3));
-                        *reinterpret_cast<u32x4*>(cd + 2 * (lane & 3)) = v;
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(ostage_all + (wbase_t + sl) * kSdChunk + 2 * qi);
+                        *reinterpret_cast<u32x4*>(cd + 2 * qi) = v;
                     }
                 }
                 rdy = false;
