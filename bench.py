@@ -216,7 +216,8 @@ def cpu_baseline(args, budget_s):
             "sample": f"pack+unpack of units x {args.unit_bytes} B (same generator/seed/density as the GPU) via "
                       f"oracle/packed_oracle.c: all-core {reps_a} x 32768 units in {t_a:.1f} s ({cores} threads), "
                       f"1-core {reps_1} x 2048 units in {t_1:.1f} s",
-            "note": "checker restatement (byte-at-a-time output), not an optimised codec: a lower bound on a "
+            "note": "checker restatement (scalar, record by record as message.zig; slices appended with one copy), "
+                    "not an optimised codec: a lower bound on a "
                     "ReleaseFast Zig build's rate"}
 
 
