@@ -4360,7 +4360,14 @@ struct VdDeep {
 };
 
 template <bool DEEP>
-__global__ __launch_bounds__(kWave) void validate_kernel(const uint8_t* __restrict__ in,
+// Occupancy: the compiler's choice (129 VGPRs) gives 3 waves/SIMD; pinned at 4 (127 VGPRs, 4
+// spilled) the trees leg runs 1.87 instead of 1.95-1.96 ms; at 5 (78 spilled) 3.42 ms (same box,
+// scripts/dev/vd_ab.sh; CPK_VD_WAVES overrides for A/B).
+#ifndef CPK_VD_WAVES
+#define CPK_VD_WAVES 4
+#endif
+#define CPK_VD_ATTR __attribute__((amdgpu_waves_per_eu(CPK_VD_WAVES, CPK_VD_WAVES)))
+__global__ __launch_bounds__(kWave) CPK_VD_ATTR void validate_kernel(const uint8_t* __restrict__ in,
                                                          const uint64_t* __restrict__ in_off,
                                                          const uint64_t* __restrict__ in_len, uint32_t n,
                                                          uint32_t per_wave, uint64_t seg_limit, uint64_t trav_limit,
