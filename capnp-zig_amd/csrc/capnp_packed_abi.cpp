@@ -124,22 +124,31 @@ struct HostCtx {
 
 HostCtx g_ctx;
 
-// Device buffers of capnp_packed_frame_connections (grow-only; its own stream and lock,
-// so framing never waits on a single-buffer call).
+// Device buffers of capnp_packed_frame_connections (grow-only; its own streams and lock,
+// so framing never waits on a single-buffer call). Frame slots are double-buffered: round r
+// decodes into d_out[r % 2] while the copy stream moves round r - 1's frames to the host.
 struct FrameCtx {
     std::mutex mu;
     hipStream_t stream = nullptr;
+    hipStream_t copy = nullptr;   // frames D2H, overlapping the next round
+    hipEvent_t ev_done[2] = {nullptr, nullptr};  // round into d_out[b] decoded
+    hipEvent_t ev_copied[2] = {nullptr, nullptr};  // frames of d_out[b] on the host
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
-    uint8_t* d_out = nullptr;
-    size_t out_cap = 0;
+    uint8_t* d_out[2] = {nullptr, nullptr};
+    size_t out_cap[2] = {0, 0};
     uint8_t* d_meta = nullptr;
     size_t meta_cap = 0;
 
     int init() {
         if (stream) return CAPNP_PACKED_OK;
         hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-        return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "hipStreamCreate");
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&copy, hipStreamNonBlocking);
+        for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+            e = hipEventCreateWithFlags(&ev_done[b], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_copied[b], hipEventDisableTiming);
+        }
+        return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "hipStreamCreate(framer)");
     }
     int reserve(uint8_t** p, size_t* cap, size_t need) {
         if (need <= *cap && *p) return CAPNP_PACKED_OK;
@@ -518,6 +527,11 @@ int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const u
     if (st) return st;
     std::lock_guard<std::mutex> lock(g_fr.mu);
     if ((st = g_fr.init())) return st;
+    // no copy of an earlier call may still write into its caller's frames buffer: each call
+    // ends with the copy stream drained (copies_done below), also on its error paths
+    struct CopiesDone {
+        ~CopiesDone() { (void)hipStreamSynchronize(g_fr.copy); }
+    } copies_done;
     if ((st = g_fr.reserve(&g_fr.d_in, &g_fr.in_cap, in_bytes + 16))) return st;
     if ((st = g_fr.reserve(&g_fr.d_meta, &g_fr.meta_cap, (size_t)n * 7 * sizeof(uint64_t)))) return st;
     const hipStream_t s = g_fr.stream;
@@ -533,7 +547,8 @@ int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const u
     }
     uint64_t fcur = 0;  // bytes of `frames` used by earlier rounds
     uint32_t nf = 0;
-    for (;;) {
+    for (uint32_t r = 0;; ++r) {
+        const uint32_t b = r & 1;  // this round's frame slots: d_out[b]
         // one round: the next message of every connection that may still hold one
         uint32_t k = 0;
         for (uint32_t c = 0; c < n; ++c)
@@ -552,13 +567,17 @@ int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const u
             h_out_off[j] = slots;
             slots += h_out_cap[j];
         }
-        if ((st = g_fr.reserve(&g_fr.d_out, &g_fr.out_cap, slots + 16))) return st;
+        // round r - 2's frames left d_out[b] before it is reused (or reallocated)
+        e = hipEventSynchronize(g_fr.ev_copied[b]);
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(frames copy)");
+        if ((st = g_fr.reserve(&g_fr.d_out[b], &g_fr.out_cap[b], slots + 16))) return st;
         uint64_t* const dm = reinterpret_cast<uint64_t*>(g_fr.d_meta);
         e = hipMemcpyAsync(dm, h_in_off, 4ull * k * sizeof(uint64_t), hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(H2D round)");
         int32_t* const d_st = reinterpret_cast<int32_t*>(dm + 6ull * k);
-        e = cpk::launch_read_message(g_fr.d_in, dm, dm + k, k, g_fr.d_out, dm + 2ull * k, dm + 3ull * k, dm + 4ull * k,
-                                     dm + 5ull * k, d_st, s);
+        e = cpk::launch_read_message(g_fr.d_in, dm, dm + k, k, g_fr.d_out[b], dm + 2ull * k, dm + 3ull * k,
+                                     dm + 4ull * k, dm + 5ull * k, d_st, s);
+        if (e == hipSuccess) e = hipEventRecord(g_fr.ev_done[b], s);
         if (e != hipSuccess) return hip_fail(e, "read-message launch");
         uint64_t* const h_len = h_in_off + 4 * k;
         uint64_t* const h_cons = h_in_off + 5 * k;
@@ -578,8 +597,11 @@ int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const u
         if (good) {
             if (fcur > frames_cap || span > frames_cap - fcur || good > max_frames - nf)
                 return fail(CAPNP_PACKED_OUT_OF_SPACE, "frames buffer or frame table too small");
-            e = hipMemcpy(frames + fcur, g_fr.d_out, span, hipMemcpyDeviceToHost);
-            if (e != hipSuccess) return hip_fail(e, "hipMemcpy(D2H frames)");
+            // on the copy stream, while the next round decodes into the other buffer
+            e = hipStreamWaitEvent(g_fr.copy, g_fr.ev_done[b], 0);
+            if (e == hipSuccess) e = hipMemcpyAsync(frames + fcur, g_fr.d_out[b], span, hipMemcpyDeviceToHost, g_fr.copy);
+            if (e == hipSuccess) e = hipEventRecord(g_fr.ev_copied[b], g_fr.copy);
+            if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H frames)");
         }
         for (uint32_t j = 0; j < k; ++j) {
             const uint32_t c = idx[j];
