@@ -2033,143 +2033,6 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
     status[unit] = (!SIZE_ONLY && 8 * words > cap) ? ST_SPACE : ST_OK;
 }
 
-// Dev experiment (CPK_SIZE2=1|2): the size-only walk of decode_index_kernel<true> with C
-// independent units per lane (C x 64 units per wave), to measure whether the walk is bound
-// by each lane's dependent record chain (C = 2 interleaves two chains per instruction).
-template <int C>
-__global__ __launch_bounds__(kWave) void size_walk_kernel(const uint8_t* __restrict__ in,
-                                                          const uint64_t* __restrict__ in_off,
-                                                          const uint64_t* __restrict__ in_len, uint32_t n,
-                                                          uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                                          const uint32_t* __restrict__ list,
-                                                          const uint32_t* __restrict__ list_count) {
-    constexpr uint32_t kRing = 80;
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[C * kWave * kRing];
-    const uint32_t lane = lane_id();
-    const uint32_t count = list ? *list_count : n;
-    const uint32_t base = blockIdx.x * kWave * C;
-    if (base >= count) return;
-    uint32_t unit[C], end[C], pos[C], words[C], st[C];
-    bool valid[C];
-    const uint8_t* src[C];
-    uint32_t maxr = 0;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const uint32_t slot = base + c * kWave + lane;
-        valid[c] = slot < count;
-        unit[c] = valid[c] ? ((list && count != n) ? list[slot] : slot) : 0u;
-        src[c] = cpk_dummy16;
-        uint64_t P = 0;
-        if (valid[c]) {
-            src[c] = in + in_off[unit[c]];
-            P = in_len[unit[c]];
-        }
-        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src[c]) & 15);
-        const bool take = valid[c] && P > 0 && P < kIxSizeMax;
-        end[c] = take ? s + (uint32_t)P : 0u;
-        pos[c] = take ? s : kIxDead;
-        words[c] = 0;
-        st[c] = ST_OK;
-        maxr = max(maxr, (end[c] + 63) >> 6);
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
-    maxr = __builtin_amdgcn_readfirstlane(maxr);
-    const uint32_t qp = lane & 3;
-    struct Ch {
-        const uint4 *q0, *q1, *q2, *q3;
-        uint32_t l0, l1, l2, l3;
-        uint4 d0, d1, d2, d3;
-    } ch[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src[c]) & 15);
-        const uint32_t np = (end[c] + 15) >> 4;
-        const uint64_t sb = reinterpret_cast<uint64_t>(src[c] - s);
-#define CPK_SW_Q(M, Q, LL)                                                                            \
-        {                                                                                          \
-            const uint32_t r = 16 * (M) + lane / 4;                                                \
-            const uint64_t rb = __shfl(sb, r, kWave);                                              \
-            const uint32_t rn = __shfl(np, r, kWave);                                              \
-            ch[c].Q = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16); \
-            ch[c].LL = rn ? rn - 1 : 0u;                                                           \
-        }
-        CPK_SW_Q(0, q0, l0) CPK_SW_Q(1, q1, l1) CPK_SW_Q(2, q2, l2) CPK_SW_Q(3, q3, l3)
-#undef CPK_SW_Q
-    }
-#define CPK_SW_LOAD(K)                                                       \
-    _Pragma("unroll") for (int c = 0; c < C; ++c) {                          \
-        ch[c].d0 = ch[c].q0[min(4 * (K) + qp, ch[c].l0)];                    \
-        ch[c].d1 = ch[c].q1[min(4 * (K) + qp, ch[c].l1)];                    \
-        ch[c].d2 = ch[c].q2[min(4 * (K) + qp, ch[c].l2)];                    \
-        ch[c].d3 = ch[c].q3[min(4 * (K) + qp, ch[c].l3)];                    \
-    }
-    if (maxr > 0) { CPK_SW_LOAD(0u) }
-    for (uint32_t k = 0; k <= maxr; ++k) {
-        if (k < maxr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (k > 0) {
-            wave_lds_sync();
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                uint8_t* const ring = ring_all + (c * kWave + lane) * kRing;
-                *reinterpret_cast<uint4*>(ring) = *reinterpret_cast<const uint4*>(ring + 64);
-            }
-            wave_lds_sync();
-        }
-        if (k < maxr) {
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                uint8_t* const wq = ring_all + (c * kWave + lane / 4) * kRing + 16 + 16 * qp;
-                *reinterpret_cast<uint4*>(wq) = ch[c].d0;
-                *reinterpret_cast<uint4*>(wq + 16 * kRing) = ch[c].d1;
-                *reinterpret_cast<uint4*>(wq + 32 * kRing) = ch[c].d2;
-                *reinterpret_cast<uint4*>(wq + 48 * kRing) = ch[c].d3;
-            }
-            if (k + 1 < maxr) { CPK_SW_LOAD(k + 1) }
-            wave_lds_sync();
-        }
-        const uint32_t ob = 64 * k;
-        uint32_t lim[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) lim[c] = min(ob + 48, end[c]);
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (int c = 0; c < C; ++c) any |= pos[c] < lim[c];
-            if (__builtin_amdgcn_ballot_w64(any) == 0) break;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const bool act = pos[c] < lim[c];
-                const uint8_t* const a = ring_all + (c * kWave + lane) * kRing + ((pos[c] + 16u - ob) & 63u);
-                uint32_t t = a[0];
-                uint32_t b1 = a[1];
-                uint32_t c9 = a[9];
-                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                const bool z = t == 0u, f = t == 0xFFu;
-                const uint32_t len = 1u + __popc(t) + (uint32_t)(z | f) + (f ? 8u * c9 : 0u);
-                const bool eof = act && pos[c] + len > end[c];
-                const bool ok = act && !eof;
-                st[c] = eof ? ST_EOF : st[c];
-                words[c] += ok ? 1u + (z ? b1 : 0u) + (f ? c9 : 0u) : 0u;
-                pos[c] = eof ? kIxDead : (ok ? pos[c] + len : pos[c]);
-            }
-        }
-    }
-#undef CPK_SW_LOAD
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        if (!valid[c]) continue;
-        const uint64_t P = in_len[unit[c]];
-        if (P >= kIxSizeMax) {
-            status[unit[c]] = kStNeedFull;
-            continue;
-        }
-        out_len[unit[c]] = st[c] == ST_OK ? 8ull * words[c] : 0ull;
-        status[unit[c]] = st[c];
-    }
-}
-
 #ifdef CPK_FILL_PROF
 // Diagnostic build: cycles per fill-kernel phase, summed over waves (s_memtime).
 __device__ unsigned long long cpk_fill_prof[8];
@@ -5300,20 +5163,9 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
         window_resolve_kernel<<<res_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, nullptr, out_len, status, q);
         decode_index_kernel<true><<<ix_blocks, kWave, 0, ss>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
                                                                out_len, status, nullptr, q + serial_off(n), q + 5);
-        static const int size2 = [] {  // dev A/B knob (size_walk_kernel)
-            const char* e = getenv("CPK_SIZE2");
-            return e ? atoi(e) : 0;
-        }();
-        if (size2 == 1)
-            size_walk_kernel<1><<<ix_blocks, kWave, 0, stream>>>(in, in_off, in_len, n, out_len, status,
-                                                                  q + kQHead + 2ull * n, q + 4);
-        else if (size2 == 2)
-            size_walk_kernel<2><<<(n + 2 * kWave - 1) / (2 * kWave), kWave, 0, stream>>>(
-                in, in_off, in_len, n, out_len, status, q + kQHead + 2ull * n, q + 4);
-        else
-            decode_index_kernel<true><<<ix_blocks, kWave, 0, stream>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
-                                                                       out_len, status, nullptr, q + kQHead + 2ull * n,
-                                                                       q + 4);
+        decode_index_kernel<true><<<ix_blocks, kWave, 0, stream>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
+                                                                   out_len, status, nullptr, q + kQHead + 2ull * n,
+                                                                   q + 4);
         e = hipGetLastError();
         const hipError_t j = side.join();
         if (e == hipSuccess) e = j;
