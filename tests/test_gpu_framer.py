@@ -190,3 +190,60 @@ def test_frame_connections_slot_growth_and_small_buffers():
         assert got[c] == frames, f"connection {c}"
         assert int(cons[c]) == len(conns[c]) - len(rest)
         assert int(st[c]) == (cp.END_OF_STREAM if code in (cp.OK, cp.END_OF_STREAM) else code)
+
+
+def _frame_connections(streams, frames):
+    """capnp_packed_frame_connections through the C-ABI with the caller's `frames` buffer."""
+    import ctypes
+    k = len(streams)
+    lens = np.array([len(s) for s in streams], dtype=np.uint64)
+    base = np.zeros(k, dtype=np.uint64)
+    base[1:] = np.cumsum(lens)[:-1]
+    host = np.frombuffer(b"".join(streams) + b"\0", dtype=np.uint8).copy()
+    g = np.full(k, 64, dtype=np.uint64)  # small slot guesses: OUT_OF_SPACE rounds too
+    max_frames = int(lens.sum()) // 2 + k + 16
+    f_off = np.zeros(max_frames, dtype=np.uint64)
+    f_len = np.zeros(max_frames, dtype=np.uint64)
+    f_conn = np.zeros(max_frames, dtype=np.uint32)
+    cons = np.zeros(k, dtype=np.uint64)
+    st = np.zeros(k, dtype=np.int32)
+    nf = ctypes.c_uint32(0)
+    rc = cp.lib().capnp_packed_frame_connections(
+        host.ctypes.data, int(lens.sum()), base.ctypes.data, lens.ctypes.data, k, g.ctypes.data, frames.ctypes.data,
+        frames.size, f_off.ctypes.data, f_len.ctypes.data, f_conn.ctypes.data, max_frames, cons.ctypes.data,
+        st.ctypes.data, ctypes.byref(nf))
+    assert rc == cp.OK, cp.lib().capnp_packed_last_error()
+    n = nf.value
+    out = [[] for _ in range(k)]
+    for i in range(n):  # pop order within a connection is the table's order
+        o, ln, c = int(f_off[i]), int(f_len[i]), int(f_conn[i])
+        out[c].append(bytes(frames[o:o + ln]))
+    return out, cons.tolist(), st.tolist()
+
+
+def test_frame_connections_into_page_locked_frames():
+    """The frames of every round go D2H on a copy stream while the next round decodes (double-
+    buffered slots, capnp_packed_abi.cpp); into a page-locked buffer those copies are truly
+    asynchronous. The call must still return with every frame in place: same frames, consumed
+    counts and statuses as into a pageable buffer, and as the oracle reader."""
+    rng = np.random.default_rng(0xF7A3E)
+    streams, expect = [], []
+    for c in range(96):
+        msgs, packed = make_stream(rng, int(rng.integers(0, 12)))
+        data = b"".join(packed)
+        if c % 7 == 3 and len(data) > 4:
+            data = data[:-3]  # ends inside a message: EndOfStream, the tail stays buffered
+        streams.append(data)
+        expect.append(oracle_frames(data))
+    cap = 4 * sum(len(s) for s in streams) + (1 << 20)
+    pinned = torch.empty(cap, dtype=torch.uint8, pin_memory=True).numpy()
+    pinned[:] = 0xA5
+    pageable = np.full(cap, 0x5A, dtype=np.uint8)
+    got_pin = _frame_connections(streams, pinned)
+    got_page = _frame_connections(streams, pageable)
+    assert got_pin == got_page
+    frames, cons, sts = got_pin
+    for c, (ofr, rest, code) in enumerate(expect):
+        assert frames[c] == ofr, f"connection {c}"
+        assert cons[c] == len(streams[c]) - len(rest), f"connection {c}"
+        assert sts[c] == (cp.END_OF_STREAM if code in (cp.OK, cp.END_OF_STREAM) else code), f"connection {c}"
