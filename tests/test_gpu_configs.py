@@ -342,3 +342,26 @@ def test_message_init_batch_matches_message_init():
 
 def struct_u32(v):
     return int(v).to_bytes(4, "little")
+
+
+@pytest.mark.parametrize("env", [{"CPK_MID_STREAM": "1"}, {"CPK_MID_STREAM": "1", "CPK_SM_FRAC": "0.3"}])
+def test_c5_mid_units_on_second_stream(env):
+    """The opt-in second side stream for a decode batch's mid units (CPK_MID_STREAM=1,
+    read once per process): the C5 tests above, in a child process that
+    sets it, with the small decoder's grid at its default share and at 30%."""
+    import os
+    import subprocess
+    import sys
+    tests = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(tests)
+    code = ("import test_gpu_configs as t\n"
+            "for thr in (26, 128, 230): t.test_c5_skewed_sizes_every_unit(thr, 'twopass')\n"
+            "t.test_c5_full_size_1M_units('twopass')\n"
+            "import capnp_packed as cp\n"
+            "with cp.decoder('fused'): t.test_c5_skewed_sizes_every_unit(128, 'fused')\n"
+            "print('child ok')\n")
+    path = os.pathsep.join([os.path.join(repo, "capnp-zig_amd"), tests, repo])
+    run_env = dict(os.environ, PYTHONPATH=path, **env)
+    out = subprocess.run([sys.executable, "-c", code], env=run_env, cwd=repo, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0 and "child ok" in out.stdout, out.stderr[-3000:]
