@@ -1778,13 +1778,21 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 // A unit's status on entry says which pass owns it, so no pass redoes another's work.
 constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2, kRdOne = 3;
 
+#ifndef CPK_IX_BW  // waves per block of the index pass (dev A/B; each wave owns 64 units)
+#define CPK_IX_BW 1
+#endif
+constexpr uint32_t kIxBw = CPK_IX_BW;
+// blocks of the index pass for a batch of n units
+__host__ __device__ constexpr uint32_t ix_blocks_for(uint32_t n) {
+    return (uint32_t)((((uint64_t)n + kWave - 1) / kWave + kIxBw - 1) / kIxBw);
+}
 #ifdef CPK_IX_WAVES  // dev A/B: pin the index pass's occupancy (waves per SIMD)
 #define CPK_IX_ATTR __attribute__((amdgpu_waves_per_eu(CPK_IX_WAVES, CPK_IX_WAVES)))
 #else
 #define CPK_IX_ATTR
 #endif
 template <bool SIZE_ONLY, int RD = kRdNone>
-__global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
+__global__ __launch_bounds__(kWave * kIxBw) CPK_IX_ATTR void decode_index_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
@@ -1795,12 +1803,14 @@ __global__ __launch_bounds__(kWave) CPK_IX_ATTR void decode_index_kernel(
     static_assert(RD != kRdOne || !SIZE_ONLY, "the one-pass read writes records");
     constexpr bool kStop = RD == kRdWalk || RD == kRdOne;  // the walk stops at the framed length
     constexpr uint32_t kRing = 80;  // [0, 16): block k-1's last piece, [16, 80): block k
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[kWave * kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kIxBw * kWave * kRing];
+    uint8_t* const ring_all = ring_blk + (threadIdx.x >> 6) * (kWave * kRing);  // this wave's
+    const uint32_t wv = blockIdx.x * kIxBw + (threadIdx.x >> 6);
     const uint32_t lane = lane_id();
     // with a class list (launch_decode: the mid units), lane l takes list entry 64b + l
     const uint32_t count = list ? *list_count : n;
-    if (blockIdx.x * kWave >= count) return;  // wave-uniform
-    const uint32_t slot = blockIdx.x * kWave + lane;
+    if (wv * kWave >= count) return;  // wave-uniform
+    const uint32_t slot = wv * kWave + lane;
     const bool valid = slot < count;
     const uint32_t unit = valid ? ((list && count != n) ? list[slot] : slot) : 0u;
 
@@ -5224,7 +5234,7 @@ template <bool SIZE_ONLY>
 static void launch_index(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n, uint8_t* out,
                          const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
                          hipStream_t stream) {
-    decode_index_kernel<SIZE_ONLY><<<(n + kWave - 1) / kWave, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+    decode_index_kernel<SIZE_ONLY><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                                    out_cap, out_len, status, nullptr);
 }
 
@@ -5285,13 +5295,12 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
         const uint32_t win_blocks = (uint32_t)std::min<uint64_t>((wcap + kWvWaves - 1) / kWvWaves, spec_res);
         const uint32_t res_blocks = std::min((n + kWvWaves - 1) / kWvWaves, res_res);
         const hipStream_t ss = side.stream();
-        const uint32_t ix_blocks = (n + kWave - 1) / kWave;
         long_windows_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
         window_spec_kernel<<<win_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, q);
         window_resolve_kernel<<<res_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, nullptr, out_len, status, q);
-        decode_index_kernel<true><<<ix_blocks, kWave, 0, ss>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
+        decode_index_kernel<true><<<ix_blocks_for(n), kWave * kIxBw, 0, ss>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
                                                                out_len, status, nullptr, q + serial_off(n), q + 5);
-        decode_index_kernel<true><<<ix_blocks, kWave, 0, stream>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
+        decode_index_kernel<true><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, in_len, n, nullptr, nullptr, nullptr,
                                                                    out_len, status, nullptr, q + kQHead + 2ull * n,
                                                                    q + 4);
         e = hipGetLastError();
@@ -5358,7 +5367,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                         out_len, status, mid, q + 4);
     } else {
         uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
-        decode_index_kernel<false><<<(n + kWave - 1) / kWave, kWave, 0, ms>>>(
+        decode_index_kernel<false><<<ix_blocks_for(n), kWave * kIxBw, 0, ms>>>(
             in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4, rec);
         decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off,
                                                                            out_len, out_cap, status, mid, q + 4, rec);
@@ -5413,17 +5422,16 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                                uint64_t* consumed, int32_t* status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    const uint32_t wv = (n + kWave - 1) / kWave;
     read_header_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
                                                                          status);
     // one walk for the units the fill pass can take: records and the stop at the framed length
-    decode_index_kernel<false, kRdOne><<<wv, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+    decode_index_kernel<false, kRdOne><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                   out_len, status, consumed);
     // the rest (kStNeedWalk): the walk to the framed length, then the gated write pass
-    decode_index_kernel<true, kRdWalk><<<wv, kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+    decode_index_kernel<true, kRdWalk><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                   out_len, status, consumed);
     // the message's own bytes from here on: in_len = consumed
-    decode_index_kernel<false, kRdGate><<<wv, kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off, out_cap,
+    decode_index_kernel<false, kRdGate><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, consumed, n, out, out_off, out_cap,
                                                                    out_len, status, nullptr);
     decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, consumed, n, out, out_off,
                                                                        out_len, out_cap, status);
