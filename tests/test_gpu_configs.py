@@ -344,11 +344,13 @@ def struct_u32(v):
     return int(v).to_bytes(4, "little")
 
 
-@pytest.mark.parametrize("env", [{"CPK_MID_STREAM": "1"}, {"CPK_MID_STREAM": "1", "CPK_SM_FRAC": "0.3"}])
-def test_c5_mid_units_on_second_stream(env):
-    """The opt-in second side stream for a decode batch's mid units (CPK_MID_STREAM=1,
-    read once per process): the C5 tests above, in a child process that
-    sets it, with the small decoder's grid at its default share and at 30%."""
+@pytest.mark.parametrize("env", [{"CPK_MID_STREAM": "1"}, {"CPK_MID_STREAM": "1", "CPK_SM_FRAC": "0.3"},
+                                 {"CPK_SIDE_STREAM": "0"}])
+def test_c5_stream_knobs(env):
+    """The launch knobs read once per process: the opt-in second side
+    stream for a decode batch's mid units (CPK_MID_STREAM=1), with the small decoder's grid
+    at its default share and at 30%, and the long units after the main grid instead of on
+    the side stream (CPK_SIDE_STREAM=0). The C5 tests above, in a child process that sets them."""
     import os
     import subprocess
     import sys
