@@ -207,10 +207,14 @@ SIGNATURES = {
                                                       ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_set_decoder": (ctypes.c_int, [ctypes.c_int]),
     "capnp_packed_set_all_or_nothing": (ctypes.c_int, [ctypes.c_int]),
+    "capnp_packed_set_launch_flags": (ctypes.c_uint32, [ctypes.c_uint32]),
 }
 
 # capnp_packed_set_decoder values (include/capnp_packed.h)
-DECODERS = {"auto": 0, "twopass": 1, "fused": 2}
+DECODERS = {"auto": 0, "twopass": 1, "fused": 2, "stream": 3}
+# capnp_packed_set_launch_flags bits (include/capnp_packed.h)
+LAUNCH_LONG_INLINE = 0x1
+LAUNCH_MID_SIDE_STREAM = 0x2
 
 
 def lib():
@@ -626,8 +630,8 @@ class PackedConnections:
 # ---------------------------------------------------------------------------
 
 def set_decoder(name: str) -> str:
-    """Select the mid-unit batch decoder ("auto", "twopass" or "fused"; every one is
-    bit-exact) for batches enqueued from now on; returns the previous setting's name."""
+    """Select the mid-unit batch decoder ("auto", "twopass", "fused" or "stream"; every one
+    is bit-exact) for batches enqueued from now on; returns the previous setting's name."""
     prev = lib().capnp_packed_set_decoder(DECODERS[name])
     if prev < 0 or prev not in DECODERS.values():
         _raise(prev, "set_decoder")
@@ -638,6 +642,27 @@ def set_all_or_nothing(on: bool) -> bool:
     """Small decode units all-or-nothing too (capnp_packed_set_all_or_nothing); returns the
     previous setting."""
     return bool(lib().capnp_packed_set_all_or_nothing(1 if on else 0))
+
+
+def set_launch_flags(flags: int) -> int:
+    """Launch policy bits (capnp_packed_set_launch_flags: LAUNCH_LONG_INLINE,
+    LAUNCH_MID_SIDE_STREAM); returns the previous flags. No result depends on them."""
+    return int(lib().capnp_packed_set_launch_flags(int(flags)))
+
+
+class launch_flags:
+    """Context manager: `with launch_flags(LAUNCH_LONG_INLINE): ...` restores the flags after."""
+
+    def __init__(self, flags: int):
+        self.flags, self.prev = flags, None
+
+    def __enter__(self):
+        self.prev = set_launch_flags(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        set_launch_flags(self.prev)
+        return False
 
 
 class decoder:

@@ -319,12 +319,16 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
 size_t capnp_packed_batch_workspace_bytes(uint32_t n) { return cpk::queue_bytes(n); }
 
 int capnp_packed_set_decoder(int decoder) {
-    if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_FUSED)
+    if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_STREAM)
         return fail(CAPNP_PACKED_INVALID_ARGUMENT, "unknown decoder");
     return cpk::set_decoder(decoder);
 }
 
 int capnp_packed_set_all_or_nothing(int on) { return cpk::set_all_or_nothing(on); }
+
+uint32_t capnp_packed_set_launch_flags(uint32_t flags) {
+    return cpk::set_launch_flags(flags & (CAPNP_PACKED_LAUNCH_LONG_INLINE | CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM));
+}
 
 int capnp_packed_stream_release(void* stream) {
     int st = ensure_device();

@@ -23,6 +23,7 @@ size_t queue_bytes(uint32_t n);
 // capnp_packed_set_decoder: returns the previous setting
 int set_decoder(int decoder);
 int set_all_or_nothing(int on);
+uint32_t set_launch_flags(uint32_t flags);
 hipError_t release_stream(hipStream_t stream);
 void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept);
 

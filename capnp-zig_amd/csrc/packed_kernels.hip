@@ -2359,6 +2359,264 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 }
 
 // ---------------------------------------------------------------------------
+// DECODE, streaming single pass (round 4; DESIGN.md §2.3b, the default for mid units).
+// The packed bytes cross HBM once and no piece records exist. The record chain is walked
+// where it is cheapest, lane per unit (64 units per wave, one record per instruction), and
+// the output is written where stores coalesce, many lanes per unit:
+//   ring   decode_index_kernel's load scheme: round k's 64-B blocks of the wave's 64 units
+//          come in by quad-coalesced 16-B loads issued one round ahead, land in the units'
+//          80-B LDS rings (block k-1's last piece, block k), and the walk takes the records
+//          whose first byte is in [64k - 16, 64k + 48) (all their bytes are resident);
+//   walk   every step, every active lane emits exactly one output word: a record (the tag's
+//          word; for 00 its first zero word, for FF its first literal word), one word of an
+//          FF run's literal body (8 bytes at pos), or one more word of a zero run. The step
+//          writes a u16 entry (tag << 8 | ring offset of the word's packed bytes) to row i of
+//          the wave's list; lanes keep their own state (next position, literal-body end,
+//          zero words left), so a run that crosses a round just continues. Zero runs of 16
+//          or more extra words are filled by the whole wave instead (one job per lane per
+//          sub-round), and words past a unit's capacity are counted, not emitted;
+//   store  after at most kDsK steps (a sub-round) the wave writes the listed words: G lanes
+//          per unit (G = 4, 8 or 16 by the longest list), lane (u, i) expands unit u's
+//          entry i from the unit's ring (v_alignbyte + v_perm with the tag's selector) and
+//          stores word W_u + i, so a store instruction writes 64/G runs of G words;
+// Errors follow message.zig:88-191 (UnexpectedEof for a record that runs past the input,
+// OutOfSpace with the required size), found at the walk's end: a failed unit may hold a
+// prefix of its output in its slot (never a byte past out_cap). Callers that need the slot
+// untouched select the two-pass decoder (capnp_packed_set_all_or_nothing).
+constexpr uint32_t kDsWaves = 4;       // waves per block (one 1-KB selector table per block)
+constexpr uint32_t kDsK = 16;          // walk steps per sub-round = list rows
+constexpr uint32_t kDsRowE = 66;       // list row stride in u16 entries (132 B: conflict-free rows)
+constexpr uint32_t kDsRing = 80;       // ring bytes per unit
+constexpr uint32_t kDsZJob = 16;       // zero runs with this many extra words or more: a wave fill
+constexpr uint32_t kDsDead = 0xFFFFFFF0u;  // walk position of a lane with nothing (more) to walk
+constexpr uint32_t kDsWave = kWave * kDsRing + kDsK * kDsRowE * 2 + kWave * 8;  // LDS bytes per wave
+
+// Expand selectors packed 4 bits per byte: byte k = sel[k] | sel[k + 4] << 4 (sel values are
+// 0..7 or 0x0C), so the table is 1 KB.
+struct SelLut32 {
+    uint32_t v[256];
+};
+constexpr SelLut32 make_sel_lut32() {
+    SelLut32 l{};
+    for (uint32_t t = 0; t < 256; ++t) {
+        const uint64_t s = kExpandLut.v[t];
+        uint32_t x = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+            x |= (uint32_t)(((s >> (8 * k)) & 0xFu) | (((s >> (8 * (k + 4))) & 0xFu) << 4)) << (8 * k);
+        l.v[t] = x;
+    }
+    return l;
+}
+__device__ constexpr SelLut32 kExpandLut32 = make_sel_lut32();
+
+// s_waitcnt needs an immediate: wait until at most min(c, 63) vector-memory operations are
+// outstanding (fewer than the true number of younger operations only waits longer).
+__device__ __forceinline__ void vmcnt_at_most63(uint32_t c) {
+#define CPK_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define CPK_VM8(B) CPK_VM(B) CPK_VM(B + 1) CPK_VM(B + 2) CPK_VM(B + 3) CPK_VM(B + 4) CPK_VM(B + 5) CPK_VM(B + 6) CPK_VM(B + 7)
+    switch (c < 63u ? c : 63u) {
+        CPK_VM8(0) CPK_VM8(8) CPK_VM8(16) CPK_VM8(24) CPK_VM8(32) CPK_VM8(40) CPK_VM8(48)
+        CPK_VM(56) CPK_VM(57) CPK_VM(58) CPK_VM(59) CPK_VM(60) CPK_VM(61) CPK_VM(62)
+        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    }
+#undef CPK_VM8
+#undef CPK_VM
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return __builtin_amdgcn_readlane(wave_incl_max(v, 0), kWave - 1);
+}
+
+__global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
+    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
+    __shared__ uint32_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t lds_all[kDsWaves * kDsWave];
+    lut[threadIdx.x] = kExpandLut32.v[threadIdx.x];  // 256 threads
+    __syncthreads();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const ring_all = lds_all + wave * kDsWave;                              // 64 x 80 B
+    uint16_t* const lst = reinterpret_cast<uint16_t*>(ring_all + kWave * kDsRing);  // kDsK rows
+    uint64_t* const meta = reinterpret_cast<uint64_t*>(ring_all + kWave * kDsRing + kDsK * kDsRowE * 2);
+    const uint32_t wv = blockIdx.x * kDsWaves + wave;
+    const uint32_t lane = lane_id();
+    const uint32_t count = list ? *list_count : n;
+    if (wv * kWave >= count) return;  // wave-uniform
+    const uint32_t slot = wv * kWave + lane;
+    const bool valid = slot < count;
+    const uint32_t unit = valid ? ((list && count != n) ? list[slot] : slot) : 0u;
+
+    // ---- per-lane unit ---------------------------------------------------------------
+    const uint8_t* src = cpk_dummy16;
+    uint64_t P64 = 0, cap = 0;
+    uint8_t* dstb = nullptr;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P64 = in_len[unit];
+        dstb = out + out_off[unit];
+        cap = out_cap[unit];
+        if (P64 > 0 && (reinterpret_cast<uintptr_t>(dstb) & 7)) st = ST_ARG;  // an empty unit writes nothing
+    }
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    // mid units: at most kFlPieces pieces (class_scatter); the bound keeps positions in u32
+    const bool take = valid && st == ST_OK && P64 > 0 && P64 <= (1u << 24);
+    if (valid && st == ST_OK && P64 > (1u << 24)) st = ST_ARG;  // unreachable for the mid class
+    const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
+    const uint32_t npieces = (end + 15) >> 4;
+    const uint32_t maxr = __builtin_amdgcn_readfirstlane(wave_max_u32((end + 63) >> 6));
+    const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0xFFFFFFF0u);  // words the slot holds
+
+    // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block ------------
+    const uint4* qsrc[4];
+    uint32_t qlast[4];
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m) {
+        const uint32_t r = 16 * m + lane / 4;
+        const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
+        const uint32_t rn = __shfl(npieces, r, kWave);
+        qsrc[m] = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16);
+        qlast[m] = rn ? rn - 1 : 0u;
+    }
+    const uint32_t qp = lane & 3;
+    uint4 d0, d1, d2, d3;
+    auto load = [&](uint32_t k) {
+        d0 = load_nt(qsrc[0] + min(4 * k + qp, qlast[0]));
+        d1 = load_nt(qsrc[1] + min(4 * k + qp, qlast[1]));
+        d2 = load_nt(qsrc[2] + min(4 * k + qp, qlast[2]));
+        d3 = load_nt(qsrc[3] + min(4 * k + qp, qlast[3]));
+    };
+    uint8_t* const wq = ring_all + (lane / 4) * kDsRing + 16 + 16 * qp;  // unit 16m + l/4: + 16 * kDsRing * m
+    uint8_t* const ring = ring_all + lane * kDsRing;
+
+    uint32_t pos = take ? s : kDsDead;  // next record / literal word (aligned space)
+    uint32_t lit_end = 0;               // end of the FF literal body pos is in (pos < lit_end)
+    uint32_t zrem = 0;                  // zero words of the current run still to emit
+    uint32_t wc = 0;                    // words of the unit so far (emitted, counted past capw)
+    uint32_t younger = 0;               // vector-memory ops issued after the round's loads
+    if (maxr > 0) load(0);
+    for (uint32_t k = 0; k <= maxr; ++k) {
+        if (k < maxr) vmcnt_at_most63(younger);  // round k's loads have landed
+        younger = 0;
+        if (k > 0) {
+            wave_lds_sync();  // every lane is done with round k-1's ring reads
+            *reinterpret_cast<uint4*>(ring) = *reinterpret_cast<const uint4*>(ring + 64);
+            wave_lds_sync();
+        }
+        if (k < maxr) {
+            *reinterpret_cast<uint4*>(wq) = d0;
+            *reinterpret_cast<uint4*>(wq + 16 * kDsRing) = d1;
+            *reinterpret_cast<uint4*>(wq + 32 * kDsRing) = d2;
+            *reinterpret_cast<uint4*>(wq + 48 * kDsRing) = d3;
+            if (k + 1 < maxr) load(k + 1);
+            wave_lds_sync();
+        }
+        const uint32_t ob = 64 * k;              // ring offset o = pos + 16 - ob in [0, 64)
+        const uint32_t lim = min(ob + 48, end);  // records / literal words starting before lim
+        for (;;) {  // sub-rounds
+            // ---- walk: up to kDsK steps, one output word per active lane per step ------
+            const uint32_t w0 = wc;  // the unit's word index of list row 0
+            uint32_t nent = 0;       // entries listed this sub-round
+            uint32_t zjob = 0;       // extra words of a zero run the wave fills after the stores
+#pragma unroll 1
+            for (uint32_t i = 0; i < kDsK; ++i) {
+                const bool inz = zrem != 0u;
+                const bool act = zjob == 0u && (inz || pos < lim);
+                if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                const uint32_t o = (pos + 16u - ob) & 63u;  // any pos reads inside the lane's ring
+                uint32_t t = ring[o];
+                uint32_t b1 = ring[o + 1];
+                uint32_t c9 = ring[o + 9];
+                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per step
+                const bool lit = !inz && pos < lit_end;          // a literal body word at pos
+                const bool rec = act && !inz && !lit;
+                const bool z = t == 0u, f = t == 0xFFu;
+                // message.zig:101-141: 00 c -> 1 + c zero words; FF w c -> w, then c literal
+                // words; other tags -> one word of popc(tag) packed bytes
+                const uint32_t len = lit ? 8u : 1u + __popc(t) + (uint32_t)(z | f);  // FF: 10, body apart
+                const uint32_t lend = pos + 10u + 8u * c9;  // end of an FF record's body
+                const bool eof = rec && (pos + len > end || (f && lend > end));  // :105-137
+                const uint32_t tg = inz ? 0u : lit ? 0xFFu : t;
+                const uint32_t dd = lit ? o : o + 1u;  // ring offset of the word's packed bytes
+                lst[i * kDsRowE + lane] = (uint16_t)((tg << 8) | dd);
+                const bool em = act && !eof;
+                const uint32_t wn = wc + (em ? 1u : 0u);
+                const bool zr = rec && !eof && z && b1 != 0u;  // a zero run with extra words
+                const bool bulk = zr && wn >= capw;             // past the slot: counted only
+                const bool job = zr && !bulk && b1 >= kDsZJob;
+                zrem = inz ? zrem - 1u : ((zr && !bulk && !job) ? b1 : 0u);
+                zjob = job ? b1 : 0u;
+                wc = wn + (bulk ? b1 : 0u);
+                lit_end = (rec && f) ? lend : lit_end;
+                pos = eof ? kDsDead : (inz ? pos : pos + len);
+                st = eof ? ST_EOF : st;
+                nent = em ? i + 1u : nent;
+            }
+            // ---- store the listed words: G lanes per unit ---------------------------------
+            const uint32_t lu = w0 < capw ? min(nent, capw - w0) : 0u;  // entries that fit the slot
+            meta[lane] = (reinterpret_cast<uint64_t>(dstb) + 8ull * w0) | ((uint64_t)lu << 56);
+            const uint32_t nmax = wave_max_u32(lu);
+            wave_lds_sync();
+            if (nmax > 0) {
+                const uint32_t lg = nmax > 8u ? 4u : nmax > 4u ? 3u : 2u;  // G = 1 << lg
+                const uint32_t ii = lane & ((1u << lg) - 1u);
+                const uint32_t per = kWave >> lg;  // units per store instruction
+                for (uint32_t u0 = 0; u0 < (uint32_t)kWave; u0 += per) {
+                    const uint32_t u = u0 + (lane >> lg);
+                    const uint64_t m = meta[u];
+                    const bool ok = ii < (uint32_t)(m >> 56);
+                    const uint32_t e = lst[ii * kDsRowE + u];
+                    const uint32_t dd = e & 0xFFu;
+                    const uint32_t* const rw = reinterpret_cast<const uint32_t*>(ring_all + u * kDsRing + (dd & ~3u));
+                    const uint32_t r0 = rw[0], r1 = rw[1], r2 = rw[2];
+                    const uint32_t x = lut[e >> 8];
+                    const uint32_t sh = dd & 3u;
+                    const uint32_t lo = __builtin_amdgcn_alignbyte(r1, r0, sh);
+                    const uint32_t hi = __builtin_amdgcn_alignbyte(r2, r1, sh);
+                    const uint32_t a = __builtin_amdgcn_perm(hi, lo, x & 0x0F0F0F0Fu);
+                    const uint32_t b = __builtin_amdgcn_perm(hi, lo, (x >> 4) & 0x0F0F0F0Fu);
+                    if (__builtin_amdgcn_ballot_w64(ok) != 0) {  // uniform: the store issues
+                        if (ok) {
+                            uint64_t* const p = reinterpret_cast<uint64_t*>((m & 0x00FFFFFFFFFFFFFFull) + 8ull * ii);
+                            __builtin_nontemporal_store((uint64_t)a | ((uint64_t)b << 32), p);
+                        }
+                        ++younger;
+                    }
+                }
+            }
+            // ---- zero runs the wave fills: words [wc, wc + c) of each lane with a job --------
+            uint64_t jobs = __builtin_amdgcn_ballot_w64(zjob != 0u);
+            while (jobs) {
+                const uint32_t jl = (uint32_t)__builtin_ctzll(jobs);
+                jobs &= jobs - 1;
+                const uint32_t jw = readlane(wc, jl), jc = readlane(zjob, jl), jcap = readlane(capw, jl);
+                const uint64_t jd = (uint64_t)readlane((uint32_t)reinterpret_cast<uint64_t>(dstb), jl) |
+                                    ((uint64_t)readlane((uint32_t)(reinterpret_cast<uint64_t>(dstb) >> 32), jl) << 32);
+                const uint32_t hi = min(jw + jc, jcap);  // jw < jcap (a job is never past the slot)
+                for (uint32_t w = jw + lane; w < hi; w += kWave)
+                    __builtin_nontemporal_store(0ull, reinterpret_cast<uint64_t*>(jd) + w);
+                younger += (hi - jw + kWave - 1) / kWave;
+            }
+            wc += zjob;
+            // ---- next sub-round, or the next round when every lane is past lim -------------
+            if (__builtin_amdgcn_ballot_w64(zrem != 0u || pos < lim) == 0) break;
+            wave_lds_sync();  // the store reads of the list and meta are done
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!valid) return;
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8ull * wc;
+    status[unit] = wc > capw ? ST_SPACE : ST_OK;
+}
+
+// ---------------------------------------------------------------------------
 // DECODE, fused single pass (round 3): the packed bytes cross HBM once
 // and no piece records exist. One wave per unit, persistent grid, the next unit's pieces
 // prefetched into registers while this one is decoded (as decode_fill_kernel).
@@ -4048,7 +4306,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
 //      wave write whole runs of each unit's slot.
 // A unit is written only when it decodes OK within its capacity: small units are
 // all-or-nothing too (message.zig:90 raises before any output), like mid and long units.
-// Opt-in (CPK_SMALL=group): measured slower than decode_small_kernel, because a group's
+// Opt-in (capnp_packed_set_all_or_nothing(1)): measured slower than decode_small_kernel, because a group's
 // decode phase waits for its longest unit (C5's sizes are heavy-tailed) while the lane
 // kernel refills each lane as its unit ends.
 constexpr uint32_t kSgWaves = 4;
@@ -4928,7 +5186,7 @@ struct StreamCtx {
     std::mutex mu;
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    hipStream_t s2 = nullptr;  // a second side stream (dev knob CPK_MID_STREAM: C5's mid units)
+    hipStream_t s2 = nullptr;  // a second side stream (CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM: C5's mid units)
     hipEvent_t join2 = nullptr;
     uint32_t* q = nullptr;  // class workspace (queue_bytes): kQHead counters, lists, tile / window table
     uint64_t qcap = 0;
@@ -4981,18 +5239,17 @@ static void launch_classes(const uint8_t* in, const uint64_t* in_off, const uint
     class_scatter_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q);
 }
 
-// Opt-in (CPK_MID_STREAM=1), decode: a batch's mid units (index + fill passes) on a second
-// side stream, launched before the small units' kernel, whose grid then takes 85% of its
-// resident size so the mid passes get CUs from the start. Same box, round 3:
-// C5 decode 0.678 -> 0.660 ms, but the headline (all mid units) 2.474 -> 2.499 ms from the
-// extra stream's fork and join, so it stays off by default.
-static bool mid_stream_knob() {
-    static const bool on = [] {
-        const char* e = getenv("CPK_MID_STREAM");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
+// Launch policy (capnp_packed_set_launch_flags, process-wide; no result depends on it):
+//   CAPNP_PACKED_LAUNCH_LONG_INLINE      the long-unit kernels run after the main grid on the
+//                                        caller's stream instead of on a side stream;
+//   CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM  decode: a batch's mid units on a second side stream,
+//                                        launched before the small units' kernel, whose grid then
+//                                        takes 85% of its resident size. Round 3:
+//                                        C5 decode 0.678 -> 0.660 ms, but the headline (all mid
+//                                        units) 2.474 -> 2.499 ms from the extra fork and join.
+static std::atomic<uint32_t> g_launch_flags{0};
+uint32_t set_launch_flags(uint32_t f) { return g_launch_flags.exchange(f); }
+static bool mid_side_stream() { return g_launch_flags.load(std::memory_order_relaxed) & CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM; }
 
 class SideLaunch {
   public:
@@ -5006,11 +5263,7 @@ class SideLaunch {
             ctx_ = c.get();
         }
         lock_ = std::unique_lock<std::mutex>(ctx_->mu);
-        static const bool concurrent = [] {  // CPK_SIDE_STREAM=0: long units after the main grid
-            const char* e = getenv("CPK_SIDE_STREAM");
-            return !(e && e[0] == '0');
-        }();
-        if (!concurrent) {
+        if (g_launch_flags.load(std::memory_order_relaxed) & CAPNP_PACKED_LAUNCH_LONG_INLINE) {
             side_ = main_;
             ok_ = true;
             return;
@@ -5245,33 +5498,19 @@ static uint32_t fallback_blocks(uint32_t n) {
     return full < 2048u ? full : 2048u;
 }
 
-// Mid-unit decoder (capnp_packed_set_decoder; CPK_DECODE=twopass|fused sets the start value).
-static std::atomic<int>& decoder_setting() {
-    static std::atomic<int> v([] {
-        const char* e = getenv("CPK_DECODE");
-        if (e && std::string(e) == "fused") return (int)CAPNP_PACKED_DECODER_FUSED;
-        if (e && std::string(e) == "twopass") return (int)CAPNP_PACKED_DECODER_TWO_PASS;
-        return (int)CAPNP_PACKED_DECODER_AUTO;
-    }());
-    return v;
-}
-// Small-unit decoder (capnp_packed_set_all_or_nothing; CPK_SMALL=group sets the start
-// value): 1 the lane-streaming kernel (default: a failed small unit may keep a prefix),
-// 0 the group-staged kernel (all-or-nothing for small units too, slower).
-static std::atomic<int>& small_setting() {
-    static std::atomic<int> v([] {
-        const char* e = getenv("CPK_SMALL");
-        return (e && std::string(e) == "group") ? 0 : 1;
-    }());
-    return v;
-}
-static int small_variant() { return small_setting().load(std::memory_order_relaxed); }
-int set_all_or_nothing(int on) { return small_setting().exchange(on ? 0 : 1) == 0 ? 1 : 0; }
+// Mid-unit decoder (capnp_packed_set_decoder).
+static std::atomic<int> g_decoder{CAPNP_PACKED_DECODER_AUTO};
+// Small-unit decoder (capnp_packed_set_all_or_nothing): 1 the lane-streaming kernel (default: a
+// failed small unit may keep a prefix), 0 the group-staged kernel (all-or-nothing for small units
+// too, slower).
+static std::atomic<int> g_small{1};
+static int small_variant() { return g_small.load(std::memory_order_relaxed); }
+int set_all_or_nothing(int on) { return g_small.exchange(on ? 0 : 1) == 0 ? 1 : 0; }
 static int decoder_variant() {
-    const int v = decoder_setting().load(std::memory_order_relaxed);
+    const int v = g_decoder.load(std::memory_order_relaxed);
     return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
 }
-int set_decoder(int v) { return decoder_setting().exchange(v); }
+int set_decoder(int v) { return g_decoder.exchange(v); }
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
@@ -5314,10 +5553,8 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     // index pass, fill pass; the fallback owns the long units from the start
     // (decode_long_unit): it goes first, on the side stream, beside passes 1 and 2
     static const uint32_t sm_res = resident_blocks(decode_small_kernel, kSmBlock, 8);
-    static const double sm_frac = [] {  // share of the resident grid (CPK_SM_FRAC: dev A/B)
-        const char* e = getenv("CPK_SM_FRAC");
-        return e ? atof(e) : mid_stream_knob() ? 0.85 : 1.0;
-    }();
+    const bool mid_stream = mid_side_stream();
+    const double sm_frac = mid_stream ? 0.85 : 1.0;  // share of the resident grid
     const uint32_t sm_cap = std::max(1u, (uint32_t)(sm_res * sm_frac));
     const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_cap);
     SideLaunch side(stream, ws, ws_bytes);
@@ -5343,8 +5580,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     window_fill_kernel<<<wfill_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, status, q);
     decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status, q);
-    // the mid units' passes on a second side stream, before the small kernel (mid_stream_knob)
-    const bool mid_stream = mid_stream_knob();
+    // the mid units' passes on a second side stream, before the small kernel (mid_side_stream)
     const hipStream_t ms = mid_stream ? side.stream2() : stream;
     if (!mid_stream) {
         if (small_variant() == 0) {
@@ -5359,8 +5595,15 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     }
     const uint32_t* const mid = q + kQHead + 2ull * n;
     // mid units: the indexed two-pass decoder (index pass + fill pass), or the fused
-    // single-pass decoder when selected (capnp_packed_set_decoder / CPK_DECODE=fused)
-    if (decoder_variant() == CAPNP_PACKED_DECODER_FUSED) {
+    // single-pass decoder when selected (capnp_packed_set_decoder)
+    // the streaming decoder may leave a failed unit's prefix: all-or-nothing takes the two-pass one
+    const int dv = (decoder_variant() == CAPNP_PACKED_DECODER_STREAM && small_variant() == 0)
+                       ? (int)CAPNP_PACKED_DECODER_TWO_PASS : decoder_variant();
+    if (dv == CAPNP_PACKED_DECODER_STREAM) {
+        const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);  // waves past the mid count exit
+        decode_stream_kernel<<<sd_blocks, kDsWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                      out_len, status, mid, q + 4);
+    } else if (dv == CAPNP_PACKED_DECODER_FUSED) {
         static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);
         const uint32_t fu_blocks = std::min((n + kFuWaves - 1) / kFuWaves, fu_res);
         decode_fused_kernel<<<fu_blocks, kFuWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,

@@ -307,13 +307,15 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
  * semantic one: every decoder is bit-exact):
  *   CAPNP_PACKED_DECODER_TWO_PASS  index pass + fill pass (the packed bytes are read twice);
  *   CAPNP_PACKED_DECODER_FUSED     single pass: per-lane 8-state entry maps, one read;
+ *   CAPNP_PACKED_DECODER_STREAM    single pass: lane-per-unit walk by 64-B windows, stores
+ *                                  by many lanes per unit (a failed unit may hold a prefix);
  *   CAPNP_PACKED_DECODER_AUTO      the library's default.
- * The environment variable CPK_DECODE=twopass|fused sets the initial value. Returns the
- * previous value; applies to batches enqueued after the call (process-wide). */
+ * Returns the previous value; applies to batches enqueued after the call (process-wide). */
 enum {
     CAPNP_PACKED_DECODER_AUTO = 0,
     CAPNP_PACKED_DECODER_TWO_PASS = 1,
-    CAPNP_PACKED_DECODER_FUSED = 2
+    CAPNP_PACKED_DECODER_FUSED = 2,
+    CAPNP_PACKED_DECODER_STREAM = 3
 };
 int capnp_packed_set_decoder(int decoder);
 
@@ -325,6 +327,17 @@ int capnp_packed_set_decoder(int decoder);
  * with on != 0 they are decoded through LDS and stored only when OK, at a cost (C5 decode
  * 0.69 -> 0.79 ms). */
 int capnp_packed_set_all_or_nothing(int on);
+
+/* Launch policy (process-wide, for batches enqueued from now on; returns the previous flags;
+ * unknown bits are ignored). No result depends on it, only where the kernels run:
+ *   CAPNP_PACKED_LAUNCH_LONG_INLINE      long units run after the main grid on the caller's stream
+ *                                        instead of on a side stream forked from and joined into it;
+ *   CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM  decode: mid units on a second side stream beside the small
+ *                                        units' kernel (helps batches of mostly small units with a
+ *                                        few mid ones; costs a fork/join otherwise). */
+#define CAPNP_PACKED_LAUNCH_LONG_INLINE 0x1u
+#define CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM 0x2u
+uint32_t capnp_packed_set_launch_flags(uint32_t flags);
 
 #ifdef __cplusplus
 }

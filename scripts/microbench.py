@@ -42,7 +42,10 @@ def main():
     ap.add_argument("--pk-stride", type=int, default=0, help="packed slot stride (default encode_bound)")
     ap.add_argument("--dense", action="store_true", help="decode from a dense packed stream")
     ap.add_argument("--no-store", action="store_true", help="decode with zero output capacity (walk only, no stores)")
+    ap.add_argument("--decoder", default="", help="mid-unit decoder (capnp_packed_set_decoder name)")
     a = ap.parse_args()
+    if a.decoder:
+        cp.set_decoder(a.decoder)
     n, ub = a.units, a.unit_bytes
     dev = torch.device("cuda", 0)
     d_in = cp.generate(n, ub, seed=0xC0DE0003, zero_thresh=a.zero_thresh, device=dev)

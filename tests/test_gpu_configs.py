@@ -19,7 +19,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["twopass", "fused"])
+@pytest.fixture(params=["twopass", "fused", "stream"])
 def decoder(request):
     """Runs the test under each mid-unit decoder (capnp_packed_set_decoder)."""
     with cp.decoder(request.param):
@@ -344,26 +344,17 @@ def struct_u32(v):
     return int(v).to_bytes(4, "little")
 
 
-@pytest.mark.parametrize("env", [{"CPK_MID_STREAM": "1"}, {"CPK_MID_STREAM": "1", "CPK_SM_FRAC": "0.3"},
-                                 {"CPK_SIDE_STREAM": "0"}])
-def test_c5_stream_knobs(env):
-    """The launch knobs read once per process: the opt-in second side
-    stream for a decode batch's mid units (CPK_MID_STREAM=1), with the small decoder's grid
-    at its default share and at 30%, and the long units after the main grid instead of on
-    the side stream (CPK_SIDE_STREAM=0). The C5 tests above, in a child process that sets them."""
-    import os
-    import subprocess
-    import sys
-    tests = os.path.dirname(os.path.abspath(__file__))
-    repo = os.path.dirname(tests)
-    code = ("import test_gpu_configs as t\n"
-            "for thr in (26, 128, 230): t.test_c5_skewed_sizes_every_unit(thr, 'twopass')\n"
-            "t.test_c5_full_size_1M_units('twopass')\n"
-            "import capnp_packed as cp\n"
-            "with cp.decoder('fused'): t.test_c5_skewed_sizes_every_unit(128, 'fused')\n"
-            "print('child ok')\n")
-    path = os.pathsep.join([os.path.join(repo, "capnp-zig_amd"), tests, repo])
-    run_env = dict(os.environ, PYTHONPATH=path, **env)
-    out = subprocess.run([sys.executable, "-c", code], env=run_env, cwd=repo, capture_output=True, text=True,
-                         timeout=110)
-    assert out.returncode == 0 and "child ok" in out.stdout, out.stderr[-3000:]
+@pytest.mark.parametrize("flags", [cp.LAUNCH_MID_SIDE_STREAM, cp.LAUNCH_LONG_INLINE,
+                                   cp.LAUNCH_MID_SIDE_STREAM | cp.LAUNCH_LONG_INLINE],
+                         ids=["mid_side_stream", "long_inline", "both"])
+def test_c5_launch_flags(flags):
+    """The launch policy (capnp_packed_set_launch_flags): the second side
+    stream for a decode batch's mid units (the small decoder's grid then at 85%), and the long
+    units after the main grid instead of on the side stream. The C5 tests above under each."""
+    with cp.launch_flags(flags):
+        for thr in (26, 128, 230):
+            test_c5_skewed_sizes_every_unit(thr, "twopass")
+        test_c5_full_size_1M_units("twopass")
+        for dec in ("fused", "stream"):
+            with cp.decoder(dec):
+                test_c5_skewed_sizes_every_unit(128, dec)

@@ -3,9 +3,10 @@
 returns UnexpectedEof / no output before it writes a byte): a mid or long unit whose
 status is UNEXPECTED_EOF or OUT_OF_SPACE leaves its output slot exactly as it was.
 Small units (<= 512 packed bytes into <= 8-KiB slots, decoded a lane each in one
-streaming pass) are the documented exception: a failed one may hold
-a prefix of its output, never a byte past its out_cap; with
-capnp_packed_set_all_or_nothing(1) they are all-or-nothing too (the group-staged decoder).
+streaming pass) and, under the streaming mid-unit decoder, mid units are
+the documented exception: a failed one may hold a prefix of its output,
+never a byte past its out_cap; with capnp_packed_set_all_or_nothing(1) they are
+all-or-nothing too (the group-staged small decoder, the two-pass mid decoder).
 
 Units of each size class are decoded from a dense packed stream
 (unaligned unit starts) into slots pre-filled with a sentinel byte:
@@ -25,7 +26,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["twopass", "fused"])
+@pytest.fixture(params=["twopass", "fused", "stream"])
 def decoder(request):
     """Runs the test under each mid-unit decoder (capnp_packed_set_decoder)."""
     with cp.decoder(request.param):
@@ -47,7 +48,19 @@ def words(rng, n_words, thr):
 
 @pytest.mark.parametrize("cls,n_words,thr", CLASSES, ids=[c[0] for c in CLASSES])
 def test_failed_units_leave_their_slot_untouched(cls, n_words, thr, decoder):
-    check_class(cls, n_words, thr, strict=False)
+    check_class(cls, n_words, thr, strict=False, prefix_mid=decoder == "stream")
+
+
+@pytest.mark.parametrize("cls,n_words,thr", CLASSES[1:], ids=[c[0] for c in CLASSES[1:]])
+def test_mid_units_all_or_nothing_when_asked_under_stream(cls, n_words, thr):
+    """capnp_packed_set_all_or_nothing(1) routes mid units past the streaming decoder (which
+    may leave a failed unit's prefix) to the two-pass decoder: every failed slot untouched."""
+    prev = cp.set_all_or_nothing(True)
+    try:
+        with cp.decoder("stream"):
+            check_class(cls, n_words, thr, strict=True)
+    finally:
+        cp.set_all_or_nothing(prev)
 
 
 def test_small_units_all_or_nothing_when_asked():
@@ -59,7 +72,7 @@ def test_small_units_all_or_nothing_when_asked():
         cp.set_all_or_nothing(prev)
 
 
-def check_class(cls, n_words, thr, strict):
+def check_class(cls, n_words, thr, strict, prefix_mid=False):
     rng = np.random.default_rng(0xC0DE + n_words)
     n = 384
     data = [words(rng, n_words, thr) for _ in range(n)]
@@ -104,7 +117,7 @@ def check_class(cls, n_words, thr, strict):
             assert ol[i] == len(ref)
             assert s[:len(ref)].tobytes() == ref, (cls, i)
             assert (s[len(ref):] == SENTINEL).all(), (cls, i, "bytes past out_len written")
-        elif cls == "small" and not strict:
+        elif (cls == "small" or (cls == "mid" and prefix_mid)) and not strict:
             assert (s[caps[i]:] == SENTINEL).all(), (cls, i, int(want), "bytes past out_cap written")
         else:
             assert (s == SENTINEL).all(), (cls, i, int(want), "failed unit wrote into its slot")
