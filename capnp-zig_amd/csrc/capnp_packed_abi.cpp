@@ -96,8 +96,11 @@ struct HostCtx {
         return CAPNP_PACKED_OK;
     }
     static size_t grow(size_t need) { return need < 65536 ? 65536 : need + need / 2; }
+    // A buffer grown by an unusually large call is given back on the next call that needs a
+    // quarter of it or less (above 64 MiB): the context does not pin its peak for the process.
+    static bool keep(size_t need, size_t cap) { return need <= cap && !(cap > (64u << 20) && need <= cap / 4); }
     int reserve(uint8_t** p, size_t* cap, size_t need) {
-        if (need <= *cap && *p) return CAPNP_PACKED_OK;
+        if (*p && keep(need, *cap)) return CAPNP_PACKED_OK;
         if (need > (SIZE_MAX / 3) * 2) return fail(CAPNP_PACKED_OUT_OF_SPACE, "workspace size overflows size_t");
         const size_t want = grow(need);
         if (*p) (void)hipFree(*p);
@@ -109,7 +112,7 @@ struct HostCtx {
         return CAPNP_PACKED_OK;
     }
     int reserve_host(uint8_t** p, size_t* cap, size_t need) {
-        if (need <= *cap && *p) return CAPNP_PACKED_OK;
+        if (*p && keep(need, *cap)) return CAPNP_PACKED_OK;
         if (need > (SIZE_MAX / 3) * 2) return fail(CAPNP_PACKED_OUT_OF_SPACE, "staging size overflows size_t");
         const size_t want = grow(need);
         if (*p) (void)hipHostFree(*p);
@@ -174,13 +177,16 @@ uint64_t unpack_bound(size_t n) { return n > (UINT64_MAX / 1024) ? UINT64_MAX : 
 // PCIe once (pinned staging), the kernels run with an output slot of `slot` bytes, and the
 // output comes back only when the unit is OK; *len_out is out_len (for OUT_OF_SPACE: the
 // size the unit needs).
+// reuse_in: the device already holds `in` from the previous call (a retry with a larger slot).
 int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out,
-               uint64_t* used_out = nullptr) {
+               uint64_t* used_out = nullptr, bool reuse_in = false) {
     int st = g_ctx.init();
     if (st) return st;
     if (n > SIZE_MAX - 16 || slot > SIZE_MAX - 16) return fail(CAPNP_PACKED_OUT_OF_SPACE, "buffer size overflows size_t");
-    if ((st = g_ctx.reserve(&g_ctx.d_in, &g_ctx.in_cap, n + 16))) return st;
-    if ((st = g_ctx.reserve_host(&g_ctx.h_in, &g_ctx.h_in_cap, n + 16))) return st;
+    if (!reuse_in) {
+        if ((st = g_ctx.reserve(&g_ctx.d_in, &g_ctx.in_cap, n + 16))) return st;
+        if ((st = g_ctx.reserve_host(&g_ctx.h_in, &g_ctx.h_in_cap, n + 16))) return st;
+    }
     const bool write = (kind == 0 || kind == 1 || kind == 4);
     if (write && (st = g_ctx.reserve(&g_ctx.d_out, &g_ctx.out_cap, slot + 16))) return st;
     uint64_t* const hm = g_ctx.h_meta;
@@ -188,7 +194,7 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
     std::memcpy(hm, meta, sizeof(meta));
     hipStream_t s = g_ctx.stream;
     hipError_t e = hipSuccess;
-    if (n) {
+    if (n && !reuse_in) {
         std::memcpy(g_ctx.h_in, in, n);
         e = hipMemcpyAsync(g_ctx.d_in, g_ctx.h_in, n, hipMemcpyHostToDevice, s);
     }
@@ -306,12 +312,20 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
     int st = ensure_device();
     if (st) return st;
     std::lock_guard<std::mutex> lock(g_ctx.mu);
-    // one H2D and one decode into a slot of the caller's capacity (never more than n packed
-    // bytes can produce): the decoders size every unit before writing it (message.zig:90),
-    // so a unit that does not fit ends OUT_OF_SPACE with its size in out_len
+    // One H2D and one decode into a device slot of min(cap, 8 n, at least 64 KiB) bytes: dense
+    // data expands ~1.1-2x, so that slot nearly always holds it, and a large reusable caller
+    // buffer does not size the device slot (up to 1024 n). A unit that does not fit ends
+    // OUT_OF_SPACE with its size in out_len (the output is copied back only when OK, so the
+    // caller's buffer is untouched, message.zig:90); if the caller's capacity holds that size
+    // the decode runs again from the input already on the device, into a slot of that size.
     const uint64_t bound = unpack_bound(n);
+    const uint64_t room = cap < bound ? cap : bound;
+    const uint64_t guess = n > (UINT64_MAX / 8) ? UINT64_MAX : (8ull * n < 65536 ? 65536 : 8ull * n);
+    const uint64_t first = room < guess ? room : guess;
     uint64_t len = 0;
-    st = run_single(1, in, n, out, (size_t)(cap < bound ? cap : bound), &len);
+    st = run_single(1, in, n, out, (size_t)first, &len);
+    if (st == CAPNP_PACKED_OUT_OF_SPACE && first < room && len <= room)
+        st = run_single(1, in, n, out, (size_t)len, &len, nullptr, true);
     *out_len = (st == CAPNP_PACKED_OK || st == CAPNP_PACKED_OUT_OF_SPACE) ? (size_t)len : 0;
     return st;
 }

@@ -5203,7 +5203,9 @@ struct StreamCtx {
     }
 };
 static std::mutex g_ctx_mu;
-static std::map<std::pair<int, uintptr_t>, std::unique_ptr<StreamCtx>> g_ctx;
+// shared_ptr: a batch being enqueued keeps its context alive even if capnp_packed_stream_release
+// drops it from the map meanwhile (no use-after-free, whatever the callers do).
+static std::map<std::pair<int, uintptr_t>, std::shared_ptr<StreamCtx>> g_ctx;
 
 // Byte offset of the piece-record region (decode: kRecStride per mid-list entry) in the
 // class workspace, after the lists and the tile / window table.
@@ -5258,9 +5260,9 @@ class SideLaunch {
         if (hipGetDevice(&dev) != hipSuccess) return;
         {
             std::lock_guard<std::mutex> g(g_ctx_mu);
-            std::unique_ptr<StreamCtx>& c = g_ctx[{dev, reinterpret_cast<uintptr_t>(main)}];
-            if (!c) c.reset(new StreamCtx());
-            ctx_ = c.get();
+            std::shared_ptr<StreamCtx>& c = g_ctx[{dev, reinterpret_cast<uintptr_t>(main)}];
+            if (!c) c = std::make_shared<StreamCtx>();
+            ctx_ = c;
         }
         lock_ = std::unique_lock<std::mutex>(ctx_->mu);
         if (g_launch_flags.load(std::memory_order_relaxed) & CAPNP_PACKED_LAUNCH_LONG_INLINE) {
@@ -5371,7 +5373,7 @@ class SideLaunch {
     hipStream_t main_;
     void* ws_;
     size_t ws_bytes_;
-    StreamCtx* ctx_ = nullptr;
+    std::shared_ptr<StreamCtx> ctx_;  // held until after the join and the unlock
     std::unique_lock<std::mutex> lock_;
     hipStream_t side_ = nullptr;
     bool ok_ = false, forked_ = false, forked2_ = false;
@@ -5383,7 +5385,7 @@ hipError_t release_stream(hipStream_t stream) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    std::unique_ptr<StreamCtx> c;
+    std::shared_ptr<StreamCtx> c;
     {
         std::lock_guard<std::mutex> g(g_ctx_mu);
         auto it = g_ctx.find({dev, reinterpret_cast<uintptr_t>(stream)});

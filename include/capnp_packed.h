@@ -98,11 +98,14 @@ int capnp_packed_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
 int capnp_packed_decoded_size(const uint8_t* in, size_t n, size_t* out_size);
 
 /* Replaces `fn unpackPacked(allocator, packed) ![]u8` (message.zig:88-145).
- * One host-to-device copy and one device decode into a slot of min(cap, 1024 n) bytes:
- * the decoders size the unit before writing it, so errors are raised before any output
- * byte is written, as in the reference (size pass first), and out is untouched on any
+ * One host-to-device copy and one device decode into a device slot of min(cap, 8 n,
+ * at least 64 KiB) bytes; if the unit needs more and cap holds it, the decode runs again
+ * from the input already on the device into a slot of exactly that size. The output is
+ * copied back only when the unit is OK, so errors are raised before any output byte
+ * reaches `out`, as in the reference (size pass first), and out is untouched on any
  * error. On OUT_OF_SPACE, *out_len is the required size: a caller may pass a guessed
- * capacity and call again with the exact one. */
+ * capacity and call again with the exact one. The device buffers grow with the largest
+ * call and are given back by the next call needing a quarter of them or less (> 64 MiB). */
 int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 
 /* ------------------------------------------------------------------------

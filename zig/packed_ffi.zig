@@ -226,7 +226,8 @@ pub fn estimateUnpackedSize(packed_bytes: []const u8) Error!usize {
 /// call into a buffer of 4x the packed size; a message that expands more reports its size
 /// (OUT_OF_SPACE) and is decoded again into a buffer of exactly that size.
 pub fn unpackPacked(allocator: std.mem.Allocator, packed_bytes: []const u8) Error![]u8 {
-    var cap: usize = @max(4096, 4 * packed_bytes.len);
+    // 4x the packed size, saturating (no overflow panic in safe builds)
+    var cap: usize = @max(4096, std.math.mul(usize, 4, packed_bytes.len) catch std.math.maxInt(usize));
     var attempt: u32 = 0;
     while (true) : (attempt += 1) {
         const out = try allocator.alloc(u8, cap);
@@ -241,7 +242,11 @@ pub fn unpackPacked(allocator: std.mem.Allocator, packed_bytes: []const u8) Erro
             allocator.free(out);
             return err;
         };
-        return allocator.realloc(out, len);
+        // a failed shrink must not leak `out`
+        return allocator.realloc(out, len) catch |err| {
+            allocator.free(out);
+            return err;
+        };
     }
 }
 
@@ -253,7 +258,7 @@ pub const ReadResult = struct { framed: []u8, consumed: usize };
 /// took; the caller advances its buffer by `consumed`. EndOfStream means the buffer
 /// holds only part of the message (read more and call again).
 pub fn readPackedMessageBuffered(allocator: std.mem.Allocator, buffered: []const u8) Error!ReadResult {
-    var cap: usize = @max(4096, 8 * buffered.len);
+    var cap: usize = @max(4096, std.math.mul(usize, 8, buffered.len) catch std.math.maxInt(usize));
     while (true) {
         const buf = try allocator.alloc(u8, cap);
         var len: usize = 0;
@@ -268,7 +273,11 @@ pub fn readPackedMessageBuffered(allocator: std.mem.Allocator, buffered: []const
             allocator.free(buf);
             return err;
         };
-        return .{ .framed = try allocator.realloc(buf, len), .consumed = used };
+        const framed = allocator.realloc(buf, len) catch |err| {
+            allocator.free(buf); // a failed shrink must not leak `buf`
+            return err;
+        };
+        return .{ .framed = framed, .consumed = used };
     }
 }
 
