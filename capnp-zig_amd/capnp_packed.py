@@ -17,6 +17,7 @@ for device memory and streams): uint8 byte buffers, int64 offset/length tensors
 from __future__ import annotations
 
 import ctypes
+from collections import deque
 import gc
 import os
 import struct
@@ -208,6 +209,14 @@ SIGNATURES = {
     "capnp_packed_set_decoder": (ctypes.c_int, [ctypes.c_int]),
     "capnp_packed_set_all_or_nothing": (ctypes.c_int, [ctypes.c_int]),
     "capnp_packed_set_launch_flags": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "capnp_packed_framer_create": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "capnp_packed_framer_destroy": (ctypes.c_int, [_vp]),
+    "capnp_packed_framer_read": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp,
+                                                _vp, ctypes.c_uint32, _vp, ctypes.POINTER(ctypes.c_uint32)]),
+    "capnp_packed_framer_reset": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "capnp_packed_framer_buffered": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
+    "capnp_packed_framer_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64),
+                                                 ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 # capnp_packed_set_decoder values (include/capnp_packed.h)
@@ -473,6 +482,91 @@ def read_packed_message_bytes(data) -> tuple:
 # Framing for packed byte streams
 # ---------------------------------------------------------------------------
 
+class FramerSession:
+    """A capnp_packed_framer: the Framer state of n connections kept on the device between
+    reads (include/capnp_packed.h). Each connection's unconsumed packed bytes
+    stay in device memory and the walk to the current message's end resumes where the last
+    read left it, so a message split over k reads is uploaded once and walked once."""
+
+    def __init__(self, n_conns: int):
+        h = _vp()
+        _raise(lib().capnp_packed_framer_create(int(n_conns), ctypes.byref(h)), "framer_create")
+        self.handle, self.n = h, int(n_conns)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().capnp_packed_framer_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def read(self, reads: dict):
+        """Append `reads` ({connection: bytes}) and pop every whole message. Returns
+        (frames, status): frames[c] lists connection c's frames in order (read-only
+        memoryviews of the call's frame buffers), status an int32 array: END_OF_STREAM, or the
+        reader's error after which the connection's bytes were dropped."""
+        n = self.n
+        lens = np.zeros(n, dtype=np.uint64)
+        for c, d in reads.items():
+            lens[c] = len(d)
+        off = np.zeros(n, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)[:-1]
+        total = int(lens.sum())
+        host = np.empty(max(total, 1), dtype=np.uint8)
+        for c, d in reads.items():
+            if len(d):
+                host[int(off[c]):int(off[c]) + len(d)] = np.frombuffer(d, dtype=np.uint8)
+        frames = {}
+        status = np.zeros(n, dtype=np.int32)
+        cap, max_frames = max(1 << 16, 4 * total), max(1024, total // 2 + 64)
+        first = True
+        while True:
+            buf = np.empty(cap, dtype=np.uint8)
+            f_off = np.empty(max_frames, dtype=np.uint64)
+            f_len = np.empty(max_frames, dtype=np.uint64)
+            f_conn = np.empty(max_frames, dtype=np.uint32)
+            st_call = np.zeros(n, dtype=np.int32)
+            nf = ctypes.c_uint32(0)
+            rc = lib().capnp_packed_framer_read(
+                self.handle, host.ctypes.data if first else None, total if first else 0,
+                off.ctypes.data, lens.ctypes.data, buf.ctypes.data, cap, f_off.ctypes.data, f_len.ctypes.data,
+                f_conn.ctypes.data, max_frames, st_call.ctypes.data, ctypes.byref(nf))
+            if rc not in (OK, OUT_OF_SPACE):
+                _raise(rc, "framer_read")
+            first = False
+            err = st_call != END_OF_STREAM
+            status[err] = st_call[err]
+            view = memoryview(buf).toreadonly()
+            k = nf.value
+            for o, ln, c in zip(f_off[:k].tolist(), f_len[:k].tolist(), f_conn[:k].tolist()):
+                frames.setdefault(c, []).append(view[o:o + ln])
+            if rc == OK:
+                break
+            # frames or the table filled up: pop the rest into larger ones (no new bytes)
+            if k == 0:
+                cap *= 2
+            max_frames *= 2
+        status[status == 0] = END_OF_STREAM
+        return frames, status
+
+    def buffered(self, c: int) -> int:
+        b = ctypes.c_uint64()
+        _raise(lib().capnp_packed_framer_buffered(self.handle, int(c), ctypes.byref(b)), "framer_buffered")
+        return b.value
+
+    def reset(self, c: int) -> None:
+        _raise(lib().capnp_packed_framer_reset(self.handle, int(c)), "framer_reset")
+
+    def stats(self) -> dict:
+        up, mv = ctypes.c_uint64(), ctypes.c_uint64()
+        _raise(lib().capnp_packed_framer_stats(self.handle, ctypes.byref(up), ctypes.byref(mv)), "framer_stats")
+        return {"uploaded_bytes": up.value, "moved_bytes": mv.value}
+
+
 class PackedFramer:
     """The RPC `Framer` (src/rpc/level0/framing.zig:4-90) for a PACKED byte stream.
     It has the same surface: push / buffered_bytes / reset / pop_frame.
@@ -481,147 +575,103 @@ class PackedFramer:
       while the buffered bytes do not hold one yet (the reader's EndOfStream).
     - pop_frame() raises the reader's other errors (reader.zig:84-156). The caller then
       reset()s, as Connection.handleRead does (level2/connection.zig:175-184).
-    - A message's end is only known by decoding its packed records. So pop_frame runs
-      Reader.readPackedMessage on the device through the single-buffer C-ABI.
-    - PackedConnections batches this across many connections."""
+    - A message's end is only known by decoding its packed records, so the buffered bytes
+      live on the device (a one-connection FramerSession): a push's bytes are uploaded once,
+      and the walk to the message end resumes where the previous pop left it.
+    - PackedConnections does this for many connections at once."""
 
     max_frame_words = 8 * 1024 * 1024  # framing.zig:5 / reader.zig:6
     max_segment_count = MAX_SEGMENT_COUNT
 
     def __init__(self):
-        self.buffer = bytearray()
+        self.session = FramerSession(1)
+        self.pending = []      # pushed bytes not yet handed to the session
+        self.ready = deque()   # frames popped from the device (then the error that ended them)
 
     def push(self, data) -> None:
         if len(data):
-            self.buffer += bytes(data)
+            self.pending.append(bytes(data))
 
     def buffered_bytes(self) -> int:
-        return len(self.buffer)
+        return self.session.buffered(0) + sum(len(d) for d in self.pending)
 
     def reset(self) -> None:
-        self.buffer.clear()
+        self.session.reset(0)
+        self.pending.clear()
+        self.ready.clear()
 
     def pop_frame(self):
-        if not self.buffer:
+        if not self.ready and self.pending:
+            data = b"".join(self.pending)
+            self.pending.clear()
+            frames, status = self.session.read({0: data})
+            self.ready.extend(bytes(f) for f in frames.get(0, []))
+            if int(status[0]) != END_OF_STREAM:
+                rs = int(status[0])
+                self.ready.append(_ERRORS.get(rs, DeviceError)(
+                    f"readPackedMessage: {lib().capnp_packed_status_name(rs).decode()}"))
+        if not self.ready:
             return None
-        try:
-            framed, used = read_packed_message_bytes(self.buffer)
-        except EndOfStream:
-            return None
-        del self.buffer[:used]
-        return framed
+        v = self.ready.popleft()
+        if isinstance(v, Exception):
+            raise v
+        return v
+
+
+class _ConnView:
+    """A PackedConnections connection's framer surface (bufferedBytes / reset)."""
+
+    def __init__(self, session, c):
+        self._s, self._c = session, c
+
+    def buffered_bytes(self) -> int:
+        return self._s.buffered(self._c)
+
+    def reset(self) -> None:
+        self._s.reset(self._c)
 
 
 class PackedConnections:
     """Connection.handleRead (src/rpc/level2/connection.zig:153-203) over many
-    connections at once. Each connection has its own PackedFramer buffer.
-    - handle_read(reads) pushes every connection's socket read, copies the buffered
-      bytes to the device once, and pops frames in rounds. Each round is one
-      read_message_batch with one unit per connection that may still hold a message.
+    connections at once, on one FramerSession: every connection's Framer state (its
+    unconsumed packed bytes, the current message's framed length, where the walk to its end
+    stopped) stays on the device between reads.
+    - handle_read(reads) uploads only the new bytes and pops every whole message in one
+      native call (capnp_packed_framer_read).
     - Per connection, the result is the list of frames popped (in order), or a PackedError.
     - On the error the connection's framer is reset and the connection is closed for
       further reads, as handleRead does (175-184). Frames popped before the error are
       dropped with it; handleRead would already have delivered them, so
       `frames_before_error` keeps them.
-    - A connection whose buffer ends inside a message keeps those bytes for its next read
-      (the reader's EndOfStream = popFrame's null)."""
+    - A connection whose bytes end inside a message keeps them for its next read (the
+      reader's EndOfStream = popFrame's null), and its walk resumes there."""
 
     def __init__(self, n_conns: int, device="cuda"):
-        self.framers = [PackedFramer() for _ in range(n_conns)]
+        self.session = FramerSession(n_conns)
+        self.framers = [_ConnView(self.session, c) for c in range(n_conns)]
         self.closed = [False] * n_conns
         self.frames_before_error = {}
-        self._last = {}  # connection -> its last frame's size (the next round's slot guess)
         self.device = torch.device(device)
 
     def handle_read(self, reads: dict) -> dict:
-        """One native call (capnp_packed_frame_connections): the connections' buffered
-        bytes go to the device once, rounds of the batched reader pop every frame, and the
-        frames come back in one host buffer. Each frame is a read-only memoryview into that
-        buffer (no per-frame copy; the buffer lives as long as its frames). A connection's
-        framer keeps only the bytes left after its last whole message."""
-        conns, sizes = [], []
-        for c in range(len(self.framers)):
-            if self.closed[c]:
-                continue
-            m = self.framers[c].buffered_bytes() + (len(reads[c]) if c in reads else 0)
-            if m:
-                conns.append(c)
-                sizes.append(m)
-        result = {c: [] for c in conns}
-        if not conns:
-            return result
-        k = len(conns)
-        lens = np.array(sizes, dtype=np.uint64)
-        base = np.zeros(k, dtype=np.uint64)
-        base[1:] = np.cumsum(lens)[:-1]
-        total = int(lens.sum())
-        # the framers' bytes, then this read, straight into one input buffer (the framer's
-        # push is the copy into it)
-        host = np.empty(max(total, 1), dtype=np.uint8)
-        for i, c in enumerate(conns):
-            b, old = int(base[i]), self.framers[c].buffer
-            if old:
-                host[b:b + len(old)] = np.frombuffer(old, dtype=np.uint8)
-                b += len(old)
-            if c in reads and len(reads[c]):
-                host[b:b + len(reads[c])] = np.frombuffer(reads[c], dtype=np.uint8)
-        # first guess at each frame's size: the connection's last frame (8 KiB at first), at
-        # most 8x its buffered bytes; OutOfSpace rounds are redone at the framed length
-        guess = np.array([min(self._last.get(c, 8192), max(8, 8 * int(n))) for c, n in zip(conns, sizes)],
-                         dtype=np.uint64)
-        max_frames = total // 64 + k + 16
-        frames_cap = max(1 << 16, 4 * total + 2 * int(guess.sum()))
-        consumed = np.zeros(k, dtype=np.uint64)
-        status = np.zeros(k, dtype=np.int32)
-        nf = ctypes.c_uint32(0)
-        while True:
-            g = guess.copy()
-            frames = np.empty(frames_cap, dtype=np.uint8)
-            f_off = np.empty(max_frames, dtype=np.uint64)
-            f_len = np.empty(max_frames, dtype=np.uint64)
-            f_conn = np.empty(max_frames, dtype=np.uint32)
-            st = lib().capnp_packed_frame_connections(
-                host.ctypes.data, total, base.ctypes.data, lens.ctypes.data, k, g.ctypes.data, frames.ctypes.data,
-                frames_cap, f_off.ctypes.data, f_len.ctypes.data, f_conn.ctypes.data, max_frames,
-                consumed.ctypes.data, status.ctypes.data, ctypes.byref(nf))
-            if st != OUT_OF_SPACE:
-                break
-            # the frames or the frame table did not fit: the call is redone (its input is unchanged)
-            frames_cap *= 2
-            max_frames = min(2 * max_frames, total // 2 + k + 16)
-        _raise(st, "frame_connections")
-        view = memoryview(frames).toreadonly()
-        n = nf.value
-        order = np.argsort(f_conn[:n], kind="stable")  # frames by connection, in pop order
-        offs, flen = f_off[:n][order].tolist(), f_len[:n][order].tolist()
-        ends = np.cumsum(np.bincount(f_conn[:n], minlength=k)).tolist()
-        s0 = 0
-        # one memoryview per frame: the cyclic collector is held off while they are made (they
-        # hold no cycles; its passes over the caller's live objects cost more than the slicing
-        # itself: 65K frames took 80-170 ms with it, 10 ms without, DESIGN.md §2.7)
+        """One native call: the connections' new bytes go to the device once, every whole
+        message is popped, and the frames come back as read-only memoryviews of the call's
+        frame buffer (no per-frame copy; the buffer lives as long as its frames)."""
+        live = {c: d for c, d in reads.items() if not self.closed[c] and len(d)}
         gc_on = gc.isenabled()
-        gc.disable()
+        gc.disable()  # no cycles among the views; the collector's passes cost more (DESIGN.md §2.7)
         try:
-            for i, c in enumerate(conns):
-                s1 = ends[i]
-                if s1 > s0:
-                    result[c] = [view[o:o + ln] for o, ln in zip(offs[s0:s1], flen[s0:s1])]
-                s0 = s1
-                self._last[c] = int(g[i])
-                rs = int(status[i])
-                if rs != END_OF_STREAM:
-                    err = _ERRORS.get(rs, DeviceError)(
-                        f"readPackedMessage: {lib().capnp_packed_status_name(rs).decode()}")
-                    self.frames_before_error[c] = result[c]
-                    result[c] = err
-                    self.framers[c].reset()
-                    self.closed[c] = True
-                else:  # the bytes after the last whole message wait for the next read
-                    b = int(base[i] + consumed[i])
-                    self.framers[c].buffer = bytearray(host[b:int(base[i] + lens[i])].tobytes())
+            frames, status = self.session.read(live)
         finally:
             if gc_on:
                 gc.enable()
+        result = {c: [] for c in live}
+        result.update(frames)
+        for c in np.nonzero(status != END_OF_STREAM)[0].tolist():
+            rs = int(status[c])
+            self.frames_before_error[c] = result.get(c, [])
+            result[c] = _ERRORS.get(rs, DeviceError)(f"readPackedMessage: {lib().capnp_packed_status_name(rs).decode()}")
+            self.closed[c] = True
         return result
 
 

@@ -651,3 +651,394 @@ int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const u
 
 }  // extern "C"
 
+
+// ---------------------------------------------------------------------------
+// Resumable framing of packed socket streams: Connection.handleRead
+// (src/rpc/level2/connection.zig:153-203) with Framer state kept across reads
+// (src/rpc/level0/framing.zig:42-90 keeps expected_total; reader.zig:84-156 is one pass).
+// Each connection's unconsumed packed bytes live in a region of one device arena, so a read
+// uploads only its new bytes. Per connection the session keeps the current message's framed
+// length (need, from read_header_kernel once its header is decoded) and where its walk
+// stopped (X: packed bytes from the message start, W: words decoded), so the next read's
+// walk (frame_walk_kernel) starts there: a message split over k reads is uploaded once and
+// walked once. A complete message is decoded straight from the arena into its frame slot
+// (the batch decoder) and copied to the caller's frames buffer.
+//
+// Regions: a connection's region is [off, off + cap) of the arena, its bytes [m0, len) of
+// it. A read that does not fit moves the connection's bytes to a fresh region of twice their
+// size at the arena top (the bytes of a partial message move once per doubling); when the
+// top reaches the end, every connection's bytes move to a new arena of twice the live size.
+// ---------------------------------------------------------------------------
+struct capnp_packed_framer {
+    std::mutex mu;
+    uint32_t n = 0;
+    hipStream_t s = nullptr;
+    uint8_t* arena = nullptr;
+    uint64_t acap = 0, top = 0;
+    std::vector<uint64_t> off, cap, m0, len, need, X, W;  // per connection (host authoritative)
+    // device scratch: per-connection arrays (base, avail, need, X, W, consumed, status),
+    // lists and unit metadata of a round, copy jobs, the input staging and the frame slots
+    uint8_t* d_state = nullptr;
+    uint64_t state_cap = 0;
+    uint8_t* d_stage = nullptr;
+    uint64_t stage_cap = 0;
+    uint8_t* d_frames = nullptr;
+    uint64_t frames_dcap = 0;
+    uint64_t uploaded = 0, moved = 0;  // bytes copied H2D (new reads) and moved between regions
+
+    ~capnp_packed_framer() {
+        if (s) (void)hipStreamSynchronize(s);
+        if (arena) (void)hipFree(arena);
+        if (d_state) (void)hipFree(d_state);
+        if (d_stage) (void)hipFree(d_stage);
+        if (d_frames) (void)hipFree(d_frames);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    static int grow(uint8_t** p, uint64_t* c, uint64_t need) {
+        if (*p && need <= *c) return CAPNP_PACKED_OK;
+        const uint64_t want = need < 65536 ? 65536 : need + need / 2;
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+        *c = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(p), want);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(framer session)");
+        *c = want;
+        return CAPNP_PACKED_OK;
+    }
+    int run_jobs(std::vector<uint64_t>& jobs) {
+        if (jobs.empty()) return CAPNP_PACKED_OK;
+        const uint32_t nj = (uint32_t)(jobs.size() / 3);
+        // the jobs go after the per-connection arrays in the state scratch
+        const uint64_t at = (uint64_t)n * 56 + 256;
+        int st = grow(&d_state, &state_cap, at + jobs.size() * 8 + 64 * (uint64_t)n + 4096);
+        if (st) return st;
+        uint64_t* const dj = reinterpret_cast<uint64_t*>(d_state + at);
+        hipError_t e = hipMemcpyAsync(dj, jobs.data(), jobs.size() * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = cpk::launch_copy_jobs(dj, nj, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);  // `jobs` is reused by the caller
+        if (e != hipSuccess) return hip_fail(e, "framer copy jobs");
+        jobs.clear();
+        return CAPNP_PACKED_OK;
+    }
+    static uint64_t region_for(uint64_t bytes) { return std::max<uint64_t>(65536, (2 * bytes + 255) & ~255ull); }
+    // Every connection's live bytes into a new arena sized for `extra` more bytes of regions.
+    int rearena(const std::vector<uint64_t>& want) {
+        uint64_t total = 0;
+        for (uint32_t c = 0; c < n; ++c) total += want[c] ? region_for(want[c]) : 0;
+        const uint64_t ncap = std::max<uint64_t>(2 * total, 1u << 20);
+        uint8_t* na = nullptr;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&na), ncap + 64);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(framer arena)");
+        std::vector<uint64_t> jobs;
+        uint64_t t = 0;
+        for (uint32_t c = 0; c < n; ++c) {
+            const uint64_t live = len[c] - m0[c];
+            if (!want[c]) {
+                off[c] = cap[c] = m0[c] = len[c] = 0;
+                continue;
+            }
+            const uint64_t rc = region_for(want[c]);
+            if (live) {
+                jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(na + t), reinterpret_cast<uint64_t>(arena + off[c] + m0[c]), live});
+                moved += live;
+            }
+            off[c] = t;
+            cap[c] = rc;
+            m0[c] = 0;
+            len[c] = live;
+            t += rc;
+        }
+        int st = run_jobs(jobs);
+        if (st) {
+            (void)hipFree(na);
+            return st;
+        }
+        if (arena) (void)hipFree(arena);
+        arena = na;
+        acap = ncap;
+        top = t;
+        return CAPNP_PACKED_OK;
+    }
+};
+
+namespace {
+
+int framer_check(capnp_packed_framer* f, uint32_t conn) {
+    if (!f) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "framer is null");
+    if (conn >= f->n) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "connection index out of range");
+    return CAPNP_PACKED_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int capnp_packed_framer_create(uint32_t n_conns, capnp_packed_framer** out) {
+    if (!out) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "out is null");
+    *out = nullptr;
+    if (n_conns == 0) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "a framer needs at least one connection");
+    int st = ensure_device();
+    if (st) return st;
+    capnp_packed_framer* f = new (std::nothrow) capnp_packed_framer();
+    if (!f) return fail(CAPNP_PACKED_OUT_OF_SPACE, "framer allocation");
+    f->n = n_conns;
+    for (auto* v : {&f->off, &f->cap, &f->m0, &f->len, &f->need, &f->X, &f->W}) v->assign(n_conns, 0);
+    hipError_t e = hipStreamCreateWithFlags(&f->s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        f->s = nullptr;
+        delete f;
+        return hip_fail(e, "hipStreamCreate(framer session)");
+    }
+    *out = f;
+    return CAPNP_PACKED_OK;
+}
+
+int capnp_packed_framer_destroy(capnp_packed_framer* f) {
+    if (!f) return CAPNP_PACKED_OK;
+    delete f;  // synchronises its stream first
+    return CAPNP_PACKED_OK;
+}
+
+int capnp_packed_framer_reset(capnp_packed_framer* f, uint32_t conn) {
+    int st = framer_check(f, conn);
+    if (st) return st;
+    std::lock_guard<std::mutex> lock(f->mu);
+    f->m0[conn] = f->len[conn] = 0;
+    f->need[conn] = f->X[conn] = f->W[conn] = 0;
+    return CAPNP_PACKED_OK;
+}
+
+int capnp_packed_framer_buffered(capnp_packed_framer* f, uint32_t conn, uint64_t* bytes) {
+    int st = framer_check(f, conn);
+    if (st) return st;
+    if (!bytes) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "bytes is null");
+    std::lock_guard<std::mutex> lock(f->mu);
+    *bytes = f->len[conn] - f->m0[conn];
+    return CAPNP_PACKED_OK;
+}
+
+int capnp_packed_framer_stats(capnp_packed_framer* f, uint64_t* uploaded, uint64_t* moved) {
+    if (!f || !uploaded || !moved) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null pointer");
+    std::lock_guard<std::mutex> lock(f->mu);
+    *uploaded = f->uploaded;
+    *moved = f->moved;
+    return CAPNP_PACKED_OK;
+}
+
+int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
+                             const uint64_t* in_len, uint8_t* frames, uint64_t frames_cap, uint64_t* frame_off,
+                             uint64_t* frame_len, uint32_t* frame_conn, uint32_t max_frames, int32_t* status,
+                             uint32_t* n_frames) {
+    if (!n_frames) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "n_frames is null");
+    *n_frames = 0;
+    if (!f) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "framer is null");
+    const uint32_t n = f->n;
+    if (!status || (in_bytes && (!in || !in_off || !in_len)) || (max_frames && (!frame_off || !frame_len || !frame_conn)) ||
+        (frames_cap && !frames))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null pointer");
+    if (in_len)
+        for (uint32_t c = 0; c < n; ++c)
+            if (in_len[c] && (!in_off || in_off[c] > in_bytes || in_len[c] > in_bytes - in_off[c]))
+                return fail(CAPNP_PACKED_INVALID_ARGUMENT, "connection bytes outside the input buffer");
+    std::lock_guard<std::mutex> lock(f->mu);
+    const hipStream_t s = f->s;
+    hipError_t e = hipSuccess;
+    int st = CAPNP_PACKED_OK;
+    for (uint32_t c = 0; c < n; ++c) status[c] = CAPNP_PACKED_END_OF_STREAM;
+
+    // ---- 1. the new bytes: one H2D into the staging buffer, appended to the regions ---------
+    if (in_bytes && in_len) {
+        if ((st = capnp_packed_framer::grow(&f->d_stage, &f->stage_cap, in_bytes + 32))) return st;
+        e = hipMemcpyAsync(f->d_stage, in, in_bytes, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
+        f->uploaded += in_bytes;
+        // regions: a connection whose bytes would pass its region's end gets a new one
+        std::vector<uint64_t> want(n, 0);
+        uint64_t grow_bytes = 0;
+        bool any_grow = false;
+        for (uint32_t c = 0; c < n; ++c) {
+            const uint64_t live = f->len[c] - f->m0[c] + in_len[c];
+            want[c] = live;
+            if (in_len[c] && f->len[c] + in_len[c] > f->cap[c]) {
+                any_grow = true;
+                grow_bytes += capnp_packed_framer::region_for(live);
+            }
+        }
+        std::vector<uint64_t> jobs;
+        if (any_grow && f->top + grow_bytes > f->acap) {
+            if ((st = f->rearena(want))) return st;  // every region sized for its bytes after this read
+        } else if (any_grow) {
+            for (uint32_t c = 0; c < n; ++c) {
+                if (!in_len[c] || f->len[c] + in_len[c] <= f->cap[c]) continue;
+                const uint64_t live = f->len[c] - f->m0[c];
+                const uint64_t rc = capnp_packed_framer::region_for(want[c]);
+                if (live) {
+                    jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + f->top),
+                                             reinterpret_cast<uint64_t>(f->arena + f->off[c] + f->m0[c]), live});
+                    f->moved += live;
+                }
+                f->off[c] = f->top;
+                f->cap[c] = rc;
+                f->m0[c] = 0;
+                f->len[c] = live;
+                f->top += rc;
+            }
+        }
+        for (uint32_t c = 0; c < n; ++c) {
+            if (!in_len[c]) continue;
+            jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + f->off[c] + f->len[c]),
+                                     reinterpret_cast<uint64_t>(f->d_stage + in_off[c]), in_len[c]});
+            f->len[c] += in_len[c];
+        }
+        if ((st = f->run_jobs(jobs))) return st;
+    }
+
+    // ---- 2. rounds: headers, walks from the saved positions, decodes of whole messages ------
+    // state scratch: base, avail, need, X, W, consumed (u64 x n), status (i32 x n), then round
+    // lists / unit metadata (7 u64 x n) and the copy jobs (run_jobs) past them
+    if ((st = capnp_packed_framer::grow(&f->d_state, &f->state_cap, (uint64_t)n * 56 + 256 + 64ull * n + 4096))) return st;
+    uint64_t* const d_base = reinterpret_cast<uint64_t*>(f->d_state);
+    uint64_t* const d_avail = d_base + n;
+    uint64_t* const d_need = d_base + 2ull * n;
+    uint64_t* const d_X = d_base + 3ull * n;
+    uint64_t* const d_W = d_base + 4ull * n;
+    uint64_t* const d_cons = d_base + 5ull * n;
+    int32_t* const d_st = reinterpret_cast<int32_t*>(d_base + 6ull * n);
+    // round scratch past the copy-job area would be reallocated by run_jobs; a separate block:
+    std::vector<uint64_t> h(6ull * n), hm(7ull * n);
+    std::vector<int32_t> hst(n);
+    std::vector<uint32_t> list;
+    std::vector<uint8_t> dead(n, 0);  // an error this call: the connection was reset
+    uint64_t fcur = 0;
+    uint32_t nf = 0;
+    uint8_t* d_round = nullptr;  // unit metadata of the header and decode passes (7 u64 x k + list)
+    uint64_t round_cap = 0;
+    struct Free {
+        uint8_t** p;
+        ~Free() {
+            if (*p) (void)hipFree(*p);
+        }
+    } free_round{&d_round};
+    auto fail_conn = [&](uint32_t c, int32_t code) {
+        status[c] = code;
+        dead[c] = 1;
+        f->m0[c] = f->len[c] = 0;  // Connection.handleRead resets the framer (connection.zig:175-184)
+        f->need[c] = f->X[c] = f->W[c] = 0;
+    };
+    bool full = false;
+    while (!full) {
+        // headers of the connections whose current message has none yet
+        list.clear();
+        for (uint32_t c = 0; c < n; ++c)
+            if (!dead[c] && f->need[c] == 0 && f->len[c] > f->m0[c]) list.push_back(c);
+        uint32_t k = (uint32_t)list.size();
+        if ((st = capnp_packed_framer::grow(&d_round, &round_cap, 7ull * 8 * (n + 1) + 4ull * n + 256))) return st;
+        uint64_t* const r_in_off = reinterpret_cast<uint64_t*>(d_round);
+        if (k) {
+            for (uint32_t j = 0; j < k; ++j) {
+                const uint32_t c = list[j];
+                hm[j] = f->off[c] + f->m0[c];
+                hm[k + j] = f->len[c] - f->m0[c];
+            }
+            e = hipMemcpyAsync(r_in_off, hm.data(), 2ull * k * 8, hipMemcpyHostToDevice, s);
+            uint64_t* const r_len = r_in_off + 2ull * k;
+            uint64_t* const r_cons = r_in_off + 3ull * k;
+            int32_t* const r_st = reinterpret_cast<int32_t*>(r_in_off + 4ull * k);
+            if (e == hipSuccess) e = cpk::launch_read_header(f->arena, r_in_off, r_in_off + k, k, r_len, r_cons, r_st, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 2ull * k, r_len, 3ull * k * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hip_fail(e, "framer header pass");
+            const int32_t* const hs = reinterpret_cast<const int32_t*>(hm.data() + 4ull * k);
+            for (uint32_t j = 0; j < k; ++j) {
+                const uint32_t c = list[j];
+                if (hs[j] == CAPNP_PACKED_OK) {
+                    f->need[c] = hm[2ull * k + j];
+                    f->X[c] = f->W[c] = 0;
+                } else if (hs[j] != CAPNP_PACKED_END_OF_STREAM) {
+                    fail_conn(c, hs[j]);
+                }
+            }
+        }
+        // walks of the connections whose framed length is known, from where they stopped
+        list.clear();
+        for (uint32_t c = 0; c < n; ++c)
+            if (!dead[c] && f->need[c] != 0 && f->len[c] > f->m0[c]) list.push_back(c);
+        k = (uint32_t)list.size();
+        if (k == 0) break;
+        for (uint32_t c = 0; c < n; ++c) {
+            h[c] = f->off[c] + f->m0[c];
+            h[n + c] = f->len[c] - f->m0[c];
+            h[2ull * n + c] = f->need[c];
+            h[3ull * n + c] = f->X[c];
+            h[4ull * n + c] = f->W[c];
+        }
+        uint32_t* const r_list = reinterpret_cast<uint32_t*>(r_in_off + 7ull * (n + 1));
+        e = hipMemcpyAsync(d_base, h.data(), 5ull * n * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(r_list, list.data(), 4ull * k, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_cons, d_st, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(h.data() + 3ull * n, d_X, 3ull * n * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), d_st, 4ull * n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "framer walk pass");
+        // whole messages: decoded from the arena into frame slots, then to the caller's buffer
+        std::vector<uint32_t> done;
+        uint64_t slots = 0;
+        for (uint32_t c : list) {
+            const int32_t ws = hst[c];
+            if (ws == CAPNP_PACKED_END_OF_STREAM) {  // the walk stopped at the held bytes' end
+                f->X[c] = h[3ull * n + c];
+                f->W[c] = h[4ull * n + c];
+            } else if (ws == CAPNP_PACKED_OK) {
+                const uint64_t L = f->need[c];
+                if (nf + done.size() + 1 > max_frames || fcur + slots + L > frames_cap) {
+                    full = true;  // stays whole in its region: the next call pops it
+                    continue;
+                }
+                done.push_back(c);
+                slots += (L + 7) & ~7ull;
+            } else {
+                fail_conn(c, ws);
+            }
+        }
+        k = (uint32_t)done.size();
+        if (k == 0) break;
+        if ((st = capnp_packed_framer::grow(&f->d_frames, &f->frames_dcap, slots + 16))) return st;
+        uint64_t so = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t c = done[j];
+            hm[j] = f->off[c] + f->m0[c];         // in_off
+            hm[k + j] = h[5ull * n + c];          // in_len = consumed
+            hm[2ull * k + j] = so;                // out_off
+            hm[3ull * k + j] = f->need[c];        // out_cap
+            so += (f->need[c] + 7) & ~7ull;
+        }
+        e = hipMemcpyAsync(r_in_off, hm.data(), 4ull * k * 8, hipMemcpyHostToDevice, s);
+        int32_t* const u_st = reinterpret_cast<int32_t*>(r_in_off + 5ull * k);
+        if (e == hipSuccess)
+            e = cpk::launch_decode(f->arena, r_in_off, r_in_off + k, k, f->d_frames, r_in_off + 2ull * k,
+                                   r_in_off + 3ull * k, r_in_off + 4ull * k, u_st, true, nullptr, 0, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(frames + fcur, f->d_frames, so, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 4ull * k, r_in_off + 4ull * k, 2ull * k * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "framer decode pass");
+        const int32_t* const us = reinterpret_cast<const int32_t*>(hm.data() + 5ull * k);
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t c = done[j];
+            if (us[j] != CAPNP_PACKED_OK || hm[4ull * k + j] != f->need[c])  // the walk verified the bytes
+                return fail(CAPNP_PACKED_DEVICE_ERROR, "framer: a walked message did not decode to its framed length");
+            frame_off[nf] = fcur + hm[2ull * k + j];
+            frame_len[nf] = f->need[c];
+            frame_conn[nf] = c;
+            ++nf;
+            f->m0[c] += h[5ull * n + c];
+            f->need[c] = f->X[c] = f->W[c] = 0;
+        }
+        fcur += so;
+    }
+    *n_frames = nf;
+    return full ? fail(CAPNP_PACKED_OUT_OF_SPACE, "frames buffer or frame table full: call again to pop the rest")
+                : CAPNP_PACKED_OK;
+}
+
+}  // extern "C"

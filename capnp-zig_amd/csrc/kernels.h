@@ -32,6 +32,16 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                                uint64_t* consumed, int32_t* status, hipStream_t stream);
 
+// Resumable packed framing (capnp_packed_framer_*): batched device byte copies (3 u64 per job:
+// dst, src, len), the header pass of Reader.readPackedMessage (framed length per unit), and the
+// walk of each listed connection's message from its saved position.
+hipError_t launch_copy_jobs(const uint64_t* jobs, uint32_t nj, hipStream_t stream);
+hipError_t launch_read_header(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                              uint64_t* out_len, uint64_t* consumed, int32_t* status, hipStream_t stream);
+hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_t nl, const uint64_t* base,
+                             const uint64_t* avail, const uint64_t* need, uint64_t* X, uint64_t* W,
+                             uint64_t* consumed, int32_t* status, hipStream_t stream);
+
 // MessageBuilder.toPackedBytes from segment lists (message.zig:2123-2179).
 hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_len, const uint32_t* seg_first,
                                  const uint32_t* seg_count, uint32_t n, uint8_t* out, const uint64_t* out_off,

@@ -5048,6 +5048,132 @@ __global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
+// Resumable framing of packed socket streams (capnp_packed_framer_*).
+// Each connection's unconsumed packed bytes stay in a device arena between reads; a read
+// appends only its new bytes, and the walk to the message end resumes where the previous
+// read left it, so a message split over k reads is uploaded once and walked once
+// (framing.zig:42-90 keeps expected_total across pushes; reader.zig:84-156 is one pass).
+// ---------------------------------------------------------------------------
+
+// Batched byte copies (dst, src, len as absolute device addresses, 3 u64 per job): a block per
+// job (grid-stride); lane t stores destination-aligned 16-B chunks from unaligned 16-B loads
+// (gfx950 global loads take any alignment), the two partial edge chunks byte by byte.
+// Jobs never overlap (appends from the staging buffer, region moves into fresh regions).
+__global__ __launch_bounds__(256) void copy_jobs_kernel(const uint64_t* __restrict__ jobs, uint32_t nj) {
+    for (uint32_t j = blockIdx.x; j < nj; j += gridDim.x) {
+        uint8_t* const dst = reinterpret_cast<uint8_t*>(jobs[3 * j]);
+        const uint8_t* const src = reinterpret_cast<const uint8_t*>(jobs[3 * j + 1]);
+        const uint64_t len = jobs[3 * j + 2];
+        if (len == 0) continue;
+        const uint64_t d0 = reinterpret_cast<uint64_t>(dst), d1 = d0 + len;
+        const uint64_t c0 = d0 & ~15ull, c1 = (d1 + 15) & ~15ull;  // 16-B chunks touched
+        for (uint64_t c = c0 + 16ull * threadIdx.x; c < c1; c += 16ull * blockDim.x) {
+            const uint64_t lo = c < d0 ? d0 : c, hi = c + 16 > d1 ? d1 : c + 16;
+            if (lo == c && hi == c + 16) {
+                uint4 v;
+                __builtin_memcpy(&v, src + (c - d0), 16);
+                *reinterpret_cast<uint4*>(c) = v;
+            } else {
+                for (uint64_t b = lo; b < hi; ++b) *reinterpret_cast<uint8_t*>(b) = src[b - d0];
+            }
+        }
+    }
+}
+
+// The walk of a connection's current message (its framed length `need` known from
+// read_header_kernel) from packed byte X, where the previous read left it, over the bytes
+// the connection now holds: window by window (wv_stage / wv_resolve: a wave per connection,
+// 4.6-KB windows resolved in parallel), counting the words of complete records only. It
+// stops at the first record after which the words reach need / 8 (reader.zig:90-93 and
+// 146-153: OK with consumed = that record's end, or InvalidPackedMessage when the record
+// produced more), or at the last complete record the bytes hold (EndOfStream: X and W saved
+// for the next read). base / avail: the message's start in the arena and its bytes.
+__global__ __launch_bounds__(kWvBlock) void frame_walk_kernel(const uint8_t* __restrict__ arena,
+                                                              const uint32_t* __restrict__ list, uint32_t nl,
+                                                              const uint64_t* __restrict__ base,
+                                                              const uint64_t* __restrict__ avail,
+                                                              const uint64_t* __restrict__ need,
+                                                              uint64_t* __restrict__ Xs, uint64_t* __restrict__ Ws,
+                                                              uint64_t* __restrict__ consumed,
+                                                              int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
+    __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const pk = pk_all + wave * kWvPk;
+    uint8_t* const mk = mk_all + wave * kWvWin;
+    for (uint32_t i = blockIdx.x * kWvWaves + wave; i < nl; i += gridDim.x * kWvWaves) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(list[i]);
+        const uint8_t* const src = arena + base[c];
+        const uint64_t P = avail[c];
+        const uint64_t Lw = need[c] >> 3;  // framed words (need is a multiple of 8)
+        uint64_t x = Xs[c], wd = Ws[c];
+        int32_t st = ST_EOS;
+        uint64_t cons = 0;
+        while (x < P) {
+            const WvWin w = wv_stage(pk, mk, src, P, x, lane);
+            uint32_t ent, cs, ce;
+            const uint32_t xw = wv_resolve(pk, mk, w, 0, lane, ent, cs, ce);
+            // the lane's complete records (a record past the held bytes ends the chain)
+            uint32_t words = 0, stop = kEOFX;
+            for (uint32_t r = ent; r < ce;) {
+                uint32_t t = pk[w.sh + r];
+                uint32_t b1 = pk[w.sh + r + 1];
+                uint32_t c9 = pk[w.sh + r + 9];
+                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                const uint32_t len = wv_len(t, c9);
+                if ((uint64_t)r + len > w.rem) {
+                    stop = r;
+                    break;
+                }
+                words += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+                r += len;
+            }
+            const uint32_t incl = wave_incl_sum(words, lane);
+            const uint32_t total = readlane(incl, kWave - 1);
+            if (wd + total >= Lw) {  // the message ends in this window
+                const uint64_t bm = __ballot(wd + incl >= Lw);
+                const uint32_t f = (uint32_t)__builtin_ctzll(bm);
+                uint32_t end = 0, over = 0;
+                if (lane == f) {
+                    uint64_t acc = wd + incl - words;
+                    for (uint32_t r = ent;;) {
+                        const uint32_t t = pk[w.sh + r], b1 = pk[w.sh + r + 1], c9 = pk[w.sh + r + 9];
+                        acc += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+                        r += wv_len(t, c9);
+                        if (acc >= Lw) {
+                            end = r;
+                            over = acc != Lw;
+                            break;
+                        }
+                    }
+                }
+                end = readlane(end, f);
+                over = readlane(over, f);
+                cons = x + end;
+                st = over ? ST_OVERSHOOT : ST_OK;
+                wd = Lw;
+                break;
+            }
+            if (xw == kEOFX) {  // the chain stops at a record the bytes do not hold yet
+                const uint64_t bm = __ballot(stop != kEOFX);
+                x += bm ? readlane(stop, (uint32_t)__builtin_ctzll(bm)) : 0u;
+                wd += total;
+                break;
+            }
+            x += xw;
+            wd += total;
+        }
+        if (lane == 0) {
+            Xs[c] = x;
+            Ws[c] = wd;
+            consumed[c] = cons;
+            status[c] = st;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // synthetic generator and offset scan
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t seed, uint64_t unit, uint64_t word) {
@@ -5682,6 +5808,30 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                                                        out_len, out_cap, status);
     decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
                                                                         out_cap, out_len, status, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_jobs(const uint64_t* jobs, uint32_t nj, hipStream_t stream) {
+    if (nj == 0) return hipSuccess;
+    copy_jobs_kernel<<<std::min(nj, 4096u), 256, 0, stream>>>(jobs, nj);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_header(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
+                              uint64_t* out_len, uint64_t* consumed, int32_t* status, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    read_header_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
+                                                                         status);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_t nl, const uint64_t* base,
+                             const uint64_t* avail, const uint64_t* need, uint64_t* X, uint64_t* W,
+                             uint64_t* consumed, int32_t* status, hipStream_t stream) {
+    if (nl == 0) return hipSuccess;
+    static const uint32_t res = resident_blocks(frame_walk_kernel, kWvBlock, 2);
+    const uint32_t blocks = std::min((nl + kWvWaves - 1) / kWvWaves, res);
+    frame_walk_kernel<<<blocks, kWvBlock, 0, stream>>>(arena, list, nl, base, avail, need, X, W, consumed, status);
     return hipGetLastError();
 }
 

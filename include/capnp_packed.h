@@ -237,6 +237,38 @@ int capnp_packed_frame_connections(const uint8_t* in, uint64_t in_bytes, const u
                                    uint32_t* frame_conn, uint32_t max_frames, uint64_t* consumed, int32_t* status,
                                    uint32_t* n_frames);
 
+/* Resumable framing of packed socket streams: Connection.handleRead
+ * (src/rpc/level2/connection.zig:153-203) over n connections whose Framer state lives on the
+ * device between reads (src/rpc/level0/framing.zig:42-90 keeps expected_total across pushes;
+ * Reader.readPackedMessage, reader.zig:84-156, is one pass). A session keeps each connection's
+ * unconsumed packed bytes in device memory, the current message's framed length once its
+ * header is decoded, and where the walk to its end stopped: a read uploads only its new bytes
+ * and the walk resumes there, so a message split over k reads is uploaded once and walked
+ * once. A session is used by one thread at a time (calls serialise on it). */
+typedef struct capnp_packed_framer capnp_packed_framer;
+int capnp_packed_framer_create(uint32_t n_conns, capnp_packed_framer** out);
+int capnp_packed_framer_destroy(capnp_packed_framer* f);
+/* Append the new reads and pop every whole message. Connection c's new bytes are
+ * in[in_off[c] .. +in_len[c]) of in[0..in_bytes) (in_len[c] = 0: none; in_off / in_len may be
+ * NULL when in_bytes is 0). Frames as capnp_packed_frame_connections: frame i is
+ * frames[frame_off[i] .. +frame_len[i]) of connection frame_conn[i], a connection's frames in
+ * order. status[c] (n entries): END_OF_STREAM (its bytes end inside a message or are used up:
+ * popFrame's null), or the reader's error, after which the connection's bytes are dropped (the
+ * reset handleRead does, connection.zig:175-184; frames popped before it are listed).
+ * OUT_OF_SPACE: `frames` or the frame table filled up; the listed frames are valid and popped,
+ * the other whole messages stay buffered: call again (in_bytes = 0) to pop them. */
+int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
+                             const uint64_t* in_len, uint8_t* frames, uint64_t frames_cap, uint64_t* frame_off,
+                             uint64_t* frame_len, uint32_t* frame_conn, uint32_t max_frames, int32_t* status,
+                             uint32_t* n_frames);
+/* Framer.reset (framing.zig:34-37) of one connection: its buffered bytes and state dropped. */
+int capnp_packed_framer_reset(capnp_packed_framer* f, uint32_t conn);
+/* Framer.bufferedBytes (framing.zig:30-32): packed bytes held for the connection. */
+int capnp_packed_framer_buffered(capnp_packed_framer* f, uint32_t conn, uint64_t* bytes);
+/* Bytes copied host-to-device (every read's bytes once) and moved between device regions since
+ * the session was made (a connection's bytes move when its region doubles). */
+int capnp_packed_framer_stats(capnp_packed_framer* f, uint64_t* uploaded, uint64_t* moved);
+
 /* Single-buffer Reader.readPackedMessage on HOST memory: decodes the message at
  * the front of in[0..n) into out[0..*out_len); *consumed = packed bytes used.
  * On OUT_OF_SPACE, *out_len is the framed length. */

@@ -1,13 +1,10 @@
-"""Host logic of PackedConnections.handle_read, on CPU: the native entry point
-capnp_packed_frame_connections is replaced by a stand-in that follows its header
-contract (include/capnp_packed.h) with the oracle's Reader.readPackedMessage
-(reader.zig:84-156), one unit per live connection per round. What is tested is the
-Python side: the input layout, frames grouped per connection in pop order, the bytes
-left in each framer, errors closing a connection (connection.zig:175-184) with its
-earlier frames in frames_before_error, and the OUT_OF_SPACE retry of the whole call.
-The device path itself is tested in test_gpu_framer.py."""
-import ctypes
-
+"""Host logic of PackedConnections.handle_read and PackedFramer, on CPU: the native
+session (FramerSession over capnp_packed_framer_*) is replaced by a stand-in that follows
+its header contract (include/capnp_packed.h) with the oracle's Reader.readPackedMessage
+(reader.zig:84-156). What is tested is the Python side: frames grouped per connection in pop
+order, errors closing a connection (connection.zig:175-184) with its earlier frames in
+frames_before_error, the bytes each framer keeps, and PackedFramer's pop / error / reset
+order. The device path itself is tested in test_gpu_framer.py."""
 import numpy as np
 import pytest
 
@@ -19,58 +16,38 @@ ORACLE_TO_ABI = {0: cp.OK, -1: cp.END_OF_STREAM, -2: cp.INVALID_SEGMENT_COUNT,
                  -3: cp.SEGMENT_COUNT_LIMIT_EXCEEDED, -6: cp.MESSAGE_TOO_LARGE, -7: cp.INVALID_PACKED_MESSAGE}
 
 
-def _arr(ptr, n, ctype):
-    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctype)), shape=(max(n, 1),))
+class FakeSession:
+    """capnp_packed_framer_* restated on the oracle reader (test stand-in)."""
 
-
-class FakeFramer:
-    """capnp_packed_frame_connections restated on the oracle reader (test stand-in)."""
-
-    def __init__(self, fail_first=0):
+    def __init__(self, n_conns):
+        self.n = n_conns
+        self.buf = [b""] * n_conns
         self.calls = 0
-        self.fail_first = fail_first  # the first calls report OUT_OF_SPACE (frames too small)
 
-    def __call__(self, inp, in_bytes, in_off, in_len, n, slot_guess, frames, frames_cap, f_off, f_len, f_conn,
-                 max_frames, consumed, status, n_frames):
+    def read(self, reads):
         self.calls += 1
-        if self.calls <= self.fail_first:
-            return cp.OUT_OF_SPACE
-        data = bytes(_arr(inp, in_bytes, ctypes.c_uint8)[:in_bytes])
-        off, ln = _arr(in_off, n, ctypes.c_uint64), _arr(in_len, n, ctypes.c_uint64)
-        guess = _arr(slot_guess, n, ctypes.c_uint64)
-        fr = _arr(frames, frames_cap, ctypes.c_uint8)
-        fo, fl = _arr(f_off, max_frames, ctypes.c_uint64), _arr(f_len, max_frames, ctypes.c_uint64)
-        fc = _arr(f_conn, max_frames, ctypes.c_uint32)
-        cons, st = _arr(consumed, n, ctypes.c_uint64), _arr(status, n, ctypes.c_int32)
-        used = [0] * n
-        live = [int(ln[c]) > 0 for c in range(n)]
-        for c in range(n):
-            st[c] = cp.END_OF_STREAM
-        cur = nf = 0
-        while True:
-            idx = [c for c in range(n) if live[c] and used[c] < int(ln[c])]
-            if not idx:
-                break
-            for c in idx:  # one round: the next message of each live connection
-                buf = data[int(off[c]) + used[c]:int(off[c]) + int(ln[c])]
-                rc, framed, u = oracle.read_packed_message(buf, cap=1 << 22)
+        for c, d in reads.items():
+            self.buf[c] += bytes(d)
+        frames, status = {}, np.full(self.n, cp.END_OF_STREAM, dtype=np.int32)
+        for c in range(self.n):
+            while self.buf[c]:
+                rc, framed, used = oracle.read_packed_message(self.buf[c], cap=1 << 22)
                 rc = ORACLE_TO_ABI[rc]
-                if rc == cp.OK:
-                    if cur + len(framed) > frames_cap or nf >= max_frames:
-                        return cp.OUT_OF_SPACE
-                    fr[cur:cur + len(framed)] = np.frombuffer(framed, dtype=np.uint8)
-                    fo[nf], fl[nf], fc[nf] = cur, len(framed), c
-                    nf += 1
-                    cur += (len(framed) + 7) // 8 * 8
-                    used[c] += u
-                    guess[c] = max(8, len(framed))
-                else:
-                    live[c] = False
-                    st[c] = rc
-        for c in range(n):
-            cons[c] = used[c]
-        n_frames._obj.value = nf
-        return cp.OK
+                if rc == cp.END_OF_STREAM:
+                    break
+                if rc != cp.OK:
+                    status[c] = rc
+                    self.buf[c] = b""  # the session drops a failed connection's bytes
+                    break
+                frames.setdefault(c, []).append(memoryview(framed))
+                self.buf[c] = self.buf[c][used:]
+        return frames, status
+
+    def buffered(self, c):
+        return len(self.buf[c])
+
+    def reset(self, c):
+        self.buf[c] = b""
 
 
 def make_stream(rng, n_msgs):
@@ -99,11 +76,9 @@ def oracle_frames(data: bytes):
     return frames, data, cp.OK
 
 
-@pytest.mark.parametrize("fail_first", [0, 2])
-def test_handle_read_host_logic(monkeypatch, fail_first):
-    fake = FakeFramer(fail_first)
-    monkeypatch.setattr(cp.lib(), "capnp_packed_frame_connections", fake)
-    rng = np.random.default_rng(0x5EED + fail_first)
+def test_handle_read_host_logic(monkeypatch):
+    monkeypatch.setattr(cp, "FramerSession", FakeSession)
+    rng = np.random.default_rng(0x5EED)
     n_conns = 23
     bad = bytes([0x03, 0x57, 0x02])  # segment count 600 > 512
     streams, expect = [], []
@@ -133,7 +108,33 @@ def test_handle_read_host_logic(monkeypatch, fail_first):
         frames, rest, rc = expect[c]
         assert [bytes(f) for f in delivered[c]] == frames, f"connection {c}"
         if rc in (cp.OK, cp.END_OF_STREAM):
-            assert c not in errors and bytes(conns.framers[c].buffer) == (rest if rc else b"")
+            assert c not in errors and conns.framers[c].buffered_bytes() == (len(rest) if rc else 0)
         else:
             assert errors[c].status == rc and conns.closed[c] and conns.framers[c].buffered_bytes() == 0
-    assert fake.calls >= 3 + fail_first
+    assert conns.session.calls == 3
+
+
+def test_packed_framer_host_logic(monkeypatch):
+    """PackedFramer over the session: frames in push order, None while a message is
+    incomplete (bytes kept), the reader's error after the frames before it, reset."""
+    monkeypatch.setattr(cp, "FramerSession", FakeSession)
+    rng = np.random.default_rng(0xF00D)
+    packed = make_stream(rng, 5)
+    msgs = [oracle.read_packed_message(p, cap=1 << 22)[1] for p in packed]
+    f = cp.PackedFramer()
+    stream = b"".join(packed)
+    got = []
+    for i in range(0, len(stream), 37):
+        f.push(stream[i:i + 37])
+        while (fr := f.pop_frame()) is not None:
+            got.append(fr)
+    assert got == msgs and f.buffered_bytes() == 0
+    f.push(packed[0][:-1])
+    assert f.pop_frame() is None and f.buffered_bytes() == len(packed[0]) - 1
+    f.push(packed[0][-1:] + packed[1] + bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF]))
+    assert f.pop_frame() == msgs[0] and f.pop_frame() == msgs[1]
+    with pytest.raises(cp.PackedError) as e:
+        f.pop_frame()
+    assert e.value.status == cp.INVALID_SEGMENT_COUNT
+    f.reset()
+    assert f.buffered_bytes() == 0 and f.pop_frame() is None
