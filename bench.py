@@ -70,6 +70,7 @@ def parse():
     ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
     ap.add_argument("--no-validate", action="store_true", help="skip the Message.validate leg")
     ap.add_argument("--only", default="", help=argparse.SUPPRESS)  # dev: run one side leg (validate, c5, ...)
+    ap.add_argument("--decoder", default="", help=argparse.SUPPRESS)  # dev: capnp_packed_set_decoder name
     return ap.parse_args()
 
 
@@ -503,6 +504,49 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
             "note": "host buffers in and out (PCIe + host-side framing), rounds of read_message_batch"}
 
 
+def framer_split_leg(args, dev, read_bytes=65536, sizes_words=(1 << 17, 1 << 19, 1 << 21, 1 << 23)):
+    """Verdict r3 item 2, RPC framing of packed messages that span socket reads: one
+    connection receives one message of 1, 4, 16 and 64 MiB framed (the last is the 8 Mi-word
+    limit, framing.zig:5) in 64 KiB reads (connection.zig:68's read size) through
+    PackedConnections (the device-resident FramerSession). Time from the first
+    read to the popped frame, host buffers in and out; bytes uploaded against the stream.
+    Linear when ms per MiB stays flat as the message grows."""
+    rows = []
+    for words in sizes_words:
+        fb = 8 * words
+        d_fr = cp.generate(1, fb, seed=0xC0DE000B, zero_thresh=args.zero_thresh, device=dev)
+        d_fr[:8] = torch.tensor(list(struct.pack("<II", 0, words - 1)), dtype=torch.uint8, device=dev)
+        off, ln = cp.uniform_layout(1, fb, device=dev)
+        slot = cp.encode_bound(fb)
+        pk_off, pk_cap = cp.uniform_layout(1, slot, device=dev)
+        d_pk = torch.zeros(slot, dtype=torch.uint8, device=dev)
+        plen = torch.zeros(1, dtype=torch.int64, device=dev)
+        pst = torch.zeros(1, dtype=torch.int32, device=dev)
+        cp.encode_batch(d_fr, off, ln, d_pk, pk_off, pk_cap, plen, pst)
+        torch.cuda.synchronize()
+        stream = d_pk[:int(plen.item())].cpu().numpy().tobytes()
+        reads = [stream[i:i + read_bytes] for i in range(0, len(stream), read_bytes)]
+        pc = cp.PackedConnections(1, device=dev)
+        frames = []
+        t0 = time.perf_counter()
+        for piece in reads:
+            res = pc.handle_read({0: piece})
+            frames += res.get(0, []) if isinstance(res.get(0), list) else [res.get(0)]
+        dt = time.perf_counter() - t0
+        ok = len(frames) == 1 and isinstance(frames[0], memoryview) and bytes(frames[0]) == d_fr.cpu().numpy().tobytes()
+        st = pc.session.stats()
+        rows.append({"framed_MiB": fb / 2 ** 20, "packed_bytes": len(stream), "reads": len(reads),
+                     "ms": round(dt * 1e3, 2), "ms_per_MiB": round(dt * 1e3 / (fb / 2 ** 20), 3),
+                     "framed_GiB_s": round(fb / dt / 2 ** 30, 3),
+                     "uploaded_over_stream": round(st["uploaded_bytes"] / len(stream), 4),
+                     "moved_over_stream": round(st["moved_bytes"] / len(stream), 4), "bit_exact": bool(ok)})
+        del d_fr, d_pk
+        torch.cuda.empty_cache()
+    return {"read_bytes": read_bytes, "rows": rows,
+            "note": "one message per connection in 64 KiB reads, host buffers in and out; the walk resumes "
+                    "across reads (capnp_packed_framer_*), so ms_per_MiB flat = linear"}
+
+
 def message_leg(args, dev, reps=10, segs=4, seg_words=127):
     """SURVEY §8(f) row 2, framing fused with the codec: 1M messages of 4 segments x
     127 words (framed 4088 B) from a segment pool, packed straight from the segment
@@ -815,9 +859,11 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
+    if args.decoder:
+        cp.set_decoder(args.decoder)
     if args.only:
         legs = {"validate": validate_leg, "c5": skewed_leg, "dense": dense_leg, "read_message": read_message_leg,
-                "framing": message_leg, "rpc_framer": framer_leg}
+                "framing": message_leg, "rpc_framer": framer_leg, "rpc_framer_split": framer_split_leg}
         print(json.dumps({args.only: legs[args.only](args, dev)}), flush=True)
         return
     n, ub = args.units, args.unit_bytes
@@ -862,6 +908,8 @@ def main():
         if not args.no_read_message:
             torch.cuda.empty_cache()
             extra["rpc_framer"] = framer_leg(args, dev)
+            torch.cuda.empty_cache()
+            extra["rpc_framer_split"] = framer_split_leg(args, dev)
         if not args.no_validate:
             torch.cuda.empty_cache()
             extra["validate"] = validate_leg(args, dev)

@@ -772,9 +772,9 @@ __device__ __forceinline__ bool encode_tiled_unit(const uint8_t* in, uint64_t of
 // long_tiles_kernel / long_windows_kernel turn them into the tile / window tables (huge
 // units first) and the serial list of units the table could not hold.
 constexpr uint64_t kQHuge = 65536;
-constexpr uint32_t kQHead = 16;
+constexpr uint32_t kQHead = 32;
 constexpr uint32_t kClassBlock = 1024;  // units per class-kernel block
-constexpr uint32_t kClassK = 8;         // per-block class counters (7 classes used)
+constexpr uint32_t kClassK = 12;        // per-block class counters (11 classes used)
 __host__ __device__ inline uint64_t class_blocks(uint64_t n) { return (n + kClassBlock - 1) / kClassBlock; }
 // u32 index of the serial list (long units no tile / window table could hold)
 __host__ __device__ inline uint64_t serial_off(uint64_t n) { return kQHead + 3 * n + kClassK * class_blocks(n); }
@@ -3104,15 +3104,19 @@ __global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const ui
 // batch order, and no atomic is contended.
 // decode mid units are binned by packed length (CL_MID + 0..3: <= 1280, <= 2048, <= 3072,
 // more bytes), so the lanes of an index-pass wave walk units of similar length in lockstep;
-// the mid list is the bins in order (batch order within a bin)
-enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3, CL_MID_BINS = 4 };
+// the mid list is the bins in order (batch order within a bin). The streaming decoder
+// (KIND 3) takes small and mid units together: 8 bins (<= 64, 128, 256, 512, 1280, 2048,
+// 3072, more packed bytes), so a wave's 64 lanes walk units of about as many 64-B rounds.
+enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3, CL_MID_BINS = 8 };
 constexpr uint64_t kSmEncWords = 64;  // encode: units of at most 64 words are small
 constexpr uint64_t kSmDecP = 512;     // decode: small = at most 512 packed bytes ...
 constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
 
 __device__ __forceinline__ uint32_t* q_blocks(uint32_t* q, uint32_t n) { return q + kQHead + 3ull * n; }
 
-template <int KIND>  // 0: encode, 1: decode, 2: decoded size (no output: long by packed length alone)
+// KIND 0: encode, 1: decode (small lane kernel + indexed / fused mid decoders), 2: decoded size
+// (no output: long by packed length alone), 3: decode by the streaming decoder (no small class)
+template <int KIND>
 __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
                                                uint32_t u) {
@@ -3128,6 +3132,11 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
         return (!valid || (len >> 3) <= kSmEncWords) ? CL_SMALL : CL_MID;
     }
     const uint64_t cap = out_cap[u];
+    if (KIND == 3) {
+        if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
+        return CL_MID + (len > 64) + (len > 128) + (len > 256) + (len > 512) + (len > 1280) + (len > 2048) +
+               (len > 3072);
+    }
     if (len <= kSmDecP && cap <= kSmDecCap) return CL_SMALL;
     if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
     return CL_MID + (len > 1280) + (len > 2048) + (len > 3072);
@@ -5685,10 +5694,17 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const double sm_frac = mid_stream ? 0.85 : 1.0;  // share of the resident grid
     const uint32_t sm_cap = std::max(1u, (uint32_t)(sm_res * sm_frac));
     const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_cap);
+    // the streaming decoder may leave a failed unit's prefix: all-or-nothing takes the two-pass one
+    const int dv = (decoder_variant() == CAPNP_PACKED_DECODER_STREAM && small_variant() == 0)
+                       ? (int)CAPNP_PACKED_DECODER_TWO_PASS : decoder_variant();
+    const bool streaming = dv == CAPNP_PACKED_DECODER_STREAM;
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-    launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    if (streaming)  // small and mid units in one list, binned by packed length
+        launch_classes<3>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    else
+        launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
     // long units, window-parallel (window table) or, if the table is full, serial
@@ -5708,6 +5724,15 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     window_fill_kernel<<<wfill_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, status, q);
     decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status, q);
+    const uint32_t* const mid = q + kQHead + 2ull * n;
+    if (streaming) {  // small and mid units, 64 per wave
+        const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);  // waves past the count exit
+        decode_stream_kernel<<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                          out_cap, out_len, status, mid, q + 4);
+        e = hipGetLastError();
+        const hipError_t j = side.join();
+        return e != hipSuccess ? e : j;
+    }
     // the mid units' passes on a second side stream, before the small kernel (mid_side_stream)
     const hipStream_t ms = mid_stream ? side.stream2() : stream;
     if (!mid_stream) {
@@ -5721,17 +5746,9 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                      out_len, status, q);
         }
     }
-    const uint32_t* const mid = q + kQHead + 2ull * n;
     // mid units: the indexed two-pass decoder (index pass + fill pass), or the fused
     // single-pass decoder when selected (capnp_packed_set_decoder)
-    // the streaming decoder may leave a failed unit's prefix: all-or-nothing takes the two-pass one
-    const int dv = (decoder_variant() == CAPNP_PACKED_DECODER_STREAM && small_variant() == 0)
-                       ? (int)CAPNP_PACKED_DECODER_TWO_PASS : decoder_variant();
-    if (dv == CAPNP_PACKED_DECODER_STREAM) {
-        const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);  // waves past the mid count exit
-        decode_stream_kernel<<<sd_blocks, kDsWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                      out_len, status, mid, q + 4);
-    } else if (dv == CAPNP_PACKED_DECODER_FUSED) {
+    if (dv == CAPNP_PACKED_DECODER_FUSED) {
         static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);
         const uint32_t fu_blocks = std::min((n + kFuWaves - 1) / kFuWaves, fu_res);
         decode_fused_kernel<<<fu_blocks, kFuWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
