@@ -868,9 +868,19 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
 // holds them (word offsets of the segments in LDS).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig:310)
+constexpr uint32_t kMsgPadSegs = 255;  // one-tile pass: offsets 0..count in the 64 rows' pads
 
+// PAD: the word offsets live in the 16-B pads of the tile's 80-B LDS rows (offset s at row
+// s / 4, bytes 64 + 4 (s % 4)), free while the tile is staged: the one-tile pass then needs no
+// LDS beyond encode_kernel's (7 waves per SIMD, not 5), for messages of < 256 segments.
+template <bool PAD>
 struct MsgView {
     const uint32_t* woff;   // LDS: word offset of segment s in the payload, s <= count
+    __device__ __forceinline__ uint32_t wo(uint32_t s) const {
+        return PAD ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(woff) + (s >> 2) * kEncRow + 64 +
+                                                        4 * (s & 3))
+                   : woff[s];
+    }
     const uint64_t* base;   // device address of segment s (LDS copy, or the caller's array)
     uint32_t count;         // segments (>= 1)
     uint32_t hw;            // header words
@@ -879,35 +889,37 @@ struct MsgView {
 // Word q of the framed stream (q < total words). `s` is a segment hint: the segment
 // holding the previous payload word (advanced forward, so a lane's consecutive words
 // cost one search).
-__device__ __forceinline__ uint64_t msg_word(const MsgView& m, uint32_t q, uint32_t& s) {
+template <bool PAD>
+__device__ __forceinline__ uint64_t msg_word(const MsgView<PAD>& m, uint32_t q, uint32_t& s) {
     if (q < m.hw) {  // toBytes 2147-2163: u32 j = count - 1 (j = 0), size_{j-1} (1 <= j <= count), pad
         uint32_t v[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t j = 2 * q + h;
-            v[h] = j == 0 ? m.count - 1 : (j <= m.count ? m.woff[j] - m.woff[j - 1] : 0u);
+            v[h] = j == 0 ? m.count - 1 : (j <= m.count ? m.wo(j) - m.wo(j - 1) : 0u);
         }
         return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
     }
     const uint32_t p = q - m.hw;
-    if (s >= m.count || p < m.woff[s]) {  // (re)search: largest s with woff[s] <= p, non-empty
+    if (s >= m.count || p < m.wo(s)) {  // (re)search: largest s with woff[s] <= p, non-empty
         uint32_t lo = 0, hi = m.count;  // woff[lo] <= p < woff[hi]
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (m.woff[mid] <= p) lo = mid;
+            if (m.wo(mid) <= p) lo = mid;
             else hi = mid;
         }
         s = lo;
     }
-    while (p >= m.woff[s + 1]) ++s;  // skip to the segment holding p (empty ones included)
-    return *reinterpret_cast<const uint64_t*>(m.base[s] + 8ull * (p - m.woff[s]));
+    while (p >= m.wo(s + 1)) ++s;  // skip to the segment holding p (empty ones included)
+    return *reinterpret_cast<const uint64_t*>(m.base[s] + 8ull * (p - m.wo(s)));
 }
 
 // Stage framed words [tb, tb + tw) (tw <= 512) into the row layout. Lane l gathers
 // words tb + l + 64j: consecutive lanes read consecutive words (coalesced within a
 // segment), and all 8 addresses are formed before any load is issued, so the 8
 // loads are in flight together.
-__device__ __forceinline__ void msg_stage(const MsgView& m, uint32_t tb, uint32_t tw, uint32_t lane, uint32_t& hint,
+template <bool PAD>
+__device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, uint32_t tw, uint32_t lane, uint32_t& hint,
                                           uint8_t* lds) {
     const uint64_t* src[8];
     uint64_t hv[8];
@@ -925,18 +937,18 @@ __device__ __forceinline__ void msg_stage(const MsgView& m, uint32_t tb, uint32_
             } else {
                 const uint32_t p = q - m.hw;
                 if (p < wlo || p >= whi) {  // leave the cached segment window: search, then cache
-                    if (hint >= m.count || p < m.woff[hint]) {
+                    if (hint >= m.count || p < m.wo(hint)) {
                         uint32_t lo = 0, hi = m.count;
                         while (hi - lo > 1) {
                             const uint32_t mid = (lo + hi) >> 1;
-                            if (m.woff[mid] <= p) lo = mid;
+                            if (m.wo(mid) <= p) lo = mid;
                             else hi = mid;
                         }
                         hint = lo;
                     }
-                    while (p >= m.woff[hint + 1]) ++hint;
-                    wlo = m.woff[hint];
-                    whi = m.woff[hint + 1];
+                    while (p >= m.wo(hint + 1)) ++hint;
+                    wlo = m.wo(hint);
+                    whi = m.wo(hint + 1);
                     wbase = m.base[hint];
                 }
                 src[j] = reinterpret_cast<const uint64_t*>(wbase + 8ull * (p - wlo));
@@ -973,6 +985,15 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
         if (lane == 0) { out_len[msg] = 0; status[msg] = ST_ARG; }
         return;
     }
+    if (!TILED && count > kMsgPadSegs) {  // more offsets than the row pads hold: the tiled pass
+        if (lane == 0) status[msg] = kStNeedFull;
+        return;
+    }
+    // !TILED: the offsets go to the row pads of the tile slice (MsgView<true>)
+    auto wput = [&](uint32_t s, uint32_t v) {
+        if (TILED) woff[s] = v;
+        else *reinterpret_cast<uint32_t*>(lds + (s >> 2) * kEncRow + 64 + 4 * (s & 3)) = v;
+    };
     uint32_t wsum = 0;
     bool bad = false;
     uint32_t wl[8];
@@ -998,11 +1019,11 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         const uint32_t s = 8 * lane + t;
-        if (s < count) woff[s] = acc;
+        if (s < count) wput(s, acc);
         acc += wl[t];
     }
     const uint32_t payload = readlane(incl, 63);
-    if (lane == 63) woff[count] = payload;
+    if (lane == 63) wput(count, payload);
     const uint32_t hw = (1 + count + ((count & 1) ? 0 : 1)) / 2;  // toBytes 2135-2137, in words
     const uint64_t words64 = (uint64_t)hw + payload;
     if (__builtin_amdgcn_ballot_w64(bad) != 0 || words64 > 0xFFFFF000ull) {
@@ -1015,7 +1036,8 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
         return;
     }
     wave_lds_sync();
-    const MsgView m{woff, TILED ? base : (c_in ? seg_ptr + first : nullptr), count, hw};
+    const MsgView<!TILED> m{TILED ? woff : reinterpret_cast<const uint32_t*>(lds),
+                            TILED ? base : (c_in ? seg_ptr + first : nullptr), count, hw};
     uint64_t ob = 0, cap = 0;
     if (WRITE) {
         ob = out_off[msg];
@@ -1092,7 +1114,7 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
                                                                 uint64_t* __restrict__ out_len,
                                                                 int32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint32_t woff_all[kWavesPerBlock * (kMsgMaxSegs + 1)];
+    __shared__ uint32_t woff_all[TILED ? kWavesPerBlock * (kMsgMaxSegs + 1) : 1];
     __shared__ uint64_t base_all[TILED ? kWavesPerBlock * kMsgMaxSegs : 1];
     __shared__ uint64_t lut[256];
     const uint32_t lane = lane_id();

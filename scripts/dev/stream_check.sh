@@ -15,8 +15,8 @@ step() {  # name, then the command; stops the script on a crash / time limit
   if [ $rc -ge 124 ]; then exit $rc; fi
   return 0
 }
-step parity timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_decode_contract.py -x -q \
-  --timeout 120 --timeout-method thread -k "stream" > $O/pytest.log 2>&1
+step parity timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_decode_contract.py tests/test_gpu_configs.py -x -q \
+  --timeout 120 --timeout-method thread -k "stream or encode_message" > $O/pytest.log 2>&1
 tail -3 $O/pytest.log
 for t in ${THRS:-128 26 230}; do
   for d in stream twopass stream twopass; do
