@@ -3770,9 +3770,6 @@ __global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __
 // work.
 constexpr uint32_t kSmBlock = 256;
 enum : uint32_t { SM_IDLE, SM_EXIT, SM_META, SM_FIRST, SM_RUN };
-#ifndef CPK_ES_STAGE
-#define CPK_ES_STAGE 0
-#endif
 
 // Zig encoder rules (message.zig:200-271) as a word-at-a-time state machine, one word per
 // step on every lane with a predicated body (no per-word branches): a zero run (00 n-1) is
@@ -3793,20 +3790,9 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
         lut[threadIdx.x] = compact_selector(threadIdx.x);
         __syncthreads();
     }
-    // CPK_ES_STAGE (opt-in build, off by default): each lane stages its output chunks in LDS by
-    // absolutely aligned 64-B windows; a window that lies inside the slot is stored by a quad of
-    // the wave after the word step that completes it, 16 windows per store instruction. Bit-exact;
-    // C5 writes 235 -> 159 MB per launch, but 96 VGPRs (5 waves/SIMD instead of 6) and C5
-    // encode 0.630-0.637 -> 0.638-0.642 ms, same box.
-    constexpr bool STG = WRITE && CPK_ES_STAGE;
-    __shared__ __attribute__((aligned(16))) u32x4 estage_all[STG ? kSmBlock * 4 : 1];
-    __shared__ __attribute__((aligned(16))) uint64_t etab_all[STG ? (kSmBlock / kWave) * 32 : 1];
-    u32x4* const estage = estage_all + (STG ? threadIdx.x * 4 : 0);
-    uint64_t* const etab = etab_all + (STG ? (threadIdx.x >> 6) * 32 : 0);
-    int64_t st_hi = 0;  // one past the last staged chunk
-    uint32_t a0 = 0;    // the slot base's chunk position in its 64-B window
-    bool rdy = false;   // a complete window waits for the wave's store
-    uint8_t* rdst = nullptr;
+    // (Round 3 measured a variant staging each lane's output by 64-B windows in LDS for quad
+    // stores: 235 -> 159 MB written per C5 launch, but 96 VGPRs and C5 encode 0.630-0.637 ->
+    // 0.638-0.642 ms; removed in round 4)
     const uint32_t count = q[3];
     const uint32_t* const list = q + kQHead + n;
     const uint32_t lane = lane_id();
@@ -3849,33 +3835,6 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
             store_partial16(db + cs, (uint32_t)(a - cs), (uint32_t)(e - cs), x0, x1);
         }
     };
-    // the staged chunks of chunk ce's window up to ce, stored by this lane (clipped to the slot)
-    auto lane_flush = [&](int64_t ce) {
-        const int64_t wsx = ce - (int64_t)((ce + a0) & 3);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const int64_t cc = wsx + j;
-            if (cc >= 0 && cc <= ce) {
-                const u32x4 v = estage[(cc + a0) & 3];
-                flush((uint64_t)cc, (uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32), 0, 16);
-            }
-        }
-    };
-    auto stage_chunk = [&](uint64_t c, uint64_t x0, uint64_t x1) {
-        const uint32_t j = (uint32_t)(c + a0) & 3;
-        estage[j] = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
-        st_hi = (int64_t)c + 1;
-        if (j == 3) {
-            const int64_t ws = (int64_t)c - 3;
-            const uint64_t lim = cap > ~0ull - 16 ? ~0ull : da + cap;
-            if (ws >= (da ? 1 : 0) && 16 * (c + 1) <= lim) {
-                rdy = true;
-                rdst = db + 16 * ws;
-            } else {
-                lane_flush((int64_t)c);
-            }
-        }
-    };
     // a step appends <= 12 bytes, so it completes at most one chunk: kept here, written
     // once at the end of the step
     uint64_t f0 = 0, f1 = 0, fch = 0;
@@ -3915,9 +3874,6 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
         } else if (fpend && (x >> 4) == fch) {
             f0 |= m0;
             f1 |= m1;
-        } else if (STG && (int64_t)(x >> 4) < st_hi && (((x >> 4) + a0) >> 2) == (((uint64_t)(st_hi - 1) + a0) >> 2) &&
-                   (((uint64_t)st_hi + a0) & 3) != 0) {
-            reinterpret_cast<uint8_t*>(estage)[(((x >> 4) + a0) & 3) * 16 + (x & 15)] = (uint8_t)c;  // still staged
         } else if (cpos < cap) {
             db[x] = (uint8_t)c;
         }
@@ -3940,36 +3896,10 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
         mode = (cz || nz) ? 1u : ((cf || nf) ? 2u : (valid ? 0u : mode));
         run = (cz || cf) ? run + 1 : ((nz || nf) ? 1u : run);
         if (WRITE && fpend) {
-            if (STG) stage_chunk(fch, f0, f1);
-            else flush(fch, f0, f1, 0, 16);
+            flush(fch, f0, f1, 0, 16);
             fpend = false;
         }
     };
-    // the wave stores the windows completed in this step: quad i takes the i-th ready lane's
-    auto wave_store = [&]() {
-        if (!STG) return;
-        const uint64_t rm = __ballot(rdy);
-        if (rm == 0) return;
-        const uint32_t nr = (uint32_t)__popcll(rm);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u));
-        const uint32_t wbase_t = threadIdx.x & ~(kWave - 1);
-        for (uint32_t g = 0; g < nr; g += 16) {
-            wave_lds_sync();
-            if (rdy && rank >= g && rank < g + 16) {
-                etab[2 * (rank - g)] = reinterpret_cast<uint64_t>(rdst);
-                etab[2 * (rank - g) + 1] = lane;
-            }
-            wave_lds_sync();
-            const uint32_t qd = lane >> 2, qi = lane & 3;
-            if (g + qd < nr) {
-                uint8_t* const cd = reinterpret_cast<uint8_t*>(etab[2 * qd]);
-                const uint32_t sl = (uint32_t)etab[2 * qd + 1];
-                *reinterpret_cast<u32x4*>(cd + 16 * qi) = estage_all[(wbase_t + sl) * 4 + qi];
-            }
-        }
-        rdy = false;
-    };
-
     for (;;) {
         const uint64_t idle = __ballot(kind == SM_IDLE);
         if (idle) {
@@ -4025,8 +3955,6 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
                 cap = m_cap;
                 op = 0;
                 b0 = b1 = 0;
-                a0 = (uint32_t)(reinterpret_cast<uintptr_t>(db) >> 4) & 3;
-                st_hi = 0;
                 mode = 0;
                 cj = 0;
                 kind = SM_FIRST;
@@ -4041,7 +3969,6 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
                 const uint4 c = t < 2 ? c0 : c1;
                 const uint64_t w = (t & 1) ? ((uint64_t)c.z | ((uint64_t)c.w << 32)) : ((uint64_t)c.x | ((uint64_t)c.y << 32));
                 step(w, run_now && w0 + t >= s8 && w0 + t < nw);
-                wave_store();
             }
             if (run_now) {
                 if (cj + 1 < nch) {
@@ -4051,16 +3978,6 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
                 } else {
                     app(mode == 1, (uint64_t)(run - 1) << 8, 2);  // the unit ends inside a run
                     patch(mode == 2, run - 1);
-                    if (STG) {  // the staged chunks of the last window (and the pending one)
-                        bool fl = st_hi > 0 && (((uint64_t)st_hi + a0) & 3) != 0;
-                        if (fpend) {
-                            estage[(fch + a0) & 3] = u32x4{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
-                            st_hi = (int64_t)fch + 1;
-                            fpend = false;
-                            fl = true;
-                        }
-                        if (fl) lane_flush(st_hi - 1);
-                    }
                     if (WRITE && fpend) {
                         flush(fch, f0, f1, 0, 16);
                         fpend = false;

@@ -33,3 +33,5 @@ step framer timeout -k 10 600 python3 -u -m pytest tests/test_gpu_framer.py -x -
 tail -3 $O/pytest_framer.log
 step split timeout -k 10 300 python3 bench.py --only rpc_framer_split > $O/split.json 2>&1
 tail -1 $O/split.json
+step framing timeout -k 10 300 python3 bench.py --only framing > $O/framing.json 2>&1
+tail -1 $O/framing.json
