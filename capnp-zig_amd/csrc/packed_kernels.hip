@@ -2405,8 +2405,14 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
 // OutOfSpace with the required size), found at the walk's end: a failed unit may hold a
 // prefix of its output in its slot (never a byte past out_cap). Callers that need the slot
 // untouched select the two-pass decoder (capnp_packed_set_all_or_nothing).
-constexpr uint32_t kDsWaves = 4;       // waves per block (one 1-KB selector table per block)
-constexpr uint32_t kDsK = 16;          // walk steps per sub-round = list rows
+#ifndef CPK_DS_WAVES  // dev A/B: waves per block of decode_stream_kernel
+#define CPK_DS_WAVES 4
+#endif
+#ifndef CPK_DS_K  // dev A/B: walk steps per sub-round
+#define CPK_DS_K 16
+#endif
+constexpr uint32_t kDsWaves = CPK_DS_WAVES;  // waves per block (one 1-KB selector table per block)
+constexpr uint32_t kDsK = CPK_DS_K;          // walk steps per sub-round = list rows
 constexpr uint32_t kDsRowE = 66;       // list row stride in u16 entries (132 B: conflict-free rows)
 constexpr uint32_t kDsRing = 80;       // ring bytes per unit
 constexpr uint32_t kDsZJob = 16;       // zero runs with this many extra words or more: a wave fill
@@ -2456,7 +2462,7 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
     const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
     __shared__ uint32_t lut[256];
     __shared__ __attribute__((aligned(16))) uint8_t lds_all[kDsWaves * kDsWave];
-    lut[threadIdx.x] = kExpandLut32.v[threadIdx.x];  // 256 threads
+    for (uint32_t t = threadIdx.x; t < 256; t += kDsWaves * kWave) lut[t] = kExpandLut32.v[t];
     __syncthreads();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* const ring_all = lds_all + wave * kDsWave;                              // 64 x 80 B
@@ -2582,7 +2588,7 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
             const uint32_t nmax = wave_max_u32(lu);
             wave_lds_sync();
             if (nmax > 0) {
-                const uint32_t lg = nmax > 8u ? 4u : nmax > 4u ? 3u : 2u;  // G = 1 << lg
+                const uint32_t lg = nmax > 16u ? 5u : nmax > 8u ? 4u : nmax > 4u ? 3u : 2u;  // G = 1 << lg
                 const uint32_t ii = lane & ((1u << lg) - 1u);
                 const uint32_t per = kWave >> lg;  // units per store instruction
                 for (uint32_t u0 = 0; u0 < (uint32_t)kWave; u0 += per) {
