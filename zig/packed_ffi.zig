@@ -57,6 +57,19 @@ extern "capnp_packed" fn capnp_packed_frame_connections(
     slot_guess: [*]u64, frames: [*]u8, frames_cap: u64, frame_off: [*]u64, frame_len: [*]u64,
     frame_conn: [*]u32, max_frames: u32, consumed: [*]u64, status: [*]i32, n_frames: *u32,
 ) c_int;
+// Resumable framing (capnp_packed_framer_*, include/capnp_packed.h): Framer state of n
+// connections kept on the device between reads (framing.zig:42-90; DESIGN.md §2.7).
+pub const capnp_packed_framer = opaque {};
+pub extern "capnp_packed" fn capnp_packed_framer_create(n_conns: u32, out: *?*capnp_packed_framer) c_int;
+pub extern "capnp_packed" fn capnp_packed_framer_destroy(f: ?*capnp_packed_framer) c_int;
+pub extern "capnp_packed" fn capnp_packed_framer_read(
+    f: *capnp_packed_framer, in: ?[*]const u8, in_bytes: u64, in_off: ?[*]const u64, in_len: ?[*]const u64,
+    frames: [*]u8, frames_cap: u64, frame_off: [*]u64, frame_len: [*]u64, frame_conn: [*]u32,
+    max_frames: u32, status: [*]i32, n_frames: *u32,
+) c_int;
+pub extern "capnp_packed" fn capnp_packed_framer_reset(f: *capnp_packed_framer, conn: u32) c_int;
+pub extern "capnp_packed" fn capnp_packed_framer_buffered(f: *capnp_packed_framer, conn: u32, bytes: *u64) c_int;
+pub extern "capnp_packed" fn capnp_packed_framer_stats(f: *capnp_packed_framer, uploaded: *u64, moved: *u64) c_int;
 
 // ---- device batch entry points (pointers are device memory) ----------------
 pub extern "capnp_packed" fn capnp_packed_encode_batch(
@@ -107,6 +120,8 @@ pub extern "capnp_packed" fn capnp_packed_validate_batch(
 pub extern "capnp_packed" fn capnp_packed_batch_workspace_bytes(n: u32) usize;
 /// Small decode units all-or-nothing too (process-wide); returns the previous setting.
 pub extern "capnp_packed" fn capnp_packed_set_all_or_nothing(on: c_int) c_int;
+pub extern "capnp_packed" fn capnp_packed_set_decoder(decoder: c_int) c_int;
+pub extern "capnp_packed" fn capnp_packed_set_launch_flags(flags: u32) u32;
 /// Free the library's context of a caller stream (before destroying the stream).
 pub extern "capnp_packed" fn capnp_packed_stream_release(stream: ?*anyopaque) c_int;
 pub extern "capnp_packed" fn capnp_packed_encode_batch_ws(
