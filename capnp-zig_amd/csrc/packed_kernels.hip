@@ -2455,6 +2455,19 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_incl_max(v, 0), kWave - 1);
 }
 
+// The streaming decoder's global traffic in inline asm, so hipcc neither turns it into FLAT
+// instructions (pointers that went through __shfl / LDS lose their address space, and FLAT
+// counts on lgkmcnt too: every LDS wait of the walk would wait for the prefetch) nor waits for
+// it itself (its own vmcnt(0) before the ring writes would wait for the previous round's stores).
+// The kernel counts both (vmcnt_at_most63) and pins the loaded registers after its wait
+// (cdna_hip_programming.md §5.7 item 1, form ii).
+__device__ __forceinline__ void ds_gload16_nt(u32x4& d, const void* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(d) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void ds_gstore8_nt(void* p, uint64_t v) {
+    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+}
+
 __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
@@ -2509,12 +2522,12 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
         qlast[m] = rn ? rn - 1 : 0u;
     }
     const uint32_t qp = lane & 3;
-    uint4 d0, d1, d2, d3;
-    auto load = [&](uint32_t k) {
-        d0 = load_nt(qsrc[0] + min(4 * k + qp, qlast[0]));
-        d1 = load_nt(qsrc[1] + min(4 * k + qp, qlast[1]));
-        d2 = load_nt(qsrc[2] + min(4 * k + qp, qlast[2]));
-        d3 = load_nt(qsrc[3] + min(4 * k + qp, qlast[3]));
+    u32x4 d0, d1, d2, d3;
+    auto load = [&](uint32_t k) {  // 4 loads: the next round's blocks (vmcnt counts them first)
+        ds_gload16_nt(d0, qsrc[0] + min(4 * k + qp, qlast[0]));
+        ds_gload16_nt(d1, qsrc[1] + min(4 * k + qp, qlast[1]));
+        ds_gload16_nt(d2, qsrc[2] + min(4 * k + qp, qlast[2]));
+        ds_gload16_nt(d3, qsrc[3] + min(4 * k + qp, qlast[3]));
     };
     uint8_t* const wq = ring_all + (lane / 4) * kDsRing + 16 + 16 * qp;  // unit 16m + l/4: + 16 * kDsRing * m
     uint8_t* const ring = ring_all + lane * kDsRing;
@@ -2526,7 +2539,10 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
     uint32_t younger = 0;               // vector-memory ops issued after the round's loads
     if (maxr > 0) load(0);
     for (uint32_t k = 0; k <= maxr; ++k) {
-        if (k < maxr) vmcnt_at_most63(younger);  // round k's loads have landed
+        if (k < maxr) {
+            vmcnt_at_most63(younger);  // round k's loads have landed
+            asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+        }
         younger = 0;
         if (k > 0) {
             wave_lds_sync();  // every lane is done with round k-1's ring reads
@@ -2534,10 +2550,10 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
             wave_lds_sync();
         }
         if (k < maxr) {
-            *reinterpret_cast<uint4*>(wq) = d0;
-            *reinterpret_cast<uint4*>(wq + 16 * kDsRing) = d1;
-            *reinterpret_cast<uint4*>(wq + 32 * kDsRing) = d2;
-            *reinterpret_cast<uint4*>(wq + 48 * kDsRing) = d3;
+            *reinterpret_cast<u32x4*>(wq) = d0;
+            *reinterpret_cast<u32x4*>(wq + 16 * kDsRing) = d1;
+            *reinterpret_cast<u32x4*>(wq + 32 * kDsRing) = d2;
+            *reinterpret_cast<u32x4*>(wq + 48 * kDsRing) = d3;
             if (k + 1 < maxr) load(k + 1);
             wave_lds_sync();
         }
@@ -2606,10 +2622,9 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
                     const uint32_t a = __builtin_amdgcn_perm(hi, lo, x & 0x0F0F0F0Fu);
                     const uint32_t b = __builtin_amdgcn_perm(hi, lo, (x >> 4) & 0x0F0F0F0Fu);
                     if (__builtin_amdgcn_ballot_w64(ok) != 0) {  // uniform: the store issues
-                        if (ok) {
-                            uint64_t* const p = reinterpret_cast<uint64_t*>((m & 0x00FFFFFFFFFFFFFFull) + 8ull * ii);
-                            __builtin_nontemporal_store((uint64_t)a | ((uint64_t)b << 32), p);
-                        }
+                        if (ok)
+                            ds_gstore8_nt(reinterpret_cast<void*>((m & 0x00FFFFFFFFFFFFFFull) + 8ull * ii),
+                                          (uint64_t)a | ((uint64_t)b << 32));
                         ++younger;
                     }
                 }
@@ -2623,8 +2638,7 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
                 const uint64_t jd = (uint64_t)readlane((uint32_t)reinterpret_cast<uint64_t>(dstb), jl) |
                                     ((uint64_t)readlane((uint32_t)(reinterpret_cast<uint64_t>(dstb) >> 32), jl) << 32);
                 const uint32_t hi = min(jw + jc, jcap);  // jw < jcap (a job is never past the slot)
-                for (uint32_t w = jw + lane; w < hi; w += kWave)
-                    __builtin_nontemporal_store(0ull, reinterpret_cast<uint64_t*>(jd) + w);
+                for (uint32_t w = jw + lane; w < hi; w += kWave) ds_gstore8_nt(reinterpret_cast<uint64_t*>(jd) + w, 0ull);
                 younger += (hi - jw + kWave - 1) / kWave;
             }
             wc += zjob;
