@@ -109,6 +109,23 @@ __device__ __forceinline__ uint4 load_nt(const void* p) {
     return make_uint4(t.x, t.y, t.z, t.w);
 }
 
+// Ring loads / output stores of the lane-per-unit decoders (decode_index_kernel,
+// decode_stream_kernel) in inline asm, so hipcc neither turns them into FLAT instructions
+// (pointers that went through __shfl / LDS lose their address space, and FLAT counts on
+// lgkmcnt too: every LDS wait of the walk would wait for the prefetch) nor waits for them
+// itself (its own vmcnt(0) before the ring writes would also wait for the previous round's
+// stores). The kernels count them (s_waitcnt vmcnt(N)) and pin the loaded registers after
+// the wait (cdna_hip_programming.md §5.7 item 1, form ii).
+__device__ __forceinline__ void ds_gload16(u32x4& d, const void* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void ds_gload16_nt(u32x4& d, const void* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(d) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void ds_gstore8_nt(void* p, uint64_t v) {
+    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+}
+
 // Order LDS traffic between lanes of ONE wave (the wave owns its LDS slice).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1895,12 +1912,12 @@ __global__ __launch_bounds__(kWave * kIxBw) CPK_IX_ATTR void decode_index_kernel
         qlast[m] = rn ? rn - 1 : 0u;
     }
     const uint32_t qp = lane & 3;
-    uint4 d0, d1, d2, d3;
-    auto load = [&](uint32_t k) {
-        d0 = qsrc[0][min(4 * k + qp, qlast[0])];
-        d1 = qsrc[1][min(4 * k + qp, qlast[1])];
-        d2 = qsrc[2][min(4 * k + qp, qlast[2])];
-        d3 = qsrc[3][min(4 * k + qp, qlast[3])];
+    u32x4 d0, d1, d2, d3;
+    auto load = [&](uint32_t k) {  // asm global loads (ds_gload16): counted by the waits below
+        ds_gload16(d0, qsrc[0] + min(4 * k + qp, qlast[0]));
+        ds_gload16(d1, qsrc[1] + min(4 * k + qp, qlast[1]));
+        ds_gload16(d2, qsrc[2] + min(4 * k + qp, qlast[2]));
+        ds_gload16(d3, qsrc[3] + min(4 * k + qp, qlast[3]));
     };
     uint8_t* const wq = ring_all + (lane / 4) * kRing + 16 + 16 * qp;  // unit 16m + l/4: + 16 * kRing * m
     uint8_t* const ring = ring_all + lane * kRing;
@@ -1919,6 +1936,7 @@ __global__ __launch_bounds__(kWave * kIxBw) CPK_IX_ATTR void decode_index_kernel
             // k-1 when it flushed (k-1 = 7 mod 8)
             if (!SIZE_ONLY && (k & 7) == 0 && k > 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
         }
         if (k > 0) {
             wave_lds_sync();  // every lane is done with round k-1's reads
@@ -1928,10 +1946,10 @@ __global__ __launch_bounds__(kWave * kIxBw) CPK_IX_ATTR void decode_index_kernel
             wave_lds_sync();  // before the quad writes below overwrite ring + 64
         }
         if (k < maxr) {
-            *reinterpret_cast<uint4*>(wq) = d0;
-            *reinterpret_cast<uint4*>(wq + 16 * kRing) = d1;
-            *reinterpret_cast<uint4*>(wq + 32 * kRing) = d2;
-            *reinterpret_cast<uint4*>(wq + 48 * kRing) = d3;
+            *reinterpret_cast<u32x4*>(wq) = d0;
+            *reinterpret_cast<u32x4*>(wq + 16 * kRing) = d1;
+            *reinterpret_cast<u32x4*>(wq + 32 * kRing) = d2;
+            *reinterpret_cast<u32x4*>(wq + 48 * kRing) = d3;
             if (k + 1 < maxr) load(k + 1);
             wave_lds_sync();
         }
@@ -2453,19 +2471,6 @@ __device__ __forceinline__ void vmcnt_at_most63(uint32_t c) {
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_incl_max(v, 0), kWave - 1);
-}
-
-// The streaming decoder's global traffic in inline asm, so hipcc neither turns it into FLAT
-// instructions (pointers that went through __shfl / LDS lose their address space, and FLAT
-// counts on lgkmcnt too: every LDS wait of the walk would wait for the prefetch) nor waits for
-// it itself (its own vmcnt(0) before the ring writes would wait for the previous round's stores).
-// The kernel counts both (vmcnt_at_most63) and pins the loaded registers after its wait
-// (cdna_hip_programming.md §5.7 item 1, form ii).
-__device__ __forceinline__ void ds_gload16_nt(u32x4& d, const void* p) {
-    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(d) : "v"(p) : "memory");
-}
-__device__ __forceinline__ void ds_gstore8_nt(void* p, uint64_t v) {
-    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
 }
 
 __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
