@@ -15,3 +15,14 @@ for t in ${THRS:-128 26 230}; do
     done
   done
 done
+# the two-pass decoder: index pass with FLAT prefetch loads (lib_exp/ix_flat.so, the previous
+# commit) against global asm loads (shipped)
+for t in ${THRS:-128 26 230}; do
+  for r in 1 2; do
+    for lib in capnp-zig_amd/lib/libcapnp_packed.so capnp-zig_amd/lib_exp/ix_flat.so; do
+      CPK_LIB=$lib timeout -k 10 120 python3 scripts/microbench.py --reps 9 --zero-thresh $t --only decode,decoded_size --decoder twopass > $O/x.json 2>&1
+      rc=$?; [ $rc -ge 124 ] && exit $rc
+      echo "twopass t=$t lib=$(basename $lib) $(tail -1 $O/x.json)"
+    done
+  done
+done

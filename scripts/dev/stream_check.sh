@@ -35,3 +35,4 @@ step split timeout -k 10 300 python3 bench.py --only rpc_framer_split > $O/split
 tail -1 $O/split.json
 step framing timeout -k 10 300 python3 bench.py --only framing > $O/framing.json 2>&1
 tail -1 $O/framing.json
+step ds_ab bash scripts/dev/ds_ab.sh
