@@ -887,16 +887,25 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
 constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig:310)
 constexpr uint32_t kMsgPadSegs = 255;  // one-tile pass: offsets 0..count in the 64 rows' pads
 
-// PAD: the word offsets live in the 16-B pads of the tile's 80-B LDS rows (offset s at row
+// PAD: the word offsets live in the 16-B pads of the tile's 80-B LDS rows (u32 slot s at row
 // s / 4, bytes 64 + 4 (s % 4)), free while the tile is staged: the one-tile pass then needs no
 // LDS beyond encode_kernel's (7 waves per SIMD, not 5), for messages of < 256 segments.
-template <bool PAD>
+// PAD == 2 (the prefetching one-tile pass, <= 64 segments): the segment addresses live there
+// too, segment s's at u32 slots 128 + 2s, 129 + 2s.
+__device__ __forceinline__ uint8_t* msg_pad(uint8_t* lds, uint32_t slot) {
+    return lds + (slot >> 2) * kEncRow + 64 + 4 * (slot & 3);
+}
+template <int PAD>
 struct MsgView {
     const uint32_t* woff;   // LDS: word offset of segment s in the payload, s <= count
     __device__ __forceinline__ uint32_t wo(uint32_t s) const {
-        return PAD ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(woff) + (s >> 2) * kEncRow + 64 +
-                                                        4 * (s & 3))
+        return PAD ? *reinterpret_cast<const uint32_t*>(msg_pad(const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(woff)), s))
                    : woff[s];
+    }
+    __device__ __forceinline__ uint64_t ba(uint32_t s) const {
+        return PAD == 2 ? *reinterpret_cast<const uint64_t*>(
+                              msg_pad(const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(woff)), 128 + 2 * s))
+                        : base[s];
     }
     const uint64_t* base;   // device address of segment s (LDS copy, or the caller's array)
     uint32_t count;         // segments (>= 1)
@@ -906,7 +915,7 @@ struct MsgView {
 // Word q of the framed stream (q < total words). `s` is a segment hint: the segment
 // holding the previous payload word (advanced forward, so a lane's consecutive words
 // cost one search).
-template <bool PAD>
+template <int PAD>
 __device__ __forceinline__ uint64_t msg_word(const MsgView<PAD>& m, uint32_t q, uint32_t& s) {
     if (q < m.hw) {  // toBytes 2147-2163: u32 j = count - 1 (j = 0), size_{j-1} (1 <= j <= count), pad
         uint32_t v[2];
@@ -928,14 +937,14 @@ __device__ __forceinline__ uint64_t msg_word(const MsgView<PAD>& m, uint32_t q, 
         s = lo;
     }
     while (p >= m.wo(s + 1)) ++s;  // skip to the segment holding p (empty ones included)
-    return *reinterpret_cast<const uint64_t*>(m.base[s] + 8ull * (p - m.wo(s)));
+    return *reinterpret_cast<const uint64_t*>(m.ba(s) + 8ull * (p - m.wo(s)));
 }
 
 // Stage framed words [tb, tb + tw) (tw <= 512) into the row layout. Lane l gathers
 // words tb + l + 64j: consecutive lanes read consecutive words (coalesced within a
 // segment), and all 8 addresses are formed before any load is issued, so the 8
 // loads are in flight together.
-template <bool PAD>
+template <int PAD>
 __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, uint32_t tw, uint32_t lane, uint32_t& hint,
                                           uint8_t* lds) {
     const uint64_t* src[8];
@@ -966,7 +975,7 @@ __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, ui
                     while (p >= m.wo(hint + 1)) ++hint;
                     wlo = m.wo(hint);
                     whi = m.wo(hint + 1);
-                    wbase = m.base[hint];
+                    wbase = m.ba(hint);
                 }
                 src[j] = reinterpret_cast<const uint64_t*>(wbase + 8ull * (p - wlo));
             }
@@ -1053,7 +1062,7 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
         return;
     }
     wave_lds_sync();
-    const MsgView<!TILED> m{TILED ? woff : reinterpret_cast<const uint32_t*>(lds),
+    const MsgView<TILED ? 0 : 1> m{TILED ? woff : reinterpret_cast<const uint32_t*>(lds),
                             TILED ? base : (c_in ? seg_ptr + first : nullptr), count, hw};
     uint64_t ob = 0, cap = 0;
     if (WRITE) {
@@ -1112,6 +1121,117 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
     if (lane == 0) {
         out_len[msg] = pos;
         status[msg] = (WRITE && !fits) ? ST_SPACE : ST_OK;
+    }
+}
+
+// One-tile messages of at most 64 segments with the next message's metadata prefetched
+// (round 4, verdict r3 item 4): a persistent grid, each wave coding messages w, w + G, ...
+// While message i is staged, message i+G's segment count / first index / output slot are in
+// flight; once its words are staged, its segment lengths and addresses (lane l: segment l)
+// are loaded and land while message i is coded. So a message's data loads wait for one level
+// (the segment addresses are in registers, then in the row pads: MsgView<2>) instead of three
+// (message -> segment list -> lengths and addresses -> data). Other messages (more than 64
+// segments, more than 512 framed words, misaligned segments) are left to the tiled pass
+// (kStNeedFull), which also applies the argument checks.
+#ifndef CPK_EM_PF  // dev A/B: 1 = one-tile messages by encode_message_pf_kernel
+#define CPK_EM_PF 0
+#endif
+constexpr bool kEmPf = CPK_EM_PF;
+constexpr uint32_t kMsgPfSegs = 64;
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void encode_message_pf_kernel(const uint64_t* __restrict__ seg_ptr,
+                                                                   const uint64_t* __restrict__ seg_len,
+                                                                   const uint32_t* __restrict__ seg_first,
+                                                                   const uint32_t* __restrict__ seg_count, uint32_t n,
+                                                                   uint8_t* __restrict__ out,
+                                                                   const uint64_t* __restrict__ out_off,
+                                                                   const uint64_t* __restrict__ out_cap,
+                                                                   uint64_t* __restrict__ out_len,
+                                                                   int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
+    __shared__ uint64_t lut[256];
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (WRITE) lut[threadIdx.x] = compact_selector(threadIdx.x);
+    __syncthreads();
+    uint8_t* const lds = smem + wave * kEncLds;
+    const uint32_t G = gridDim.x * kWavesPerBlock;
+    uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
+    if (msg >= n) return;
+    uint32_t h_cin = 0, h_first = 0;  // the prefetched message's header
+    uint64_t h_ob = 0, h_cap = 0;
+    uint64_t s_len = 0, s_ptr = 0;     // its segment lane (lane l: segment l)
+    auto fetch_hdr = [&](uint32_t mm) {
+        if (mm < n) {
+            h_cin = seg_count[mm];
+            h_first = seg_first[mm];
+            if (WRITE) {
+                h_ob = out_off[mm];
+                h_cap = out_cap[mm];
+            }
+        }
+    };
+    auto fetch_segs = [&]() {  // the prefetched message's segments (its header has landed)
+        const uint32_t c = __builtin_amdgcn_readfirstlane(h_cin);
+        const uint32_t f = __builtin_amdgcn_readfirstlane(h_first);
+        s_len = 0;
+        s_ptr = 0;
+        if (c >= 1 && c <= kMsgPfSegs && lane < c) {
+            s_len = seg_len[f + lane];
+            s_ptr = seg_ptr[f + lane];
+        }
+    };
+    auto uni64 = [](uint64_t v) {
+        return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+               ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+    };
+    fetch_hdr(msg);
+    fetch_segs();
+    for (; msg < n; msg += G) {
+        // lane-derived values recomputed per message, not hoisted out of the loop and held
+        // in registers (as encode_message_one's tile loop; the hoisted form spilled)
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t c_in = __builtin_amdgcn_readfirstlane(h_cin);
+        const uint64_t ob = uni64(h_ob), cap = uni64(h_cap);
+        const uint64_t len = s_len, ptr = s_ptr;
+        fetch_hdr(msg + G);  // in flight while this message is staged
+        const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
+        bool done = false;
+        if (count <= kMsgPfSegs) {
+            const bool bad = ln < count && ((len & 7) != 0 || (ptr & 7) != 0 || (len >> 3) > 0xFFFFFFFFull);
+            const uint32_t wl = ln < count ? (uint32_t)(len >> 3) : 0u;
+            const uint32_t incl = wave_incl_sum(wl, ln);
+            const uint64_t words64 = (uint64_t)(1 + count + ((count & 1) ? 0 : 1)) / 2 + readlane(incl, 63);
+            if (__builtin_amdgcn_ballot_w64(bad) == 0 && words64 <= kEncMaxWords) {
+                const uint32_t words = (uint32_t)words64;
+                wave_lds_sync();  // the previous message's write-back read the slice
+                if (ln < count) {
+                    *reinterpret_cast<uint32_t*>(msg_pad(lds, ln)) = incl - wl;
+                    *reinterpret_cast<uint64_t*>(msg_pad(lds, 128 + 2 * ln)) = ptr;
+                }
+                if (ln == 63) *reinterpret_cast<uint32_t*>(msg_pad(lds, count)) = incl;  // woff[count] = payload
+                wave_lds_sync();
+                const MsgView<2> m{reinterpret_cast<const uint32_t*>(lds), nullptr, count,
+                                   (1 + count + ((count & 1) ? 0 : 1)) / 2};
+                uint32_t hint = 0xFFFFFFFFu;
+                msg_stage(m, 0, words, ln, hint, lds);
+                fetch_segs();  // the next message's segments land while this one is coded
+                wave_lds_sync();
+                uint32_t cz = 0, cf = 0;
+                const uint32_t P = encode_tile<WRITE, true>(lds, lut, ln, words, 0, cz, cf, words, words, out + ob,
+                                                            cap);
+                if (ln == 0) {
+                    out_len[msg] = P;
+                    status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
+                }
+                done = true;
+            }
+        }
+        if (!done) {
+            if (ln == 0) status[msg] = kStNeedFull;  // the tiled pass: long, many segments, or its checks
+            fetch_segs();
+        }
     }
 }
 
@@ -6006,14 +6126,26 @@ hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_le
     if (n == 0) return hipSuccess;
     // every message, then the marked multi-tile ones (a grid striding over the statuses)
     const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
+    if (kEmPf) {  // one-tile messages by the prefetching persistent pass (encode_message_pf_kernel)
+        static const uint32_t pf_res = resident_blocks(encode_message_pf_kernel<true>, kBlock, 7);
+        const uint32_t pf_blocks = std::min(blocks_for(n), pf_res);
+        if (write)
+            encode_message_pf_kernel<true><<<pf_blocks, kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count, n,
+                                                                             out, out_off, out_cap, out_len, status);
+        else
+            encode_message_pf_kernel<false><<<pf_blocks, kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count,
+                                                                              n, out, out_off, out_cap, out_len, status);
+    }
     if (write) {
-        encode_message_kernel<true, false><<<blocks_for(n), kBlock, 0, stream>>>(
-            seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
+        if (!kEmPf)
+            encode_message_kernel<true, false><<<blocks_for(n), kBlock, 0, stream>>>(
+                seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
         encode_message_kernel<true, true><<<tiled_blocks, kBlock, 0, stream>>>(
             seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
     } else {
-        encode_message_kernel<false, false><<<blocks_for(n), kBlock, 0, stream>>>(
-            seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
+        if (!kEmPf)
+            encode_message_kernel<false, false><<<blocks_for(n), kBlock, 0, stream>>>(
+                seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
         encode_message_kernel<false, true><<<tiled_blocks, kBlock, 0, stream>>>(
             seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
     }

@@ -15,6 +15,14 @@ step() {  # name, then the command; stops the script on a crash / time limit
 }
 step framing timeout -k 10 300 python3 bench.py --only framing > $O/framing.json 2>&1
 tail -1 $O/framing.json
+# the prefetching one-tile message encode (lib_exp/em_pf.so: -DCPK_EM_PF=1): its tests, then A/B
+step em_tests env CPK_LIB=capnp-zig_amd/lib_exp/em_pf.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_configs.py \
+  -x -q --timeout 200 --timeout-method thread -k "encode_message" > $O/pytest_em.log 2>&1
+tail -3 $O/pytest_em.log
+for lib in capnp-zig_amd/lib_exp/em_pf.so capnp-zig_amd/lib/libcapnp_packed.so capnp-zig_amd/lib_exp/em_pf.so; do
+  step framing_ab env CPK_LIB=$lib timeout -k 10 300 python3 bench.py --only framing > $O/framing_ab.json 2>&1
+  echo "framing lib=$(basename $lib) $(tail -1 $O/framing_ab.json)"
+done
 # the streaming small-unit encoder (lib_exp/es_stream.so: -DCPK_ES_STREAM=1): encode tests, C5 timings
 step es_tests env CPK_LIB=capnp-zig_amd/lib_exp/es_stream.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_small_units.py \
   tests/test_gpu_configs.py tests/test_gpu_stress.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread \
