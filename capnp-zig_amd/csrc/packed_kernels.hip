@@ -2716,10 +2716,10 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
                 const bool bulk = zr && wn >= capw;             // past the slot: counted only
                 const bool job = zr && !bulk && b1 >= kDsZJob;
                 zrem = inz ? zrem - 1u : ((zr && !bulk && !job) ? b1 : 0u);
-                zjob = job ? b1 : 0u;
+                zjob = job ? b1 : zjob;  // a lane waiting on its job keeps it (and its state)
                 wc = wn + (bulk ? b1 : 0u);
                 lit_end = (rec && f) ? lend : lit_end;
-                pos = eof ? kDsDead : (inz ? pos : pos + len);
+                pos = eof ? kDsDead : ((act && !inz) ? pos + len : pos);  // idle lanes stay put
                 st = eof ? ST_EOF : st;
                 nent = em ? i + 1u : nent;
             }
