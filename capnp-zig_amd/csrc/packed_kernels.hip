@@ -71,6 +71,7 @@ enum : int32_t {
     ST_EOF = CAPNP_PACKED_UNEXPECTED_EOF,
     ST_SPACE = CAPNP_PACKED_OUT_OF_SPACE,
     ST_ARG = CAPNP_PACKED_INVALID_ARGUMENT,
+    ST_DEVERR = CAPNP_PACKED_DEVICE_ERROR,  // a kernel's own loop guard tripped (never expected)
     // Reader.readPackedMessage (reader.zig:84-156)
     ST_EOS = CAPNP_PACKED_END_OF_STREAM,
     ST_SEGCOUNT = CAPNP_PACKED_INVALID_SEGMENT_COUNT,
@@ -2555,6 +2556,7 @@ constexpr uint32_t kDsRowE = 66;       // list row stride in u16 entries (132 B:
 constexpr uint32_t kDsRing = 80;       // ring bytes per unit
 constexpr uint32_t kDsZJob = 16;       // zero runs with this many extra words or more: a wave fill
 constexpr uint32_t kDsDead = 0xFFFFFFF0u;  // walk position of a lane with nothing (more) to walk
+constexpr uint32_t kDsGuard = 1024;        // sub-rounds per round before a wave gives up
 constexpr uint32_t kDsWave = kWave * kDsRing + kDsK * kDsRowE * 2 + kWave * 8;  // LDS bytes per wave
 
 // Expand selectors packed 4 bits per byte: byte k = sel[k] | sel[k + 4] << 4 (sel values are
@@ -2684,7 +2686,16 @@ __global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
         }
         const uint32_t ob = 64 * k;              // ring offset o = pos + 16 - ob in [0, 64)
         const uint32_t lim = min(ob + 48, end);  // records / literal words starting before lim
-        for (;;) {  // sub-rounds
+        // A lane emits at most ~70 sub-rounds' words per round (32 records of <= 16 listed
+        // words, or zero-run jobs); the guard only turns a defect into DEVICE_ERROR, not a hang.
+        for (uint32_t guard = 0;; ++guard) {  // sub-rounds
+            if (guard == kDsGuard) {
+                const bool live = zrem != 0u || pos < lim;
+                st = live ? ST_DEVERR : st;
+                pos = live ? kDsDead : pos;
+                zrem = 0;
+                break;
+            }
             // ---- walk: up to kDsK steps, one output word per active lane per step ------
             const uint32_t w0 = wc;  // the unit's word index of list row 0
             uint32_t nent = 0;       // entries listed this sub-round
