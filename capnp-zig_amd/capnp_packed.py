@@ -215,6 +215,7 @@ SIGNATURES = {
                                                 _vp, ctypes.c_uint32, _vp, ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_framer_reset": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "capnp_packed_framer_buffered": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
+    "capnp_packed_framer_expected": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "capnp_packed_framer_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64),
                                                  ctypes.POINTER(ctypes.c_uint64)]),
 }
@@ -531,9 +532,9 @@ class FramerSession:
             f_conn = np.empty(max_frames, dtype=np.uint32)
             st_call = np.zeros(n, dtype=np.int32)
             nf = ctypes.c_uint32(0)
-            rc = lib().capnp_packed_framer_read(
+            rc = lib().capnp_packed_framer_read(  # later calls pop what is held, no new bytes
                 self.handle, host.ctypes.data if first else None, total if first else 0,
-                off.ctypes.data, lens.ctypes.data, buf.ctypes.data, cap, f_off.ctypes.data, f_len.ctypes.data,
+                off.ctypes.data if first else None, lens.ctypes.data if first else None, buf.ctypes.data, cap, f_off.ctypes.data, f_len.ctypes.data,
                 f_conn.ctypes.data, max_frames, st_call.ctypes.data, ctypes.byref(nf))
             if rc not in (OK, OUT_OF_SPACE):
                 _raise(rc, "framer_read")
@@ -546,9 +547,10 @@ class FramerSession:
                 frames.setdefault(c, []).append(view[o:o + ln])
             if rc == OK:
                 break
-            # frames or the table filled up: pop the rest into larger ones (no new bytes)
-            if k == 0:
-                cap *= 2
+            # frames or the table filled up: pop the rest into larger ones; a buffer of the
+            # largest known framed length pops at least that message
+            big = max((self.expected(c) for c in range(n)), default=0)
+            cap = max(cap * 2 if k == 0 else cap, (big + 7) // 8 * 8 + 64)
             max_frames *= 2
         status[status == 0] = END_OF_STREAM
         return frames, status
@@ -556,6 +558,13 @@ class FramerSession:
     def buffered(self, c: int) -> int:
         b = ctypes.c_uint64()
         _raise(lib().capnp_packed_framer_buffered(self.handle, int(c), ctypes.byref(b)), "framer_buffered")
+        return b.value
+
+    def expected(self, c: int) -> int:
+        """Framer.expected_total (framing.zig:10): framed bytes of connection c's current
+        message once its header is decoded, else 0."""
+        b = ctypes.c_uint64()
+        _raise(lib().capnp_packed_framer_expected(self.handle, int(c), ctypes.byref(b)), "framer_expected")
         return b.value
 
     def reset(self, c: int) -> None:

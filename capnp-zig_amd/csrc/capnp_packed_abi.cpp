@@ -817,6 +817,15 @@ int capnp_packed_framer_buffered(capnp_packed_framer* f, uint32_t conn, uint64_t
     return CAPNP_PACKED_OK;
 }
 
+int capnp_packed_framer_expected(capnp_packed_framer* f, uint32_t conn, uint64_t* framed_bytes) {
+    int st = framer_check(f, conn);
+    if (st) return st;
+    if (!framed_bytes) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "framed_bytes is null");
+    std::lock_guard<std::mutex> lock(f->mu);
+    *framed_bytes = f->need[conn];
+    return CAPNP_PACKED_OK;
+}
+
 int capnp_packed_framer_stats(capnp_packed_framer* f, uint64_t* uploaded, uint64_t* moved) {
     if (!f || !uploaded || !moved) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null pointer");
     std::lock_guard<std::mutex> lock(f->mu);

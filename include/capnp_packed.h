@@ -265,6 +265,10 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
 int capnp_packed_framer_reset(capnp_packed_framer* f, uint32_t conn);
 /* Framer.bufferedBytes (framing.zig:30-32): packed bytes held for the connection. */
 int capnp_packed_framer_buffered(capnp_packed_framer* f, uint32_t conn, uint64_t* bytes);
+/* Framer.expected_total (framing.zig:10, :89): framed bytes of the connection's current message
+ * once its header has been decoded, else 0. After OUT_OF_SPACE from capnp_packed_framer_read,
+ * a frames buffer of the largest such size (rounded up to 8) pops that message. */
+int capnp_packed_framer_expected(capnp_packed_framer* f, uint32_t conn, uint64_t* framed_bytes);
 /* Bytes copied host-to-device (every read's bytes once) and moved between device regions since
  * the session was made (a connection's bytes move when its region doubles). */
 int capnp_packed_framer_stats(capnp_packed_framer* f, uint64_t* uploaded, uint64_t* moved);

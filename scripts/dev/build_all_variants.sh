@@ -6,5 +6,4 @@ cd "$(dirname "$0")/../.."
 bash scripts/dev/build_variant.sh ds_k32 "-DCPK_DS_K=32"
 bash scripts/dev/build_variant.sh ds_w1 "-DCPK_DS_WAVES=1"
 bash scripts/dev/build_variant.sh ds_w2 "-DCPK_DS_WAVES=2"
-bash scripts/dev/build_variant.sh es_stream "-DCPK_ES_STREAM=1"
-bash scripts/dev/build_variant.sh em_pf "-DCPK_EM_PF=1"
+bash scripts/dev/build_variant.sh ds_tst "-DCPK_DS_TSTORE=1"

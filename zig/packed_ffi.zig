@@ -69,6 +69,7 @@ pub extern "capnp_packed" fn capnp_packed_framer_read(
 ) c_int;
 pub extern "capnp_packed" fn capnp_packed_framer_reset(f: *capnp_packed_framer, conn: u32) c_int;
 pub extern "capnp_packed" fn capnp_packed_framer_buffered(f: *capnp_packed_framer, conn: u32, bytes: *u64) c_int;
+pub extern "capnp_packed" fn capnp_packed_framer_expected(f: *capnp_packed_framer, conn: u32, framed_bytes: *u64) c_int;
 pub extern "capnp_packed" fn capnp_packed_framer_stats(f: *capnp_packed_framer, uploaded: *u64, moved: *u64) c_int;
 
 // ---- device batch entry points (pointers are device memory) ----------------
