@@ -689,12 +689,24 @@ class PackedConnections:
 # ---------------------------------------------------------------------------
 
 def set_decoder(name: str) -> str:
-    """Select the mid-unit batch decoder ("auto", "twopass", "fused" or "stream"; every one
-    is bit-exact) for batches enqueued from now on; returns the previous setting's name."""
+    """Select the mid-unit batch decoder ("auto", "twopass"; "fused" and "stream" in dev builds,
+    decoder_available) for batches enqueued from now on; returns the previous setting's name.
+    Every one is bit-exact."""
     prev = lib().capnp_packed_set_decoder(DECODERS[name])
     if prev < 0 or prev not in DECODERS.values():
         _raise(prev, "set_decoder")
     return {v: k for k, v in DECODERS.items()}[prev]
+
+
+def decoder_available(name: str) -> bool:
+    """Whether this build has the decoder: "auto" and "twopass" always; "fused" and "stream"
+    in dev builds only (CPK_DEV_DECODERS=1)."""
+    L = lib()
+    prev = L.capnp_packed_set_decoder(DECODERS[name])
+    if prev not in DECODERS.values():
+        return False
+    L.capnp_packed_set_decoder(prev)
+    return True
 
 
 def set_all_or_nothing(on: bool) -> bool:

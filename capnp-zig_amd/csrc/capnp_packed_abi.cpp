@@ -335,6 +335,8 @@ size_t capnp_packed_batch_workspace_bytes(uint32_t n) { return cpk::queue_bytes(
 int capnp_packed_set_decoder(int decoder) {
     if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_STREAM)
         return fail(CAPNP_PACKED_INVALID_ARGUMENT, "unknown decoder");
+    if (!cpk::decoder_built(decoder))
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "decoder not in this build (dev builds: CPK_DEV_DECODERS=1)");
     return cpk::set_decoder(decoder);
 }
 

@@ -22,6 +22,7 @@ size_t queue_bytes(uint32_t n);
 
 // capnp_packed_set_decoder: returns the previous setting
 int set_decoder(int decoder);
+bool decoder_built(int decoder);  // the fused / streaming decoders exist in dev builds only
 int set_all_or_nothing(int on);
 uint32_t set_launch_flags(uint32_t flags);
 hipError_t release_stream(hipStream_t stream);

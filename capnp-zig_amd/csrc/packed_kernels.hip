@@ -110,8 +110,8 @@ __device__ __forceinline__ uint4 load_nt(const void* p) {
     return make_uint4(t.x, t.y, t.z, t.w);
 }
 
-// Ring loads / output stores of the lane-per-unit decoders (decode_index_kernel,
-// decode_stream_kernel) in inline asm, so hipcc neither turns them into FLAT instructions
+// Ring loads (and the dev-build streaming decoder's output stores) of the lane-per-unit
+// decoders in inline asm, so hipcc neither turns them into FLAT instructions
 // (pointers that went through __shfl / LDS lose their address space, and FLAT counts on
 // lgkmcnt too: every LDS wait of the walk would wait for the prefetch) nor waits for them
 // itself (its own vmcnt(0) before the ring writes would also wait for the previous round's
@@ -122,16 +122,6 @@ __device__ __forceinline__ void ds_gload16(u32x4& d, const void* p) {
 }
 __device__ __forceinline__ void ds_gload16_nt(u32x4& d, const void* p) {
     asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(d) : "v"(p) : "memory");
-}
-#ifndef CPK_DS_TSTORE  // dev A/B: 1 = the stream decoder's output stores without the nt hint
-#define CPK_DS_TSTORE 0
-#endif
-__device__ __forceinline__ void ds_gstore8_nt(void* p, uint64_t v) {
-#if CPK_DS_TSTORE
-    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-#else
-    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
-#endif
 }
 
 // Order LDS traffic between lanes of ONE wave (the wave owns its LDS slice).
@@ -2409,751 +2399,14 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---------------------------------------------------------------------------
-// DECODE, streaming single pass (round 4; DESIGN.md §2.3b, the default for mid units).
-// The packed bytes cross HBM once and no piece records exist. The record chain is walked
-// where it is cheapest, lane per unit (64 units per wave, one record per instruction), and
-// the output is written where stores coalesce, many lanes per unit:
-//   ring   decode_index_kernel's load scheme: round k's 64-B blocks of the wave's 64 units
-//          come in by quad-coalesced 16-B loads issued one round ahead, land in the units'
-//          80-B LDS rings (block k-1's last piece, block k), and the walk takes the records
-//          whose first byte is in [64k - 16, 64k + 48) (all their bytes are resident);
-//   walk   every step, every active lane emits exactly one output word: a record (the tag's
-//          word; for 00 its first zero word, for FF its first literal word), one word of an
-//          FF run's literal body (8 bytes at pos), or one more word of a zero run. The step
-//          writes a u16 entry (tag << 8 | ring offset of the word's packed bytes) to row i of
-//          the wave's list; lanes keep their own state (next position, literal-body end,
-//          zero words left), so a run that crosses a round just continues. Zero runs of 16
-//          or more extra words are filled by the whole wave instead (one job per lane per
-//          sub-round), and words past a unit's capacity are counted, not emitted;
-//   store  after at most kDsK steps (a sub-round) the wave writes the listed words: G lanes
-//          per unit (G = 4, 8 or 16 by the longest list), lane (u, i) expands unit u's
-//          entry i from the unit's ring (v_alignbyte + v_perm with the tag's selector) and
-//          stores word W_u + i, so a store instruction writes 64/G runs of G words;
-// Errors follow message.zig:88-191 (UnexpectedEof for a record that runs past the input,
-// OutOfSpace with the required size), found at the walk's end: a failed unit may hold a
-// prefix of its output in its slot (never a byte past out_cap). Callers that need the slot
-// untouched select the two-pass decoder (capnp_packed_set_all_or_nothing).
-#ifndef CPK_DS_WAVES  // dev A/B: waves per block of decode_stream_kernel
-#define CPK_DS_WAVES 4
+// The single-read mid-unit decoders (fused, round 3; streaming, round 4) measured slower than
+// the two-pass decoder and live in a dev build only.
+#ifndef CPK_DEV_DECODERS
+#define CPK_DEV_DECODERS 0
 #endif
-#ifndef CPK_DS_K  // dev A/B: walk steps per sub-round
-#define CPK_DS_K 16
+#if CPK_DEV_DECODERS
+#include "dev_decoders.inc"
 #endif
-constexpr uint32_t kDsWaves = CPK_DS_WAVES;  // waves per block (one 1-KB selector table per block)
-constexpr uint32_t kDsK = CPK_DS_K;          // walk steps per sub-round = list rows
-constexpr uint32_t kDsRowE = 66;       // list row stride in u16 entries (132 B: conflict-free rows)
-constexpr uint32_t kDsRing = 80;       // ring bytes per unit
-constexpr uint32_t kDsZJob = 16;       // zero runs with this many extra words or more: a wave fill
-constexpr uint32_t kDsDead = 0xFFFFFFF0u;  // walk position of a lane with nothing (more) to walk
-constexpr uint32_t kDsGuard = 1024;        // sub-rounds per round before a wave gives up
-constexpr uint32_t kDsWave = kWave * kDsRing + kDsK * kDsRowE * 2 + kWave * 8;  // LDS bytes per wave
-
-// Expand selectors packed 4 bits per byte: byte k = sel[k] | sel[k + 4] << 4 (sel values are
-// 0..7 or 0x0C), so the table is 1 KB.
-struct SelLut32 {
-    uint32_t v[256];
-};
-constexpr SelLut32 make_sel_lut32() {
-    SelLut32 l{};
-    for (uint32_t t = 0; t < 256; ++t) {
-        const uint64_t s = kExpandLut.v[t];
-        uint32_t x = 0;
-        for (uint32_t k = 0; k < 4; ++k)
-            x |= (uint32_t)(((s >> (8 * k)) & 0xFu) | (((s >> (8 * (k + 4))) & 0xFu) << 4)) << (8 * k);
-        l.v[t] = x;
-    }
-    return l;
-}
-__device__ constexpr SelLut32 kExpandLut32 = make_sel_lut32();
-
-// s_waitcnt needs an immediate: wait until at most min(c, 63) vector-memory operations are
-// outstanding (fewer than the true number of younger operations only waits longer).
-__device__ __forceinline__ void vmcnt_at_most63(uint32_t c) {
-#define CPK_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-#define CPK_VM8(B) CPK_VM(B) CPK_VM(B + 1) CPK_VM(B + 2) CPK_VM(B + 3) CPK_VM(B + 4) CPK_VM(B + 5) CPK_VM(B + 6) CPK_VM(B + 7)
-    switch (c < 63u ? c : 63u) {
-        CPK_VM8(0) CPK_VM8(8) CPK_VM8(16) CPK_VM8(24) CPK_VM8(32) CPK_VM8(40) CPK_VM8(48)
-        CPK_VM(56) CPK_VM(57) CPK_VM(58) CPK_VM(59) CPK_VM(60) CPK_VM(61) CPK_VM(62)
-        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
-    }
-#undef CPK_VM8
-#undef CPK_VM
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    return __builtin_amdgcn_readlane(wave_incl_max(v, 0), kWave - 1);
-}
-
-__global__ __launch_bounds__(kDsWaves * kWave) void decode_stream_kernel(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
-    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
-    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
-    __shared__ uint32_t lut[256];
-    __shared__ __attribute__((aligned(16))) uint8_t lds_all[kDsWaves * kDsWave];
-    for (uint32_t t = threadIdx.x; t < 256; t += kDsWaves * kWave) lut[t] = kExpandLut32.v[t];
-    __syncthreads();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t* const ring_all = lds_all + wave * kDsWave;                              // 64 x 80 B
-    uint16_t* const lst = reinterpret_cast<uint16_t*>(ring_all + kWave * kDsRing);  // kDsK rows
-    uint64_t* const meta = reinterpret_cast<uint64_t*>(ring_all + kWave * kDsRing + kDsK * kDsRowE * 2);
-    const uint32_t wv = blockIdx.x * kDsWaves + wave;
-    const uint32_t lane = lane_id();
-    const uint32_t count = list ? *list_count : n;
-    if (wv * kWave >= count) return;  // wave-uniform
-    const uint32_t slot = wv * kWave + lane;
-    const bool valid = slot < count;
-    const uint32_t unit = valid ? ((list && count != n) ? list[slot] : slot) : 0u;
-
-    // ---- per-lane unit ---------------------------------------------------------------
-    const uint8_t* src = cpk_dummy16;
-    uint64_t P64 = 0, cap = 0;
-    uint8_t* dstb = nullptr;
-    int32_t st = ST_OK;
-    if (valid) {
-        src = in + in_off[unit];
-        P64 = in_len[unit];
-        dstb = out + out_off[unit];
-        cap = out_cap[unit];
-        if (P64 > 0 && (reinterpret_cast<uintptr_t>(dstb) & 7)) st = ST_ARG;  // an empty unit writes nothing
-    }
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    // mid units: at most kFlPieces pieces (class_scatter); the bound keeps positions in u32
-    const bool take = valid && st == ST_OK && P64 > 0 && P64 <= (1u << 24);
-    if (valid && st == ST_OK && P64 > (1u << 24)) st = ST_ARG;  // unreachable for the mid class
-    const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
-    const uint32_t npieces = (end + 15) >> 4;
-    const uint32_t maxr = __builtin_amdgcn_readfirstlane(wave_max_u32((end + 63) >> 6));
-    const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0xFFFFFFF0u);  // words the slot holds
-
-    // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block ------------
-    const uint4* qsrc[4];
-    uint32_t qlast[4];
-#pragma unroll
-    for (uint32_t m = 0; m < 4; ++m) {
-        const uint32_t r = 16 * m + lane / 4;
-        const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
-        const uint32_t rn = __shfl(npieces, r, kWave);
-        qsrc[m] = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16);
-        qlast[m] = rn ? rn - 1 : 0u;
-    }
-    const uint32_t qp = lane & 3;
-    u32x4 d0, d1, d2, d3;
-    auto load = [&](uint32_t k) {  // 4 loads: the next round's blocks (vmcnt counts them first)
-        ds_gload16_nt(d0, qsrc[0] + min(4 * k + qp, qlast[0]));
-        ds_gload16_nt(d1, qsrc[1] + min(4 * k + qp, qlast[1]));
-        ds_gload16_nt(d2, qsrc[2] + min(4 * k + qp, qlast[2]));
-        ds_gload16_nt(d3, qsrc[3] + min(4 * k + qp, qlast[3]));
-    };
-    uint8_t* const wq = ring_all + (lane / 4) * kDsRing + 16 + 16 * qp;  // unit 16m + l/4: + 16 * kDsRing * m
-    uint8_t* const ring = ring_all + lane * kDsRing;
-
-    uint32_t pos = take ? s : kDsDead;  // next record / literal word (aligned space)
-    uint32_t lit_end = 0;               // end of the FF literal body pos is in (pos < lit_end)
-    uint32_t zrem = 0;                  // zero words of the current run still to emit
-    uint32_t wc = 0;                    // words of the unit so far (emitted, counted past capw)
-    uint32_t younger = 0;               // vector-memory ops issued after the round's loads
-    if (maxr > 0) load(0);
-    for (uint32_t k = 0; k <= maxr; ++k) {
-        if (k < maxr) {
-            vmcnt_at_most63(younger);  // round k's loads have landed
-            asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
-        }
-        younger = 0;
-        if (k > 0) {
-            wave_lds_sync();  // every lane is done with round k-1's ring reads
-            *reinterpret_cast<uint4*>(ring) = *reinterpret_cast<const uint4*>(ring + 64);
-            wave_lds_sync();
-        }
-        if (k < maxr) {
-            *reinterpret_cast<u32x4*>(wq) = d0;
-            *reinterpret_cast<u32x4*>(wq + 16 * kDsRing) = d1;
-            *reinterpret_cast<u32x4*>(wq + 32 * kDsRing) = d2;
-            *reinterpret_cast<u32x4*>(wq + 48 * kDsRing) = d3;
-            if (k + 1 < maxr) load(k + 1);
-            wave_lds_sync();
-        }
-        const uint32_t ob = 64 * k;              // ring offset o = pos + 16 - ob in [0, 64)
-        const uint32_t lim = min(ob + 48, end);  // records / literal words starting before lim
-        // A lane emits at most ~70 sub-rounds' words per round (32 records of <= 16 listed
-        // words, or zero-run jobs); the guard only turns a defect into DEVICE_ERROR, not a hang.
-        for (uint32_t guard = 0;; ++guard) {  // sub-rounds
-            if (guard == kDsGuard) {
-                const bool live = zrem != 0u || pos < lim;
-                st = live ? ST_DEVERR : st;
-                pos = live ? kDsDead : pos;
-                zrem = 0;
-                break;
-            }
-            // ---- walk: up to kDsK steps, one output word per active lane per step ------
-            const uint32_t w0 = wc;  // the unit's word index of list row 0
-            uint32_t nent = 0;       // entries listed this sub-round
-            uint32_t zjob = 0;       // extra words of a zero run the wave fills after the stores
-#pragma unroll 1
-            for (uint32_t i = 0; i < kDsK; ++i) {
-                const bool inz = zrem != 0u;
-                const bool act = zjob == 0u && (inz || pos < lim);
-                if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                const uint32_t o = (pos + 16u - ob) & 63u;  // any pos reads inside the lane's ring
-                uint32_t t = ring[o];
-                uint32_t b1 = ring[o + 1];
-                uint32_t c9 = ring[o + 9];
-                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per step
-                const bool lit = !inz && pos < lit_end;          // a literal body word at pos
-                const bool rec = act && !inz && !lit;
-                const bool z = t == 0u, f = t == 0xFFu;
-                // message.zig:101-141: 00 c -> 1 + c zero words; FF w c -> w, then c literal
-                // words; other tags -> one word of popc(tag) packed bytes
-                const uint32_t len = lit ? 8u : 1u + __popc(t) + (uint32_t)(z | f);  // FF: 10, body apart
-                const uint32_t lend = pos + 10u + 8u * c9;  // end of an FF record's body
-                const bool eof = rec && (pos + len > end || (f && lend > end));  // :105-137
-                const uint32_t tg = inz ? 0u : lit ? 0xFFu : t;
-                const uint32_t dd = lit ? o : o + 1u;  // ring offset of the word's packed bytes
-                lst[i * kDsRowE + lane] = (uint16_t)((tg << 8) | dd);
-                const bool em = act && !eof;
-                const uint32_t wn = wc + (em ? 1u : 0u);
-                const bool zr = rec && !eof && z && b1 != 0u;  // a zero run with extra words
-                const bool bulk = zr && wn >= capw;             // past the slot: counted only
-                const bool job = zr && !bulk && b1 >= kDsZJob;
-                zrem = inz ? zrem - 1u : ((zr && !bulk && !job) ? b1 : 0u);
-                zjob = job ? b1 : zjob;  // a lane waiting on its job keeps it (and its state)
-                wc = wn + (bulk ? b1 : 0u);
-                lit_end = (rec && f) ? lend : lit_end;
-                pos = eof ? kDsDead : ((act && !inz) ? pos + len : pos);  // idle lanes stay put
-                st = eof ? ST_EOF : st;
-                nent = em ? i + 1u : nent;
-            }
-            // ---- store the listed words: G lanes per unit ---------------------------------
-            const uint32_t lu = w0 < capw ? min(nent, capw - w0) : 0u;  // entries that fit the slot
-            meta[lane] = (reinterpret_cast<uint64_t>(dstb) + 8ull * w0) | ((uint64_t)lu << 56);
-            const uint32_t nmax = wave_max_u32(lu);
-            wave_lds_sync();
-            if (nmax > 0) {
-                const uint32_t lg = nmax > 16u ? 5u : nmax > 8u ? 4u : nmax > 4u ? 3u : 2u;  // G = 1 << lg
-                const uint32_t ii = lane & ((1u << lg) - 1u);
-                const uint32_t per = kWave >> lg;  // units per store instruction
-                for (uint32_t u0 = 0; u0 < (uint32_t)kWave; u0 += per) {
-                    const uint32_t u = u0 + (lane >> lg);
-                    const uint64_t m = meta[u];
-                    const bool ok = ii < (uint32_t)(m >> 56);
-                    const uint32_t e = lst[ii * kDsRowE + u];
-                    const uint32_t dd = e & 0xFFu;
-                    const uint32_t* const rw = reinterpret_cast<const uint32_t*>(ring_all + u * kDsRing + (dd & ~3u));
-                    const uint32_t r0 = rw[0], r1 = rw[1], r2 = rw[2];
-                    const uint32_t x = lut[e >> 8];
-                    const uint32_t sh = dd & 3u;
-                    const uint32_t lo = __builtin_amdgcn_alignbyte(r1, r0, sh);
-                    const uint32_t hi = __builtin_amdgcn_alignbyte(r2, r1, sh);
-                    const uint32_t a = __builtin_amdgcn_perm(hi, lo, x & 0x0F0F0F0Fu);
-                    const uint32_t b = __builtin_amdgcn_perm(hi, lo, (x >> 4) & 0x0F0F0F0Fu);
-                    if (__builtin_amdgcn_ballot_w64(ok) != 0) {  // uniform: the store issues
-                        if (ok)
-                            ds_gstore8_nt(reinterpret_cast<void*>((m & 0x00FFFFFFFFFFFFFFull) + 8ull * ii),
-                                          (uint64_t)a | ((uint64_t)b << 32));
-                        ++younger;
-                    }
-                }
-            }
-            // ---- zero runs the wave fills: words [wc, wc + c) of each lane with a job --------
-            uint64_t jobs = __builtin_amdgcn_ballot_w64(zjob != 0u);
-            while (jobs) {
-                const uint32_t jl = (uint32_t)__builtin_ctzll(jobs);
-                jobs &= jobs - 1;
-                const uint32_t jw = readlane(wc, jl), jc = readlane(zjob, jl), jcap = readlane(capw, jl);
-                const uint64_t jd = (uint64_t)readlane((uint32_t)reinterpret_cast<uint64_t>(dstb), jl) |
-                                    ((uint64_t)readlane((uint32_t)(reinterpret_cast<uint64_t>(dstb) >> 32), jl) << 32);
-                const uint32_t hi = min(jw + jc, jcap);  // jw < jcap (a job is never past the slot)
-                for (uint32_t w = jw + lane; w < hi; w += kWave) ds_gstore8_nt(reinterpret_cast<uint64_t*>(jd) + w, 0ull);
-                younger += (hi - jw + kWave - 1) / kWave;
-            }
-            wc += zjob;
-            // ---- next sub-round, or the next round when every lane is past lim -------------
-            if (__builtin_amdgcn_ballot_w64(zrem != 0u || pos < lim) == 0) break;
-            wave_lds_sync();  // the store reads of the list and meta are done
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!valid) return;
-    if (st != ST_OK) {
-        out_len[unit] = 0;
-        status[unit] = st;
-        return;
-    }
-    out_len[unit] = 8ull * wc;
-    status[unit] = wc > capw ? ST_SPACE : ST_OK;
-}
-
-// ---------------------------------------------------------------------------
-// DECODE, fused single pass (round 3): the packed bytes cross HBM once
-// and no piece records exist. One wave per unit, persistent grid, the next unit's pieces
-// prefetched into registers while this one is decoded (as decode_fill_kernel).
-//   stage  the unit's pieces go to the wave's LDS window at their 16-B aligned positions
-//          (unit byte 0 at window byte s = src & 15); the window past the unit, up to the
-//          end of the lanes' blocks (1024 L bytes, L pieces per lane) and 32 bytes beyond,
-//          is filled with 0x7F, a tag whose record is 8 bytes long: every lane then owns a
-//          whole block, and a record chain that reaches the unit's end continues through
-//          the fill 8 bytes at a time (lanes past the unit compose to the identity);
-//   map    lane k composes, over its block [16kL, 16(k+1)L), the map "state at the block
-//          start -> state at the block end" of the 8 chain states d = 0..7 (d = bytes to
-//          the next tag; a non-FF record is at most 8 bytes long, message.zig:101-141).
-//          A byte pair (b1, b2) maps d to [len(b1)-2, len(b2)-1, 0, 1, 2, 3, 4, 5][d]:
-//          two v_perm_b32 per pair for all 8 states, the source bytes from two 256-B LDS
-//          tables. An FF tag's length (10 + 8c) has no state: it maps to 0xFF, which
-//          v_perm keeps (a selector >= 13 gives 0xFF): "unknown";
-//   fix    a lane with unknown states and exactly one FF byte in its block: every unknown
-//          state reached that byte as a tag, so its exit is the exact walk from the FF
-//          record's landing (a landing more than 7 bytes past the block is "far": 0xFE);
-//   scan   unknown / far states are replaced by a guess (7), and a DPP prefix composition
-//          of the maps (6 steps, two v_perm each) gives every lane a speculative entry;
-//          lane 0's entry is s (a 0x7F tag at s - 8 when s >= 8);
-//   count  each lane walks its records from its entry (exact lengths), listing their
-//          positions; an exclusive max-scan of the lanes' exits checks every entry against
-//          the left neighbour's exit, and lanes whose entry was wrong walk again from the
-//          corrected one until no lane changes (exact: lane 0's entry is known, and each
-//          round fixes at least the first wrong lane). Then words and UnexpectedEof (a
-//          record running past the unit) before any output, as unpackPacked;
-//   codes, expansion: codes from the listed records, decode_fill_kernel's expansion.
-// Exactness does not depend on the data: guesses only cost re-walks.
-constexpr uint32_t kFuWaves = 4;
-constexpr uint32_t kFuPk = kFlPieces * 16 + 32;  // 64 lanes x L <= 5 pieces + the 32-B 0x7F lookahead
-constexpr uint32_t kFuFar = 0xFEu;               // map state: exit more than 7 bytes past the block
-constexpr uint32_t kFuIdLo = 0x03020100u, kFuIdHi = 0x07060504u;  // identity map
-constexpr uint32_t kFuOut = 512;   // output words per code pass (the code list)
-constexpr uint32_t kFuLoc = 16;    // records per lane the walk lists (u8 offsets in the lane's block)
-constexpr uint32_t kFuRow = kFuLoc + 1;  // + the slot the records past kFuLoc overwrite
-
-// Exact record walk (lengths of message.zig:152-191) from the tag at window position p to
-// the first record start at or past hi.
-__device__ __forceinline__ uint32_t fu_walk(const uint8_t* pk, uint32_t p, uint32_t hi) {
-    while (p < hi) {
-        uint32_t t = pk[p];
-        uint32_t c = pk[p + 9];
-        asm volatile("" : "+v"(t), "+v"(c));
-        p += 1u + __popc(t) + (uint32_t)((t == 0u) | (t == 0xFFu)) + (t == 0xFFu ? 8u * c : 0u);
-    }
-    return p;
-}
-
-// Inclusive prefix composition of 8-state maps over the wave (lane k: G_k o ... o G_0;
-// lanes a DPP step does not reach compose with the identity).
-__device__ __forceinline__ void fu_scan(uint32_t& lo, uint32_t& hi) {
-#define CPK_FU_STEP(CTRL, ROWS)                                                        \
-    {                                                                                  \
-        const uint32_t plo = dpp_mov<CTRL, ROWS>(lo, kFuIdLo);                         \
-        const uint32_t phi = dpp_mov<CTRL, ROWS>(hi, kFuIdHi);                         \
-        const uint32_t nlo = __builtin_amdgcn_perm(hi, lo, plo);                       \
-        hi = __builtin_amdgcn_perm(hi, lo, phi);                                       \
-        lo = nlo;                                                                      \
-    }
-    CPK_FU_STEP(0x111, 0xF);
-    CPK_FU_STEP(0x112, 0xF);
-    CPK_FU_STEP(0x114, 0xF);
-    CPK_FU_STEP(0x118, 0xF);
-    CPK_FU_STEP(0x142, 0xA);
-    CPK_FU_STEP(0x143, 0xC);
-#undef CPK_FU_STEP
-}
-
-// The map of one dword of a lane's block (two byte pairs): d -> src[d], src = [TA[b1],
-// TB[b2], 0, 1 | 2, 3, 4, 5] with TA = len - 2, TB = len - 1 (0xFF for an FF byte).
-__device__ __forceinline__ void fu_map_dword(const uint8_t* tab, uint32_t w, uint32_t& mlo, uint32_t& mhi) {
-    uint32_t a = tab[w & 0xFFu];
-    uint32_t b = tab[256u + ((w >> 8) & 0xFFu)];
-    uint32_t src = (a | (b << 8)) | 0x01000000u;
-    mlo = __builtin_amdgcn_perm(0x05040302u, src, mlo);
-    mhi = __builtin_amdgcn_perm(0x05040302u, src, mhi);
-    a = tab[(w >> 16) & 0xFFu];
-    b = tab[256u + (w >> 24)];
-    src = (a | (b << 8)) | 0x01000000u;
-    mlo = __builtin_amdgcn_perm(0x05040302u, src, mlo);
-    mhi = __builtin_amdgcn_perm(0x05040302u, src, mhi);
-}
-
-// 0x80 in each byte of w that is 0xFF (exact per byte)
-__device__ __forceinline__ uint32_t fu_ff_bytes(uint32_t w) {
-    const uint32_t y = ~w;
-    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-}
-
-__global__ __launch_bounds__(kFuWaves * kWave) void decode_fused_kernel(const uint8_t* __restrict__ in,
-                                                                        const uint64_t* __restrict__ in_off,
-                                                                        const uint64_t* __restrict__ in_len,
-                                                                        uint32_t n, uint8_t* __restrict__ out,
-                                                                        const uint64_t* __restrict__ out_off,
-                                                                        const uint64_t* __restrict__ out_cap,
-                                                                        uint64_t* __restrict__ out_len,
-                                                                        int32_t* __restrict__ status,
-                                                                        const uint32_t* __restrict__ list,
-                                                                        const uint32_t* __restrict__ list_count) {
-    __shared__ uint8_t tab[512];  // [0, 256): len - 2 of a tag, [256, 512): len - 1 (FF: 0xFF)
-    __shared__ __attribute__((aligned(16))) uint8_t pk_all[kFuWaves * kFuPk];
-    __shared__ __attribute__((aligned(16))) uint16_t code_all[kFuWaves * (kFuOut + 8)];  // + a dummy slot
-    __shared__ __attribute__((aligned(16))) uint8_t rl_all[kFuWaves * kWave * kFuRow];
-    __shared__ uint64_t lut[256];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    {
-        const uint32_t b = threadIdx.x;  // 256 threads: one table entry each
-        const uint32_t lm1 = max((uint32_t)__popc(b), 1u);  // 00 -> 2-byte record
-        tab[b] = (uint8_t)(b == 0xFFu ? 0xFFu : lm1 - 1u);
-        tab[256u + b] = (uint8_t)(b == 0xFFu ? 0xFFu : lm1);
-        lut[b] = expand_selector(b);
-    }
-    __syncthreads();
-    uint8_t* const pk = pk_all + wave * kFuPk;
-    uint4* const pk4 = reinterpret_cast<uint4*>(pk);
-    uint16_t* const code = code_all + wave * (kFuOut + 8);
-    uint8_t* const rl = rl_all + wave * (kWave * kFuRow);  // lane l's record list at rl[kFuRow l ..]
-    const uint32_t G = gridDim.x * kFuWaves;
-    const uint32_t u0 = blockIdx.x * kFuWaves + wave;
-    const uint32_t n_all = n;
-    if (list) n = *list_count;
-    if (u0 >= n) return;
-    if (n == n_all) list = nullptr;  // every unit is listed: batch order
-
-    // per-unit values of the wave's units k0 .. k0+63 (lane i: unit k0 + i)
-    uint64_t m_in = 0, m_out = 0, m_cap = 0;
-    uint32_t m_P = 0, m_unit = 0xFFFFFFFFu;
-    auto load_batch = [&](uint32_t k0) {
-        const uint64_t slot = (uint64_t)u0 + (uint64_t)(k0 + lane) * G;
-        m_unit = 0xFFFFFFFFu;
-        if (slot < n) {
-            const uint32_t uu = list ? list[slot] : (uint32_t)slot;
-            m_unit = uu;
-            m_in = in_off[uu];
-            m_P = (uint32_t)in_len[uu];  // mid units: <= kFlPieces * 16 bytes
-            m_out = out_off[uu];
-            m_cap = out_cap[uu];
-        }
-    };
-    struct FuMeta {
-        uint32_t unit, P;
-        const uint8_t* src;
-        uint8_t* dst;
-        uint64_t cap;
-    };
-    auto meta = [&](uint32_t j) {
-        FuMeta m;
-        m.unit = readlane(m_unit, j);
-        m.P = readlane(m_P, j);
-        m.src = in + ((uint64_t)readlane((uint32_t)m_in, j) | ((uint64_t)readlane((uint32_t)(m_in >> 32), j) << 32));
-        m.dst = out + ((uint64_t)readlane((uint32_t)m_out, j) | ((uint64_t)readlane((uint32_t)(m_out >> 32), j) << 32));
-        m.cap = (uint64_t)readlane((uint32_t)m_cap, j) | ((uint64_t)readlane((uint32_t)(m_cap >> 32), j) << 32);
-        return m;
-    };
-    auto runnable = [&](const FuMeta& m) {  // wave-uniform
-        return m.unit != 0xFFFFFFFFu && m.P > 0 && !(reinterpret_cast<uintptr_t>(m.dst) & 7);
-    };
-    uint4 v0, v1, v2, v3, v4;
-    auto load_unit = [&](const FuMeta& m) {
-        if (!runnable(m)) return;
-        const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(m.src) & 15);
-        const uint4* const b = reinterpret_cast<const uint4*>(m.src - s);
-        const uint32_t np = (s + m.P + 15) >> 4;
-        const uint32_t last = np - 1;
-        v0 = load_nt(b + min(lane, last));
-        if (np > 64) v1 = load_nt(b + min(lane + 64, last));
-        if (np > 128) v2 = load_nt(b + min(lane + 128, last));
-        if (np > 192) v3 = load_nt(b + min(lane + 192, last));
-        if (np > 256) v4 = load_nt(b + min(lane + 256, last));
-    };
-
-    load_batch(0);
-    FuMeta cur = meta(0);
-    load_unit(cur);
-    uint32_t younger = 0;  // vector-memory ops issued after cur's loads (its predecessor's stores)
-#ifdef CPK_FILL_PROF
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    for (uint32_t k = 0; (uint64_t)u0 + (uint64_t)k * G < n; ++k) {
-        const bool go = runnable(cur);
-        FL_T(t0);
-        vmcnt_at_most(younger);  // cur's pieces are in registers
-        FL_T(t1);
-        FL_ACC(0, t1 - t0);
-        younger = 0;
-        uint32_t s = 0, end = 0, L = 0;
-        if (go) {
-            s = (uint32_t)(reinterpret_cast<uintptr_t>(cur.src) & 15);
-            end = s + cur.P;
-            const uint32_t np = (end + 15) >> 4;  // <= kFlPieces (a mid unit)
-            L = (np + 63) >> 6;
-            wave_lds_sync();  // the previous unit's LDS reads are done
-            // ---- stage: pieces, 0x7F past the unit up to 1024 L (+ 32 B) -----------------
-            const uint4 f7 = make_uint4(0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu);
-            const uint32_t keep = end - 16 * (np - 1);  // unit bytes in the last piece (1..16)
-            auto put = [&](uint32_t m, uint4 v) {
-                const uint32_t pc = lane + 64 * m;
-                if (pc >= np) v = f7;
-                else if (pc == np - 1 && keep < 16) {  // bytes [keep, 16) of the last piece -> 0x7F
-                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i) {
-                        const uint32_t lo = 4 * i;
-                        const uint32_t mask = keep <= lo ? 0u : (keep >= lo + 4 ? 0xFFFFFFFFu : (1u << (8 * (keep - lo))) - 1u);
-                        w[i] = (w[i] & mask) | (0x7F7F7F7Fu & ~mask);
-                    }
-                    v = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-                pk4[pc] = v;
-            };
-            put(0, v0);
-            if (L > 1) put(1, v1);
-            if (L > 2) put(2, v2);
-            if (L > 3) put(3, v3);
-            if (L > 4) put(4, v4);
-            if (lane < 2) pk4[64 * L + lane] = f7;  // lookahead of the last block's records
-            wave_lds_sync();
-            if (lane == 0 && s >= 8) pk[s - 8] = 0x7F;  // lane 0 enters at s & 7: an 8-byte record to s
-            wave_lds_sync();
-        }
-        // the next unit's loads go out before any work or store of this unit
-        const uint32_t k1 = k + 1;
-        if ((k1 & 63) == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            load_batch(k1);
-        }
-        const FuMeta nxt = meta(k1 & 63);
-        load_unit(nxt);
-        FL_T(t2);
-        FL_ACC(1, t2 - t1);
-        if (cur.unit != 0xFFFFFFFFu && !go) {  // empty unit, or a misaligned output slot
-            if (lane == 0) {
-                out_len[cur.unit] = 0;
-                status[cur.unit] = cur.P == 0 ? ST_OK : ST_ARG;
-            }
-            younger += 2;
-        }
-        if (go) {
-            const uint32_t blk = 16 * L;          // block bytes per lane
-            const uint32_t lo = lane * blk, hi = lo + blk;
-            // ---- map -----------------------------------------------------------------
-            uint32_t mlo = kFuIdLo, mhi = kFuIdHi;
-            const uint4* const bp = pk4 + lane * L;
-            uint32_t um = 0, nchg = 0, jst = 0;  // unknown states, pieces that changed them, the last one
-#pragma unroll
-            for (uint32_t j = 0; j < kFlMaxL; ++j) {
-                if (j < L) {
-                    const uint4 d = bp[j];
-                    fu_map_dword(tab, d.x, mlo, mhi);
-                    fu_map_dword(tab, d.y, mlo, mhi);
-                    fu_map_dword(tab, d.z, mlo, mhi);
-                    fu_map_dword(tab, d.w, mlo, mhi);
-                    const uint32_t u2 = (mlo & 0x80808080u) | ((mhi & 0x80808080u) >> 1);  // unknown lo / hi states
-                    nchg += u2 != um ? 1u : 0u;
-                    jst = u2 != um ? j : jst;
-                    um = u2;
-                }
-            }
-            FL_T(t3);
-            FL_ACC(2, t3 - t2);
-            // ---- fix: unknown states that all appeared in one piece with one FF byte ----------
-            // (then each of them reached that byte as a tag; otherwise they stay unresolved)
-            uint32_t farx = 0;
-            const bool unk = um != 0;
-            if (__builtin_amdgcn_ballot_w64(unk) != 0 && unk && nchg == 1) {
-                const uint4 d = bp[jst];
-                const uint32_t f4[4] = {fu_ff_bytes(d.x), fu_ff_bytes(d.y), fu_ff_bytes(d.z), fu_ff_bytes(d.w)};
-                uint32_t J = 0, x = 0;
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) {
-                    if (J == 0 && f4[i]) x = lo + 16 * jst + 4 * i + (__builtin_ctz(f4[i]) >> 3);
-                    J += __popc(f4[i]);
-                }
-                if (J == 1) {
-                    const uint32_t X = fu_walk(pk, x + 10u + 8u * pk[x + 9], hi);
-                    farx = X;
-                    const uint32_t st = X - hi <= 7u ? X - hi : kFuFar;
-                    const uint32_t um_lo = ((mlo & 0x80808080u) >> 7) * 0xFFu;  // unknown bytes
-                    const uint32_t um_hi = ((mhi & 0x80808080u) >> 7) * 0xFFu;
-                    mlo = (mlo & ~um_lo) | (st * 0x01010101u & um_lo);
-                    mhi = (mhi & ~um_hi) | (st * 0x01010101u & um_hi);
-                }
-            }
-            FL_T(t4);
-            FL_ACC(3, t4 - t3);
-            // ---- scan: a speculative entry for every lane ------------------------------------
-            // A state the maps could not resolve (several FF bytes, or an exit more than 7 bytes
-            // past the block) is guessed as 7; the record walks below verify every entry.
-            {
-                const uint32_t hm_lo = ((mlo & 0x80808080u) >> 7) * 0xFFu;
-                const uint32_t hm_hi = ((mhi & 0x80808080u) >> 7) * 0xFFu;
-                mlo = (mlo & ~hm_lo) | (0x07070707u & hm_lo);
-                mhi = (mhi & ~hm_hi) | (0x07070707u & hm_hi);
-            }
-            const uint32_t e0 = s & 7u;
-            uint32_t glo = mlo, ghi = mhi;
-            if (lane == 0) glo = ghi = (__builtin_amdgcn_perm(mhi, mlo, e0) & 0xFFu) * 0x01010101u;
-            fu_scan(glo, ghi);
-            uint32_t E = lo + (fu_prev_lane(glo) & 0xFFu);  // entry: the first record start in the block
-            if (lane == 0) E = s;
-            (void)farx;
-            FL_T(t5);
-            FL_ACC(4, t5 - t4);
-            // ---- walk + verify: each lane walks its records from its entry (exact), one per pass:
-            //      words, and each record's offset in the lane's block in its list (rl: kFuLoc u8
-            //      per lane; a lane with more records takes the code walk below). A lane's entry is
-            //      right iff it equals the furthest exit of the lanes before it (lane 0's is); the
-            //      lanes whose entry was wrong take that exit and walk again. -----------------------
-            const uint32_t lim = min(hi, end);
-            uint8_t* const rll = rl + kFuRow * lane;
-            uint32_t words = 0, ne = 0, p = E;
-            for (;;) {
-                for (;;) {  // one record per lane per pass
-                    if (__builtin_amdgcn_ballot_w64(p < lim) == 0) break;
-                    if (p < lim) {
-                        uint32_t t = pk[p];
-                        uint32_t b1 = pk[p + 1];
-                        uint32_t c9 = pk[p + 9];
-                        asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                        const bool z = t == 0u, f = t == 0xFFu;
-                        rll[min(ne, kFuLoc)] = (uint8_t)(p - lo);  // entry kFuLoc: the overflow slot
-                        ++ne;
-                        words += 1u + (z ? b1 : 0u) + (f ? c9 : 0u);
-                        p += __popc(t) + 1u + ((z || f) ? 1u + (f ? 8u * c9 : 0u) : 0u);
-                    }
-                }
-                // p: the lane's exit (its entry when no record starts in its block)
-                const uint32_t xm = fu_prev_lane(wave_incl_max(p, lane));
-                const bool bad = lane > 0 && lo < end && E != xm;
-                if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
-                if (bad) {
-                    E = xm;
-                    p = xm;
-                    words = 0;
-                    ne = 0;
-                }
-            }
-            const uint32_t pos = min(E, lim);
-            // a record that runs past the unit leaves its lane's exit past the unit's end
-            const bool any_eof = __builtin_amdgcn_ballot_w64(lo < end && p > end) != 0;
-            const bool ovf = __builtin_amdgcn_ballot_w64(ne > kFuLoc) != 0;  // a list overflowed: code walk
-            FL_T(t6);
-            FL_ACC(5, t6 - t5);
-            const uint32_t incl = wave_incl_sum(words, lane);
-            const uint32_t T = readlane(incl, kWave - 1);
-            const uint32_t wbase = incl - words;
-            int32_t st = ST_OK;
-            if (any_eof) st = ST_EOF;
-            else if (8ull * T > cur.cap) st = ST_SPACE;
-            if (st == ST_OK) {
-                const bool a16 = !(reinterpret_cast<uintptr_t>(cur.dst) & 15);
-                uint64_t* const dst = reinterpret_cast<uint64_t*>(cur.dst);
-                const uint32_t nl = min(ne, kFuLoc);
-                for (uint32_t W0 = 0; W0 < T; W0 += kFuOut) {
-                    const uint32_t W1 = min(T, W0 + kFuOut);
-                    wave_lds_sync();
-                    reinterpret_cast<uint4*>(code)[lane] = make_uint4(kFlZero * 0x10001u, kFlZero * 0x10001u,
-                                                                      kFlZero * 0x10001u, kFlZero * 0x10001u);
-                    wave_lds_sync();
-                    if (!ovf) {
-                        // ---- codes from the list: a tag position per output word (zero words keep
-                        //      kFlZero; an FF run's body words are literal codes). The list gives every
-                        //      record's position, so the passes do not depend on each other ------------
-                        uint32_t w = wbase;
-                        uint32_t rn = 0, rs = 0, rw = 0;  // a literal run longer than 3 words: the wave writes it
-                        for (uint32_t i = 0; i < nl; ++i) {
-                            if (__builtin_amdgcn_ballot_w64(w < W1) == 0) break;
-                            if (w < W1) {
-                                const uint32_t e = lo + rll[i];
-                                uint32_t t = pk[e];
-                                uint32_t b1 = pk[e + 1];
-                                uint32_t c9 = pk[e + 9];
-                                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                                const bool z = t == 0u, f = t == 0xFFu;
-                                if (!z && w >= W0) code[w - W0] = (uint16_t)e;
-                                const uint32_t c = f ? c9 : 0u;
-                                if (c) {
-                                    if (c <= 3u || rn != 0) {
-                                        for (uint32_t j = 1; j <= c; ++j) {
-                                            const uint32_t wi = w + j;
-                                            if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (e + 1 + 8 * j));
-                                        }
-                                    } else {
-                                        rn = c;
-                                        rs = e + 9;
-                                        rw = w + 1;
-                                    }
-                                }
-                                w += 1u + (z ? b1 : 0u) + c;
-                            }
-                        }
-                        uint64_t rm = __builtin_amdgcn_ballot_w64(rn != 0);
-                        while (rm) {  // literal runs: lane i of the wave writes word i, i + 64, ...
-                            const uint32_t l = (uint32_t)__builtin_ctzll(rm);
-                            rm &= rm - 1;
-                            const uint32_t nn = readlane(rn, l), ss = readlane(rs, l), ww = readlane(rw, l);
-                            for (uint32_t j = lane; j < nn; j += kWave) {
-                                const uint32_t wi = ww + j;
-                                if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (ss + 8 * j));
-                            }
-                        }
-                    } else {
-                        // ---- code walk (decode_fill_kernel) ------------------------------------------
-                        const bool mine = words > 0 && wbase < W1 && wbase + words > W0;
-                        uint32_t p = mine ? pos : lim, w = wbase;
-                        for (;;) {
-                            const bool act = p < lim && w < W1;
-                            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-                            const uint32_t pp = act ? p : 0u;
-                            uint32_t t = pk[pp];
-                            uint32_t b1 = pk[pp + 1];
-                            uint32_t c9 = pk[pp + 9];
-                            asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                            const bool z = t == 0u, f = t == 0xFFu;
-                            code[(act && !z && w >= W0) ? w - W0 : kFuOut] = (uint16_t)pp;
-                            const uint32_t c = f ? c9 : 0u;
-                            if (act && c) {
-                                for (uint32_t i = 1; i <= c; ++i) {
-                                    const uint32_t wi = w + i;
-                                    if (wi >= W0 && wi < W1) code[wi - W0] = (uint16_t)(kFlLit | (pp + 1 + 8 * i));
-                                }
-                            }
-                            w = act ? w + 1u + (z ? b1 : 0u) + c : w;
-                            p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
-                        }
-                    }
-                    wave_lds_sync();
-                    FL_T(t7);
-                    FL_ACC(6, t7 - t6);
-                    // ---- expand by output word: coalesced stores -----------------------------------
-                    const uint32_t nw = W1 - W0;
-                    if (a16) {
-                        for (uint32_t i = 2 * lane; i < nw; i += 2 * kWave) {
-                            const uint32_t cc = *reinterpret_cast<const uint32_t*>(code + i);
-                            const uint64_t x0 = fill_word(pk, lut, cc & 0xFFFFu);
-                            const uint64_t x1 = fill_word(pk, lut, cc >> 16);
-                            if (i + 1 < nw) {
-                                const u32x4 vv = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
-                                __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(dst + W0 + i));
-                            } else {
-                                dst[W0 + i] = x0;
-                            }
-                        }
-                        younger += (nw + 2 * kWave - 1) / (2 * kWave);
-                    } else {
-                        for (uint32_t i = lane; i < nw; i += kWave) dst[W0 + i] = fill_word(pk, lut, code[i]);
-                        younger += (nw + kWave - 1) / kWave;
-                    }
-                    FL_T(t8);
-                    FL_ACC(7, t8 - t7);
-                }
-            }
-            if (lane == 0) {
-                out_len[cur.unit] = st == ST_EOF ? 0ull : 8ull * T;
-                status[cur.unit] = st;
-            }
-            younger += 2;  // the two stores above (one wave instruction each)
-        }
-        cur = nxt;
-    }
-#ifdef CPK_FILL_PROF
-    if (lane == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // ---- size classes ------------------------------------------------
 // A batch's units are split by size before the coding kernels run, so each kernel gets
@@ -5634,6 +4887,9 @@ static int decoder_variant() {
     return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
 }
 int set_decoder(int v) { return g_decoder.exchange(v); }
+bool decoder_built(int v) {
+    return v == CAPNP_PACKED_DECODER_AUTO || v == CAPNP_PACKED_DECODER_TWO_PASS || CPK_DEV_DECODERS;
+}
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
@@ -5680,10 +4936,14 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const double sm_frac = mid_stream ? 0.85 : 1.0;  // share of the resident grid
     const uint32_t sm_cap = std::max(1u, (uint32_t)(sm_res * sm_frac));
     const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_cap);
+#if CPK_DEV_DECODERS
     // the streaming decoder may leave a failed unit's prefix: all-or-nothing takes the two-pass one
     const int dv = (decoder_variant() == CAPNP_PACKED_DECODER_STREAM && small_variant() == 0)
                        ? (int)CAPNP_PACKED_DECODER_TWO_PASS : decoder_variant();
     const bool streaming = dv == CAPNP_PACKED_DECODER_STREAM;
+#else
+    constexpr bool streaming = false;
+#endif
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
@@ -5711,6 +4971,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
+#if CPK_DEV_DECODERS
     if (streaming) {  // small and mid units, 64 per wave
         const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);  // waves past the count exit
         decode_stream_kernel<<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
@@ -5719,6 +4980,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
         const hipError_t j = side.join();
         return e != hipSuccess ? e : j;
     }
+#endif
     // the mid units' passes on a second side stream, before the small kernel (mid_side_stream)
     const hipStream_t ms = mid_stream ? side.stream2() : stream;
     if (!mid_stream) {
@@ -5732,14 +4994,17 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                      out_len, status, q);
         }
     }
-    // mid units: the indexed two-pass decoder (index pass + fill pass), or the fused
-    // single-pass decoder when selected (capnp_packed_set_decoder)
+    // mid units: the indexed two-pass decoder (index pass + fill pass), or in a dev build the
+    // fused single-pass decoder when selected (capnp_packed_set_decoder)
+#if CPK_DEV_DECODERS
     if (dv == CAPNP_PACKED_DECODER_FUSED) {
         static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);
         const uint32_t fu_blocks = std::min((n + kFuWaves - 1) / kFuWaves, fu_res);
         decode_fused_kernel<<<fu_blocks, kFuWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                         out_len, status, mid, q + 4);
-    } else {
+    } else
+#endif
+    {
         uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
         decode_index_kernel<false><<<ix_blocks_for(n), kWave * kIxBw, 0, ms>>>(
             in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 4, rec);

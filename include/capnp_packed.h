@@ -345,10 +345,13 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
 /* Decoder selection for the batch decode of mid-size units (a tuning knob, not a
  * semantic one: every decoder is bit-exact):
  *   CAPNP_PACKED_DECODER_TWO_PASS  index pass + fill pass (the packed bytes are read twice);
+ *   CAPNP_PACKED_DECODER_AUTO      the library's default (the two-pass decoder).
+ * Dev builds only (built with CPK_DEV_DECODERS=1; the shipped library returns
+ * CAPNP_PACKED_INVALID_ARGUMENT for them): the single-read decoders, both measured slower
+ * than the two-pass decoder on every density:
  *   CAPNP_PACKED_DECODER_FUSED     single pass: per-lane 8-state entry maps, one read;
  *   CAPNP_PACKED_DECODER_STREAM    single pass: lane-per-unit walk by 64-B windows, stores
- *                                  by many lanes per unit (a failed unit may hold a prefix);
- *   CAPNP_PACKED_DECODER_AUTO      the library's default.
+ *                                  by many lanes per unit (a failed unit may hold a prefix).
  * Returns the previous value; applies to batches enqueued after the call (process-wide). */
 enum {
     CAPNP_PACKED_DECODER_AUTO = 0,

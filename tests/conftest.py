@@ -30,3 +30,16 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(params=["twopass", "fused", "stream"])
+def decoder(request):
+    """Runs a decode test under each mid-unit decoder (capnp_packed_set_decoder): the two-pass
+    decoder (the shipped one), and the fused / streaming single-read decoders, which exist in
+    dev builds only (CPK_DEV_DECODERS=1, capnp-zig_amd/lib_exp/dev_decoders.so via CPK_LIB;
+    DESIGN.md §2.3a / §2.3b) and are skipped otherwise."""
+    import capnp_packed as cp
+    if not cp.decoder_available(request.param):
+        pytest.skip(f"the {request.param} decoder is in dev builds only")
+    with cp.decoder(request.param):
+        yield request.param

@@ -107,11 +107,20 @@ def test_status_tables_agree():
 
 def test_decoder_selection_round_trips():
     # capnp_packed_set_decoder is a process-wide knob (no device needed to set it)
-    prev = cp.set_decoder("fused")
-    assert cp.set_decoder("twopass") == "fused"
-    with cp.decoder("fused"):
-        assert cp.set_decoder("fused") == "fused"
+    # the fused / streaming decoders exist in dev builds only (CPK_DEV_DECODERS=1)
+    for dev in ("fused", "stream"):
+        if cp.decoder_available(dev):
+            prev = cp.set_decoder(dev)
+            assert cp.set_decoder("twopass") == dev
+            with cp.decoder(dev):
+                assert cp.set_decoder(dev) == dev
+            assert cp.set_decoder(prev) == "twopass"
+        else:
+            assert cp.lib().capnp_packed_set_decoder(cp.DECODERS[dev]) == cp.INVALID_ARGUMENT
+    prev = cp.set_decoder("twopass")
     assert cp.set_decoder(prev) == "twopass"
+    if not os.environ.get("CPK_LIB"):  # the shipped build has the two-pass decoder only
+        assert not cp.decoder_available("fused") and not cp.decoder_available("stream")
     assert cp.lib().capnp_packed_set_decoder(7) == cp.INVALID_ARGUMENT
     assert cp.set_all_or_nothing(True) is False
     assert cp.set_all_or_nothing(False) is True

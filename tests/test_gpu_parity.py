@@ -139,12 +139,6 @@ PAIRS = [("binary", "packed"), ("segmented", "segmented-packed"),
          ("fixture_single.bin", "fixture_single_packed.bin"), ("fixture_far.bin", "fixture_far_packed.bin")]
 
 
-@pytest.fixture(params=["twopass", "fused", "stream"])
-def decoder(request):
-    """Every decode test runs under each mid-unit decoder (capnp_packed_set_decoder):
-    the indexed two-pass decoder and the fused single-pass decoder."""
-    with cp.decoder(request.param):
-        yield request.param
 
 
 @pytest.mark.parametrize("unpacked,packed", PAIRS)

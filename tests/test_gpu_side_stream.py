@@ -25,11 +25,6 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["twopass", "fused", "stream"])
-def decoder(request):
-    """Runs the test under each mid-unit decoder (capnp_packed_set_decoder)."""
-    with cp.decoder(request.param):
-        yield request.param
 DEV = "cuda"
 
 
