@@ -133,6 +133,17 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+#ifdef CPK_EM_PROF
+// Diagnostic build: cycles per phase of the one-tile encoders (s_memtime), summed over waves:
+// [0..3] encode_unit (prologue, stage, tile, total), [4..7] encode_message_one (same).
+__device__ unsigned long long cpk_em_prof[8];
+#define EM_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define EM_ADD(i, d) do { if (lane == 0) atomicAdd(&cpk_em_prof[i], (unsigned long long)(d)); } while (0)
+#else
+#define EM_T(v) do { } while (0)
+#define EM_ADD(i, d) do { } while (0)
+#endif
+
 // Wave scans on DPP: row_shr:1/2/4/8 inside each 16-lane row, then row_bcast:15 and
 // row_bcast:31 across rows (gfx9). A lane a step does not reach keeps `ident`. No LDS
 // round trips (the ds_bpermute scans they replace cost ~6 LDS latencies in a row).
@@ -696,6 +707,7 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
                                                       uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                       uint32_t unit, uint8_t* lds, const uint64_t* lut,
                                                       uint32_t lane) {
+    EM_T(e0);
     const uint64_t b0 = in_off[unit];
     const uint64_t nbytes = in_len[unit];
     uint64_t ob = 0, cap = 0;
@@ -727,10 +739,17 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
     const uint32_t words = (uint32_t)(nbytes >> 3);
     if (words <= kEncMaxWords) {  // one tile (the headline 4-KiB units)
         wave_lds_sync();          // the previous unit's write-back read the slice
+        EM_T(e1);
         encode_stage(lds, src, words, lane);
         wave_lds_sync();
+        EM_T(e2);
         uint32_t cz = 0, cf = 0;
         const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        EM_T(e3);
+        EM_ADD(0, e1 - e0);
+        EM_ADD(1, e2 - e1);
+        EM_ADD(2, e3 - e2);
+        EM_ADD(3, e3 - e0);
         if (lane == 0) {
             out_len[unit] = P;
             status[unit] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
@@ -996,6 +1015,7 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
                                                    uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
 
     // ---- segment table: lane l takes segments 8l .. 8l+7 ------------------------------
+    EM_T(e0);
     const uint32_t c_in = seg_count[msg];
     const uint32_t first = seg_first[msg];
     const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
@@ -1063,10 +1083,17 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
     }
     if (!TILED) {  // one tile
         uint32_t hint = 0xFFFFFFFFu;
+        EM_T(e1);
         msg_stage(m, 0, words, lane, hint, lds);
         wave_lds_sync();
+        EM_T(e2);
         uint32_t cz = 0, cf = 0;
         const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        EM_T(e3);
+        EM_ADD(4, e1 - e0);
+        EM_ADD(5, e2 - e1);
+        EM_ADD(6, e3 - e2);
+        EM_ADD(7, e3 - e0);
         if (lane == 0) {
             out_len[msg] = P;
             status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
@@ -5189,8 +5216,15 @@ hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t*
 
 }  // namespace cpk
 
+// Diagnostic builds only: read and clear the phase cycle sums.
+#ifdef CPK_EM_PROF
+extern "C" int capnp_packed_debug_em_prof(unsigned long long* out8) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_em_prof), sizeof(z)) != hipSuccess) return 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(cpk::cpk_em_prof), z, sizeof(z)) != hipSuccess;
+}
+#endif
 #ifdef CPK_FILL_PROF
-// Diagnostic build only: read and clear the fill-kernel phase cycle sums.
 extern "C" int capnp_packed_debug_fill_prof(unsigned long long* out8) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_fill_prof), sizeof(z)) != hipSuccess) return 1;
