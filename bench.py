@@ -322,7 +322,7 @@ def dense_leg(args, dev, reps=10):
             "note": "decode of 1M units from one dense packed stream (unaligned unit starts)"}
 
 
-def host_path(args, dev, n_units=1 << 16):
+def host_path(args, dev, n_units=1 << 16, chunks=8, nstreams=2):
     """PCIe-inclusive rates, reported beside the device-resident
     number and never as `value`. Host buffers are pinned; the batch is cut into 8
     chunks over 2 streams so H2D, kernels and D2H of different chunks overlap.
@@ -331,7 +331,6 @@ def host_path(args, dev, n_units=1 << 16):
     (the encode leg copies back each chunk's exact packed size, known here from a
     prior pass; a socket writer would read it from the sizes first)."""
     ub = args.unit_bytes
-    chunks = 8
     per = n_units // chunks
     d_all = cp.generate(n_units, ub, seed=args.seed, zero_thresh=args.zero_thresh, device=dev)
     in_off, in_len = cp.uniform_layout(n_units, ub, device=dev)
@@ -348,10 +347,10 @@ def host_path(args, dev, n_units=1 << 16):
     h_out = torch.empty(n_units * ub, dtype=torch.uint8).pin_memory()
     h_pk2 = torch.empty_like(h_pk).pin_memory()
     del d_all, dense
-    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)]
     cmax = int((h_off[per::per] - h_off[:-1:per]).max().item()) + 16
     bufs = []
-    for _ in range(2):
+    for _ in range(nstreams):
         b = {"un": torch.empty(per * ub, dtype=torch.uint8, device=dev),
              "pk": torch.empty(cmax, dtype=torch.uint8, device=dev),
              "len": torch.empty(per, dtype=torch.int64, device=dev),
@@ -363,7 +362,7 @@ def host_path(args, dev, n_units=1 << 16):
 
     def run_decode():
         for c in range(chunks):
-            sm, b = streams[c % 2], bufs[c % 2]
+            sm, b = streams[c % nstreams], bufs[c % nstreams]
             lo, hi = int(h_off[c * per]), int(h_off[(c + 1) * per])
             with torch.cuda.stream(sm):
                 b["pk"][:hi - lo].copy_(h_pk[lo:hi], non_blocking=True)
@@ -375,7 +374,7 @@ def host_path(args, dev, n_units=1 << 16):
 
     def run_encode():
         for c in range(chunks):
-            sm, b = streams[c % 2], bufs[c % 2]
+            sm, b = streams[c % nstreams], bufs[c % nstreams]
             lo, hi = int(h_off[c * per]), int(h_off[(c + 1) * per])
             with torch.cuda.stream(sm):
                 b["un"].copy_(h_in[c * per * ub:(c + 1) * per * ub], non_blocking=True)
@@ -397,7 +396,8 @@ def host_path(args, dev, n_units=1 << 16):
     res.update({"units": n_units, "unit_bytes": ub,
                 "bit_exact_roundtrip": bool(torch.equal(h_out, h_in) and
                                             torch.equal(h_pk2[:int(h_off[-1])], h_pk[:int(h_off[-1])])),
-                "note": "GiB/s of unpacked bytes; pinned host buffers, 8 chunks over 2 streams, dense "
+                "chunks": chunks, "streams": nstreams,
+                "note": "GiB/s of unpacked bytes; pinned host buffers, chunks over streams, dense "
                         "packed stream on the host side (PCIe Gen5 x16, 63 GB/s spec)"})
     return res
 
