@@ -902,11 +902,13 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
 // holds them (word offsets of the segments in LDS).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig:310)
-constexpr uint32_t kMsgPadSegs = 255;  // one-tile pass: offsets 0..count in the 64 rows' pads
+constexpr uint32_t kMsgOneSegs = 64;   // one-tile pass: a segment per lane (more: the tiled pass)
 
-// PAD: the word offsets live in the 16-B pads of the tile's 80-B LDS rows (u32 slot s at row
-// s / 4, bytes 64 + 4 (s % 4)), free while the tile is staged: the one-tile pass then needs no
-// LDS beyond encode_kernel's (7 waves per SIMD, not 5), for messages of < 256 segments.
+// PAD (the one-tile pass): the segments' word offsets and addresses live in the 16-B pads of the
+// tile's 80-B LDS rows (u32 slot s at row s / 4, bytes 64 + 4 (s % 4); offset s at slot s,
+// s <= count, address s at slots 128 + 2s, 129 + 2s), free while the tile is staged: the pass
+// needs no LDS beyond encode_kernel's (7 waves per SIMD, not 5), and no global load between the
+// segment table and the data.
 __device__ __forceinline__ uint8_t* msg_pad(uint8_t* lds, uint32_t slot) {
     return lds + (slot >> 2) * kEncRow + 64 + 4 * (slot & 3);
 }
@@ -917,8 +919,12 @@ struct MsgView {
         return PAD ? *reinterpret_cast<const uint32_t*>(msg_pad(const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(woff)), s))
                    : woff[s];
     }
-    __device__ __forceinline__ uint64_t ba(uint32_t s) const { return base[s]; }
-    const uint64_t* base;   // device address of segment s (LDS copy, or the caller's array)
+    __device__ __forceinline__ uint64_t ba(uint32_t s) const {
+        return PAD ? *reinterpret_cast<const uint64_t*>(
+                         msg_pad(const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(woff)), 128 + 2 * s))
+                   : base[s];
+    }
+    const uint64_t* base;   // device address of segment s (LDS, tiled pass)
     uint32_t count;         // segments (>= 1)
     uint32_t hw;            // header words
 };
@@ -1002,6 +1008,159 @@ __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, ui
     }
 }
 
+// One-tile staging by word pairs: lane l gathers framed words 2l + 128j and 2l + 1 + 128j with
+// one 16-B load when both lie in one segment (all but a segment's edges), else word by word,
+// and writes the pair to its row with one 16-B LDS store: half the load instructions and
+// address computations of msg_stage's word-per-load gather. All addresses first, then every
+// load, then the LDS stores, so the loads are in flight together.
+typedef uint64_t u64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+// Segment data loads through global (AS1) pointers: the addresses come out of LDS, and a
+// generic pointer would make FLAT loads, which also count on lgkmcnt (the LDS waits of the
+// gather would wait for the data).
+__device__ __forceinline__ uint64_t gload8(const uint64_t* p) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ u64x2_a8 gload16a8(const uint64_t* p) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) u64x2_a8*>(reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ void msg_stage_pairs(const MsgView<1>& m, uint32_t tw, uint32_t lane, uint8_t* lds) {
+    const uint64_t* pa[4];
+    const uint64_t* pb[4];
+    uint64_t ha[4], hb[4];
+    bool pair[4];
+    uint32_t hint = 0xFFFFFFFFu, hh = 0;
+    uint32_t wlo = 1, whi = 0;  // cached segment window [wlo, whi) of payload words (empty)
+    uint64_t wbase = 0;
+    auto seek = [&](uint32_t p) {  // address of payload word p (window cached)
+        if (p < wlo || p >= whi) {
+            if (hint >= m.count || p < m.wo(hint)) {
+                uint32_t lo = 0, hi = m.count;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (m.wo(mid) <= p) lo = mid;
+                    else hi = mid;
+                }
+                hint = lo;
+            }
+            while (p >= m.wo(hint + 1)) ++hint;
+            wlo = m.wo(hint);
+            whi = m.wo(hint + 1);
+            wbase = m.ba(hint);
+        }
+        return reinterpret_cast<const uint64_t*>(wbase + 8ull * (p - wlo));
+    };
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 2 * lane + 128 * j;
+        pa[j] = pb[j] = nullptr;
+        ha[j] = hb[j] = 0;
+        pair[j] = false;
+        if (i < tw) {
+            const bool two = i + 1 < tw;
+            if (i < m.hw) ha[j] = msg_word(m, i, hh);  // header word (no load)
+            else pa[j] = seek(i - m.hw);
+            if (two) {
+                if (i + 1 < m.hw) hb[j] = msg_word(m, i + 1, hh);
+                else if (i >= m.hw && i + 1 - m.hw < whi) pair[j] = true;  // same segment as word a
+                else pb[j] = seek(i + 1 - m.hw);
+            }
+        }
+    }
+    uint64_t xa[4], xb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (pair[j]) {
+            const u64x2_a8 v = gload16a8(pa[j]);
+            xa[j] = v.x;
+            xb[j] = v.y;
+        } else {
+            xa[j] = pa[j] ? gload8(pa[j]) : ha[j];
+            xb[j] = pb[j] ? gload8(pb[j]) : hb[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 2 * lane + 128 * j;
+        uint8_t* const d = lds + (i >> 3) * kEncRow + (i & 7) * 8;
+        if (i + 1 < tw) *reinterpret_cast<u32x4*>(d) = u32x4{(uint32_t)xa[j], (uint32_t)(xa[j] >> 32),
+                                                              (uint32_t)xb[j], (uint32_t)(xb[j] >> 32)};
+        else if (i < tw) *reinterpret_cast<uint64_t*>(d) = xa[j];
+    }
+}
+
+// One message of at most 64 segments and one framed tile (<= 512 words), a wave: lane s loads
+// segment s's length and address (two coalesced loads), a wave scan gives the word offsets, and
+// offsets and addresses go to the row pads (MsgView<1>); then the pair gather and encode_tile.
+// Anything else (more segments or words, and the argument checks that come with them) is
+// marked for the tiled pass (kStNeedFull), which applies toBytes' checks in the reference order.
+template <bool WRITE>
+__device__ __forceinline__ void encode_message_tile1(uint32_t msg, uint32_t lane, const uint64_t* lut, uint8_t* lds,
+                                                     const uint64_t* __restrict__ seg_ptr,
+                                                     const uint64_t* __restrict__ seg_len,
+                                                     const uint32_t* __restrict__ seg_first,
+                                                     const uint32_t* __restrict__ seg_count,
+                                                     uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                     const uint64_t* __restrict__ out_cap,
+                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
+    EM_T(e0);
+    const uint32_t c_in = seg_count[msg];
+    const uint32_t first = seg_first[msg];
+    const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
+    if (count > kMsgOneSegs) {
+        if (lane == 0) status[msg] = kStNeedFull;
+        return;
+    }
+    uint64_t len = 0, ptr = 0;
+    if (c_in && lane < count) {
+        len = seg_len[first + lane];
+        ptr = seg_ptr[first + lane];
+    }
+    uint64_t ob = 0, cap = 0;
+    if (WRITE) {
+        ob = out_off[msg];
+        cap = out_cap[msg];
+    }
+    // segments are whole words at 8-B aligned addresses (a MessageBuilder's always are); any
+    // segment of more than a tile sends the message to the tiled pass before the u32 sum
+    const bool odd = (len & 7) != 0 || (ptr & 7) != 0;
+    const bool big = (len >> 3) > kEncMaxWords;
+    if (__builtin_amdgcn_ballot_w64(odd || big) != 0) {
+        if (lane == 0) status[msg] = kStNeedFull;  // the tiled pass reports ST_ARG / codes it
+        return;
+    }
+    const uint32_t wl = (uint32_t)(len >> 3);
+    const uint32_t incl = wave_incl_sum(wl, lane);
+    const uint32_t payload = readlane(incl, 63);
+    const uint32_t hw = (1 + count + ((count & 1) ? 0 : 1)) / 2;  // toBytes 2135-2137, in words
+    const uint32_t words = hw + payload;
+    if (words > kEncMaxWords) {
+        if (lane == 0) status[msg] = kStNeedFull;
+        return;
+    }
+    if (lane < count) {
+        *reinterpret_cast<uint32_t*>(msg_pad(lds, lane)) = incl - wl;
+        *reinterpret_cast<uint64_t*>(msg_pad(lds, 128 + 2 * lane)) = ptr;
+    }
+    if (lane == 63) *reinterpret_cast<uint32_t*>(msg_pad(lds, count)) = payload;  // woff[count]
+    wave_lds_sync();
+    const MsgView<1> m{reinterpret_cast<const uint32_t*>(lds), nullptr, count, hw};
+    EM_T(e1);
+    msg_stage_pairs(m, words, lane, lds);
+    wave_lds_sync();
+    EM_T(e2);
+    uint32_t cz = 0, cf = 0;
+    const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+    EM_T(e3);
+    EM_ADD(4, e1 - e0);
+    EM_ADD(5, e2 - e1);
+    EM_ADD(6, e3 - e2);
+    EM_ADD(7, e3 - e0);
+    if (lane == 0) {
+        out_len[msg] = P;
+        status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
+    }
+}
+
 // One message (see encode_message_kernel); lds / woff / base are the wave's slices.
 template <bool WRITE, bool TILED>
 __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, const uint64_t* lut, uint8_t* lds,
@@ -1015,7 +1174,6 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
                                                    uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
 
     // ---- segment table: lane l takes segments 8l .. 8l+7 ------------------------------
-    EM_T(e0);
     const uint32_t c_in = seg_count[msg];
     const uint32_t first = seg_first[msg];
     const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
@@ -1023,15 +1181,8 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
         if (lane == 0) { out_len[msg] = 0; status[msg] = ST_ARG; }
         return;
     }
-    if (!TILED && count > kMsgPadSegs) {  // more offsets than the row pads hold: the tiled pass
-        if (lane == 0) status[msg] = kStNeedFull;
-        return;
-    }
-    // !TILED: the offsets go to the row pads of the tile slice (MsgView<true>)
-    auto wput = [&](uint32_t s, uint32_t v) {
-        if (TILED) woff[s] = v;
-        else *reinterpret_cast<uint32_t*>(lds + (s >> 2) * kEncRow + 64 + 4 * (s & 3)) = v;
-    };
+    static_assert(TILED, "one-tile messages: encode_message_tile1");
+    auto wput = [&](uint32_t s, uint32_t v) { woff[s] = v; };
     uint32_t wsum = 0;
     bool bad = false;
     uint32_t wl[8];
@@ -1048,7 +1199,7 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
             // segments are whole words at 8-B aligned addresses (a MessageBuilder's always are)
             bad |= (len & 7) != 0 || (ptr & 7) != 0 || (len >> 3) > 0xFFFFFFFFull;
             wl[t] = (uint32_t)(len >> 3);
-            if (TILED) base[s] = ptr;
+            base[s] = ptr;
             wsum += wl[t];
         }
     }
@@ -1069,36 +1220,12 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
         return;
     }
     const uint32_t words = (uint32_t)words64;
-    if (!TILED && words > kEncMaxWords) {
-        if (lane == 0) status[msg] = kStNeedFull;
-        return;
-    }
     wave_lds_sync();
-    const MsgView<TILED ? 0 : 1> m{TILED ? woff : reinterpret_cast<const uint32_t*>(lds),
-                            TILED ? base : (c_in ? seg_ptr + first : nullptr), count, hw};
+    const MsgView<0> m{woff, base, count, hw};
     uint64_t ob = 0, cap = 0;
     if (WRITE) {
         ob = out_off[msg];
         cap = out_cap[msg];
-    }
-    if (!TILED) {  // one tile
-        uint32_t hint = 0xFFFFFFFFu;
-        EM_T(e1);
-        msg_stage(m, 0, words, lane, hint, lds);
-        wave_lds_sync();
-        EM_T(e2);
-        uint32_t cz = 0, cf = 0;
-        const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
-        EM_T(e3);
-        EM_ADD(4, e1 - e0);
-        EM_ADD(5, e2 - e1);
-        EM_ADD(6, e3 - e2);
-        EM_ADD(7, e3 - e0);
-        if (lane == 0) {
-            out_len[msg] = P;
-            status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
-        }
-        return;
     }
 
     // ---- tiles, as in encode_tiled_kernel ------------------------------------------------
@@ -1143,10 +1270,10 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
     }
 }
 
-// TILED = false: every message; one framed tile (<= 512 words) is encoded here with
-// the single-tile encode_tile (segment addresses read from the caller's array, so
-// the wave's LDS is the tile plus the word offsets), longer messages are marked for
-// TILED = true, which keeps the addresses in LDS and walks the tiles.
+// TILED = false: every message; one framed tile (<= 512 words) of at most 64 segments is
+// encoded here (encode_message_tile1: offsets and addresses in the tile's row pads), other
+// messages are marked for TILED = true, which keeps the offsets and addresses in LDS arrays,
+// applies the argument checks and walks the tiles.
 // The multi-tile pass strides over the batch with a small grid, 64 statuses per load.
 template <bool WRITE, bool TILED>
 __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* __restrict__ seg_ptr,
@@ -1174,8 +1301,8 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
     if (!TILED) {
         const uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
         if (msg < n)
-            encode_message_one<WRITE, false>(msg, lane, lut, lds, woff, base, seg_ptr, seg_len, seg_first, seg_count,
-                                             out, out_off, out_cap, out_len, status);
+            encode_message_tile1<WRITE>(msg, lane, lut, lds, seg_ptr, seg_len, seg_first, seg_count, out, out_off,
+                                        out_cap, out_len, status);
         return;
     }
     const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;

@@ -251,9 +251,9 @@ def test_encode_message_batch_matches_toPackedBytes():
         p = float(rng.choice([0.1, 0.5, 0.9, 1.0, 0.0]))
         messages.append([seg(int(rng.integers(0, 300)), p) for _ in range(int(rng.integers(1, 12)))])
     messages.append([seg(1, .5) for _ in range(512)])            # the segment limit, header of 257 words
-    # one-tile messages around the 255 word offsets the one-tile pass keeps in its row pads
-    # (more segments go to the tiled pass)
-    for k in (254, 255, 256, 300):
+    # around the 64 segments the one-tile pass takes (a segment per lane; more go to the tiled
+    # pass), and the 255 offsets an earlier one-tile pass kept in its row pads
+    for k in (63, 64, 65, 254, 255, 256, 300):
         messages.append([seg(int(rng.integers(0, 2)), .5) for _ in range(k)])
     messages.append([seg(700, .5), seg(2000, 0.97), seg(5, 0.0)])  # tiles, zero and literal runs across segments
     messages.append([bytes(8 * 600), bytes(8 * 600)])             # one zero run over two segments and tiles
