@@ -912,6 +912,16 @@ constexpr uint32_t kMsgOneSegs = 64;   // one-tile pass: a segment per lane (mor
 __device__ __forceinline__ uint8_t* msg_pad(uint8_t* lds, uint32_t slot) {
     return lds + (slot >> 2) * kEncRow + 64 + 4 * (slot & 3);
 }
+typedef uint64_t u64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+// Segment data loads through global (AS1) pointers: the addresses come out of LDS, and a
+// generic pointer would make FLAT loads, which also count on lgkmcnt (the LDS waits of the
+// gather would wait for the data).
+__device__ __forceinline__ uint64_t gload8(const uint64_t* p) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ u64x2_a8 gload16a8(const uint64_t* p) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) u64x2_a8*>(reinterpret_cast<uintptr_t>(p));
+}
 template <int PAD>
 struct MsgView {
     const uint32_t* woff;   // LDS: word offset of segment s in the payload, s <= count
@@ -954,7 +964,7 @@ __device__ __forceinline__ uint64_t msg_word(const MsgView<PAD>& m, uint32_t q, 
         s = lo;
     }
     while (p >= m.wo(s + 1)) ++s;  // skip to the segment holding p (empty ones included)
-    return *reinterpret_cast<const uint64_t*>(m.ba(s) + 8ull * (p - m.wo(s)));
+    return gload8(reinterpret_cast<const uint64_t*>(m.ba(s) + 8ull * (p - m.wo(s))));
 }
 
 // Stage framed words [tb, tb + tw) (tw <= 512) into the row layout. Lane l gathers
@@ -1000,7 +1010,7 @@ __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, ui
     }
     uint64_t x[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = src[j] ? *src[j] : hv[j];
+    for (int j = 0; j < 8; ++j) x[j] = src[j] ? gload8(src[j]) : hv[j];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const uint32_t i = lane + 64 * j;
@@ -1013,16 +1023,6 @@ __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, ui
 // and writes the pair to its row with one 16-B LDS store: half the load instructions and
 // address computations of msg_stage's word-per-load gather. All addresses first, then every
 // load, then the LDS stores, so the loads are in flight together.
-typedef uint64_t u64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
-// Segment data loads through global (AS1) pointers: the addresses come out of LDS, and a
-// generic pointer would make FLAT loads, which also count on lgkmcnt (the LDS waits of the
-// gather would wait for the data).
-__device__ __forceinline__ uint64_t gload8(const uint64_t* p) {
-    return *reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(reinterpret_cast<uintptr_t>(p));
-}
-__device__ __forceinline__ u64x2_a8 gload16a8(const uint64_t* p) {
-    return *reinterpret_cast<const __attribute__((address_space(1))) u64x2_a8*>(reinterpret_cast<uintptr_t>(p));
-}
 __device__ __forceinline__ void msg_stage_pairs(const MsgView<1>& m, uint32_t tw, uint32_t lane, uint8_t* lds) {
     const uint64_t* pa[4];
     const uint64_t* pb[4];
