@@ -1111,25 +1111,7 @@ __device__ __forceinline__ void encode_message_tile1(uint32_t msg, uint32_t lane
         return;
     }
     uint64_t len = 0, ptr = 0;
-    if (count <= 8) {
-        // wave-uniform addresses: scalar loads, which do not queue behind the other waves'
-        // data loads in the vector memory pipeline (the dependent level costs that queue)
-        uint64_t L[8], A[8];
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t) {
-            L[t] = 0;
-            A[t] = 0;
-            if (c_in > t) {
-                L[t] = seg_len[first + t];
-                A[t] = seg_ptr[first + t];
-            }
-        }
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t) {
-            len = lane == t ? L[t] : len;
-            ptr = lane == t ? A[t] : ptr;
-        }
-    } else if (c_in && lane < count) {
+    if (c_in && lane < count) {
         len = seg_len[first + lane];
         ptr = seg_ptr[first + lane];
     }
