@@ -707,7 +707,18 @@ struct capnp_packed_framer {
         *c = want;
         return CAPNP_PACKED_OK;
     }
-    int run_jobs(std::vector<uint64_t>& jobs) {
+    // The copy jobs of a read (host vector hjobs, kept until the stream has consumed it, so a
+    // read's upload and region copies need no synchronisation of their own: the walk pass's
+    // synchronisation covers them).
+    std::vector<uint64_t> hjobs;
+    bool jobs_inflight = false;
+    int settle() {  // the previous read's job upload is done with hjobs
+        if (!jobs_inflight) return CAPNP_PACKED_OK;
+        jobs_inflight = false;
+        const hipError_t e = hipStreamSynchronize(s);
+        return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "framer copy jobs");
+    }
+    int run_jobs(std::vector<uint64_t>& jobs, bool wait = true) {
         if (jobs.empty()) return CAPNP_PACKED_OK;
         const uint32_t nj = (uint32_t)(jobs.size() / 3);
         // the jobs go after the per-connection arrays in the state scratch
@@ -717,9 +728,10 @@ struct capnp_packed_framer {
         uint64_t* const dj = reinterpret_cast<uint64_t*>(d_state + at);
         hipError_t e = hipMemcpyAsync(dj, jobs.data(), jobs.size() * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = cpk::launch_copy_jobs(dj, nj, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);  // `jobs` is reused by the caller
+        if (e == hipSuccess && wait) e = hipStreamSynchronize(s);  // `jobs` is reused by the caller
         if (e != hipSuccess) return hip_fail(e, "framer copy jobs");
-        jobs.clear();
+        if (wait) jobs.clear();
+        else jobs_inflight = true;  // hjobs only: cleared by the next read after settle()
         return CAPNP_PACKED_OK;
     }
     static uint64_t region_for(uint64_t bytes) { return std::max<uint64_t>(65536, (2 * bytes + 255) & ~255ull); }
@@ -858,6 +870,7 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
     for (uint32_t c = 0; c < n; ++c) status[c] = CAPNP_PACKED_END_OF_STREAM;
 
     // ---- 1. the new bytes: one H2D into the staging buffer, appended to the regions ---------
+    if ((st = f->settle())) return st;  // a previous read's copies are done with d_stage / hjobs
     if (in_bytes && in_len) {
         if ((st = capnp_packed_framer::grow(&f->d_stage, &f->stage_cap, in_bytes + 32))) return st;
         e = hipMemcpyAsync(f->d_stage, in, in_bytes, hipMemcpyHostToDevice, s);
@@ -875,7 +888,8 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
                 grow_bytes += capnp_packed_framer::region_for(live);
             }
         }
-        std::vector<uint64_t> jobs;
+        std::vector<uint64_t>& jobs = f->hjobs;
+        jobs.clear();
         if (any_grow && f->top + grow_bytes > f->acap) {
             if ((st = f->rearena(want))) return st;  // every region sized for its bytes after this read
         } else if (any_grow) {
@@ -901,7 +915,7 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
                                      reinterpret_cast<uint64_t>(f->d_stage + in_off[c]), in_len[c]});
             f->len[c] += in_len[c];
         }
-        if ((st = f->run_jobs(jobs))) return st;
+        if ((st = f->run_jobs(jobs, false))) return st;  // ordered before the passes below
     }
 
     // ---- 2. rounds: headers, walks from the saved positions, decodes of whole messages ------
@@ -959,6 +973,7 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
             if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 2ull * k, r_len, 3ull * k * 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) return hip_fail(e, "framer header pass");
+            f->jobs_inflight = false;
             const int32_t* const hs = reinterpret_cast<const int32_t*>(hm.data() + 4ull * k);
             for (uint32_t j = 0; j < k; ++j) {
                 const uint32_t c = list[j];
@@ -992,6 +1007,7 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
         if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), d_st, 4ull * n, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "framer walk pass");
+        f->jobs_inflight = false;
         // whole messages: decoded from the arena into frame slots, then to the caller's buffer
         std::vector<uint32_t> done;
         uint64_t slots = 0;
@@ -1048,6 +1064,7 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
         fcur += so;
     }
     *n_frames = nf;
+    if ((st = f->settle())) return st;  // no pass ran after the upload: the caller's bytes are consumed
     return full ? fail(CAPNP_PACKED_OUT_OF_SPACE, "frames buffer or frame table full: call again to pop the rest")
                 : CAPNP_PACKED_OK;
 }
