@@ -350,3 +350,58 @@ def test_framer_session_errors_and_reset():
     fr, st = sess.read({})
     assert [bytes(x) for x in fr[0]] == [msgs[5]] and sess.buffered(0) == 0
     sess.close()
+
+
+def _shaped_message(rng, kind):
+    """Messages whose packed form stresses the framer walk: many segments (a header of up to 129
+    words, decoded across several reads), zero-heavy (2 packed bytes per 256 words), literal-heavy
+    (FF runs of 256 words), and ordinary ones."""
+    if kind == 0:
+        return pyref.frame([bytes(8 * int(rng.integers(0, 3))) for _ in range(int(rng.integers(60, 257)))])
+    if kind == 1:
+        return pyref.frame([bytes(8 * int(rng.integers(256, 6000)))])
+    if kind == 2:
+        b = rng.integers(1, 256, 8 * int(rng.integers(200, 3000))).astype(np.uint8)
+        return pyref.frame([b.tobytes()])
+    return random_message(rng)
+
+
+def test_framer_session_fuzz_reads():
+    """The device-resident session (capnp_packed_framer_*) over 24 connections for 30 rounds:
+    each connection's stream cut into reads of 1-7 bytes (headers split byte by byte), ~1 KiB or
+    up to 64 KiB, some rounds skipping a connection; regions regrow and the arena is rebuilt as
+    connections fall behind. Every frame, in order, against the oracle reader, every byte
+    uploaded once."""
+    rng = np.random.default_rng(0x5E55)
+    n = 24
+    streams, expect = [], []
+    for c in range(n):
+        msgs = [_shaped_message(rng, int(rng.integers(0, 4))) for _ in range(int(rng.integers(1, 6)))]
+        data = b"".join(oracle.pack(m)[1] for m in msgs)
+        streams.append(data)
+        expect.append(msgs)
+    size = [int(rng.choice([4, 1024, 65536])) for _ in range(n)]
+    pos = [0] * n
+    sess = cp.FramerSession(n)
+    got = [[] for _ in range(n)]
+    uploaded = 0
+    for r in range(30):
+        reads = {}
+        for c in range(n):
+            if pos[c] >= len(streams[c]) or (r < 29 and rng.random() < 0.2):
+                continue
+            k = int(rng.integers(1, size[c] + 1))
+            if r == 29:
+                k = len(streams[c])  # the last round delivers the rest
+            reads[c] = streams[c][pos[c]:pos[c] + k]
+            pos[c] += len(reads[c])
+            uploaded += len(reads[c])
+        fr, st = sess.read(reads)
+        assert (st == cp.END_OF_STREAM).all(), st
+        for c, frames in fr.items():
+            got[c] += [bytes(x) for x in frames]
+    for c in range(n):
+        assert got[c] == expect[c], f"connection {c}"
+        assert sess.buffered(c) == 0 and sess.expected(c) == 0
+    assert sess.stats()["uploaded_bytes"] == uploaded == sum(len(s) for s in streams)
+    sess.close()
