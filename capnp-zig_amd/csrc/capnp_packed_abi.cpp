@@ -178,6 +178,11 @@ uint64_t unpack_bound(size_t n) { return n > (UINT64_MAX / 1024) ? UINT64_MAX : 
 // output comes back only when the unit is OK; *len_out is out_len (for OUT_OF_SPACE: the
 // size the unit needs).
 // reuse_in: the device already holds `in` from the previous call (a retry with a larger slot).
+// Single units up to these sizes take one kernel (cpk::launch_decode_one / launch_encode_one);
+// DESIGN.md §6.1 has the measured crossover.
+constexpr size_t kFastDecodeMax = 64 * 1024;  // packed bytes
+constexpr size_t kFastEncodeMax = 4096;       // unpacked bytes: one 512-word tile
+
 int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out,
                uint64_t* used_out = nullptr, bool reuse_in = false) {
     int st = g_ctx.init();
@@ -190,7 +195,13 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
     const bool write = (kind == 0 || kind == 1 || kind == 4);
     if (write && (st = g_ctx.reserve(&g_ctx.d_out, &g_ctx.out_cap, slot + 16))) return st;
     uint64_t* const hm = g_ctx.h_meta;
-    const uint64_t meta[7] = {0, n, 0, slot, 0, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status, consumed
+    // one kernel for a single unit the one-unit kernels take (kFastDecodeMax / kFastEncodeMax)
+    const bool one = n > 0 && ((kind == 1 && n <= kFastDecodeMax) || ((kind == 0 || kind == 3) && n <= kFastEncodeMax));
+    uint64_t meta[7] = {0, n, 0, slot, 0, 0, 0};  // in_off, in_len, out_off, out_cap, out_len, status, consumed
+    if (one && kind == 1) {
+        const int32_t need = cpk::decode_one_status();  // decode_wave_kernel<kWvMarked> takes marked units
+        std::memcpy(&meta[5], &need, sizeof(need));
+    }
     std::memcpy(hm, meta, sizeof(meta));
     hipStream_t s = g_ctx.stream;
     hipError_t e = hipSuccess;
@@ -202,7 +213,11 @@ int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot,
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(H2D)");
     uint64_t* m = g_ctx.d_meta;
     int32_t* d_status = reinterpret_cast<int32_t*>(m + 5);
-    if (kind == 0 || kind == 3)
+    if (one && kind == 1)
+        e = cpk::launch_decode_one(g_ctx.d_in, m, m + 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, s);
+    else if (one)
+        e = cpk::launch_encode_one(g_ctx.d_in, m, m + 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, s);
+    else if (kind == 0 || kind == 3)
         e = cpk::launch_encode(g_ctx.d_in, m, m + 1, 1, g_ctx.d_out, m + 2, m + 3, m + 4, d_status, write, nullptr, 0,
                                s);
     else if (kind == 4)

@@ -29,6 +29,15 @@ hipError_t release_stream(hipStream_t stream);
 void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept);
 
 // Reader.readPackedMessage over a batch of reader streams (reader.zig:84-156).
+// One unit (the single-buffer calls): the unit's status must be kStNeedFull (decode_one_status())
+// for decode_one; encode_one takes units of at most 512 words.
+int32_t decode_one_status();
+hipError_t launch_decode_one(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                             const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                             hipStream_t stream);
+hipError_t launch_encode_one(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                             const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                             bool write, hipStream_t stream);
 hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                                uint64_t* consumed, int32_t* status, hipStream_t stream);

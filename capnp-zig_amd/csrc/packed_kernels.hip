@@ -5036,7 +5036,7 @@ static std::atomic<int> g_decoder{CAPNP_PACKED_DECODER_AUTO};
 static std::atomic<int> g_small{1};
 static int small_variant() { return g_small.load(std::memory_order_relaxed); }
 int set_all_or_nothing(int on) { return g_small.exchange(on ? 0 : 1) == 0 ? 1 : 0; }
-static int decoder_variant() {
+[[maybe_unused]] static int decoder_variant() {
     const int v = g_decoder.load(std::memory_order_relaxed);
     return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
 }
@@ -5208,6 +5208,30 @@ hipError_t launch_message_init(const uint8_t* in, const uint64_t* in_off, const 
     if (n == 0) return hipSuccess;
     message_init_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, max_segs,
                                                                           seg_count, seg_off, seg_len, status);
+    return hipGetLastError();
+}
+
+// Single-buffer calls (one unit, capnp_packed_decode / capnp_packed_encode below 64 KiB / 4 KiB):
+// one kernel instead of the batch sequence (classes, side-stream fork and join, ~12 launches):
+// decode by the serial window walk of one wave (decode_wave_kernel<kWvMarked>: all-or-nothing,
+// any size, a window of 4.6 KB at a time), encode by the one-tile encoder.
+int32_t decode_one_status() { return kStNeedFull; }
+hipError_t launch_decode_one(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                             const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                             hipStream_t stream) {
+    decode_wave_kernel<kWvMarked><<<1, kWvBlock, 0, stream>>>(in, in_off, in_len, 1, out, out_off, out_cap, out_len,
+                                                               status, nullptr);
+    return hipGetLastError();
+}
+hipError_t launch_encode_one(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                             const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len, int32_t* status,
+                             bool write, hipStream_t stream) {
+    if (write)
+        encode_kernel<true><<<1, kBlock, 0, stream>>>(in, in_off, in_len, 1, out, out_off, out_cap, out_len, status,
+                                                        nullptr, nullptr);
+    else
+        encode_kernel<false><<<1, kBlock, 0, stream>>>(in, in_off, in_len, 1, out, out_off, out_cap, out_len, status,
+                                                         nullptr, nullptr);
     return hipGetLastError();
 }
 
