@@ -180,7 +180,7 @@ uint64_t unpack_bound(size_t n) { return n > (UINT64_MAX / 1024) ? UINT64_MAX : 
 // reuse_in: the device already holds `in` from the previous call (a retry with a larger slot).
 // Single units up to these sizes take one kernel (cpk::launch_decode_one / launch_encode_one);
 // DESIGN.md §6.1 has the measured crossover.
-constexpr size_t kFastDecodeMax = 64 * 1024;  // packed bytes
+constexpr size_t kFastDecodeMax = 24 * 1024;  // packed bytes (the serial window walk passes the batch path near 32 KB)
 constexpr size_t kFastEncodeMax = 4096;       // unpacked bytes: one 512-word tile
 
 int run_single(int kind, const uint8_t* in, size_t n, uint8_t* out, size_t slot, uint64_t* len_out,

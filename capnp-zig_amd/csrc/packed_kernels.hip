@@ -5211,7 +5211,7 @@ hipError_t launch_message_init(const uint8_t* in, const uint64_t* in_off, const 
     return hipGetLastError();
 }
 
-// Single-buffer calls (one unit, capnp_packed_decode / capnp_packed_encode below 64 KiB / 4 KiB):
+// Single-buffer calls (one unit, capnp_packed_decode / capnp_packed_encode up to 24 KiB / 4 KiB):
 // one kernel instead of the batch sequence (classes, side-stream fork and join, ~12 launches):
 // decode by the serial window walk of one wave (decode_wave_kernel<kWvMarked>: all-or-nothing,
 // any size, a window of 4.6 KB at a time), encode by the one-tile encoder.
