@@ -903,6 +903,9 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig:310)
 constexpr uint32_t kMsgOneSegs = 64;   // one-tile pass: a segment per lane (more: the tiled pass)
+#ifndef CPK_EM_MAP  // dev A/B: 1 = the one-tile gather finds segments through a per-word map
+#define CPK_EM_MAP 0
+#endif
 
 // PAD (the one-tile pass): the segments' word offsets and addresses live in the 16-B pads of the
 // tile's 80-B LDS rows (u32 slot s at row s / 4, bytes 64 + 4 (s % 4); offset s at slot s,
@@ -1088,6 +1091,97 @@ __device__ __forceinline__ void msg_stage_pairs(const MsgView<1>& m, uint32_t tw
     }
 }
 
+// One-tile pair gather with a per-word segment map: seg_of[p] (u8, payload word p -> its
+// segment + 1) is built once per message in the tile's row data (zeroed, each non-empty segment
+// marks its first word, a forward fill by lane and a wave max-scan: segment starts increase with
+// the index), so each pair finds its segments with one LDS byte read each and no search loop.
+// The map is read only while the addresses are formed, before any staged word is written.
+__device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_t tw, uint32_t lane, uint8_t* lds,
+                                                    uint32_t my_woff, bool my_mark) {
+    auto map_at = [&](uint32_t p) -> uint8_t* { return lds + (p >> 6) * kEncRow + (p & 63); };
+    *reinterpret_cast<uint64_t*>(lds + (lane >> 3) * kEncRow + 8 * (lane & 7)) = 0;  // words 8l .. 8l+7
+    wave_lds_sync();
+    if (my_mark) *map_at(my_woff) = (uint8_t)(lane + 1);
+    wave_lds_sync();
+    uint64_t v = *reinterpret_cast<const uint64_t*>(lds + (lane >> 3) * kEncRow + 8 * (lane & 7));
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // forward fill inside the lane's 8 words
+        const uint32_t b = (uint32_t)(v >> (8 * k)) & 0xFFu;
+        run = b ? b : run;
+        v = (v & ~(0xFFull << (8 * k))) | ((uint64_t)run << (8 * k));
+    }
+    const uint32_t before = wave_prev_lane(wave_incl_max(run, lane), 0u);  // marks increase with p
+    uint64_t fill = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t b = (uint32_t)(v >> (8 * k)) & 0xFFu;
+        fill |= (uint64_t)(b ? b : before) << (8 * k);
+    }
+    *reinterpret_cast<uint64_t*>(lds + (lane >> 3) * kEncRow + 8 * (lane & 7)) = fill;
+    wave_lds_sync();
+
+    const uint64_t* pa[4];
+    const uint64_t* pb[4];
+    uint64_t ha[4], hb[4];
+    bool pair[4];
+    uint32_t hh = 0;
+    auto addr = [&](uint32_t p, uint32_t sg) {  // payload word p in segment sg
+        return reinterpret_cast<const uint64_t*>(m.ba(sg) + 8ull * (p - m.wo(sg)));
+    };
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 2 * lane + 128 * j;
+        pa[j] = pb[j] = nullptr;
+        ha[j] = hb[j] = 0;
+        pair[j] = false;
+        if (i < tw) {
+            const bool two = i + 1 < tw;
+            // header words (at most 33) only in the first 128-word block
+            const bool hda = j == 0 && i < m.hw, hdb = j == 0 && i + 1 < m.hw;
+            uint32_t sa = 0;
+            if (hda) {
+                ha[j] = msg_word(m, i, hh);
+            } else {
+                const uint32_t p = i - m.hw;
+                sa = *map_at(p) - 1u;
+                pa[j] = addr(p, sa);
+            }
+            if (two) {
+                if (hdb) {
+                    hb[j] = msg_word(m, i + 1, hh);
+                } else {
+                    const uint32_t p = i + 1 - m.hw;
+                    const uint32_t sb = *map_at(p) - 1u;
+                    if (!hda && sb == sa) pair[j] = true;
+                    else pb[j] = addr(p, sb);
+                }
+            }
+        }
+    }
+    uint64_t xa[4], xb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (pair[j]) {
+            const u64x2_a8 w = gload16a8(pa[j]);
+            xa[j] = w.x;
+            xb[j] = w.y;
+        } else {
+            xa[j] = pa[j] ? gload8(pa[j]) : ha[j];
+            xb[j] = pb[j] ? gload8(pb[j]) : hb[j];
+        }
+    }
+    wave_lds_sync();  // every lane has read the map
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 2 * lane + 128 * j;
+        uint8_t* const d = lds + (i >> 3) * kEncRow + (i & 7) * 8;
+        if (i + 1 < tw) *reinterpret_cast<u32x4*>(d) = u32x4{(uint32_t)xa[j], (uint32_t)(xa[j] >> 32),
+                                                              (uint32_t)xb[j], (uint32_t)(xb[j] >> 32)};
+        else if (i < tw) *reinterpret_cast<uint64_t*>(d) = xa[j];
+    }
+}
+
 // One message of at most 64 segments and one framed tile (<= 512 words), a wave: lane s loads
 // segment s's length and address (two coalesced loads), a wave scan gives the word offsets, and
 // offsets and addresses go to the row pads (MsgView<1>); then the pair gather and encode_tile.
@@ -1145,7 +1239,11 @@ __device__ __forceinline__ void encode_message_tile1(uint32_t msg, uint32_t lane
     wave_lds_sync();
     const MsgView<1> m{reinterpret_cast<const uint32_t*>(lds), nullptr, count, hw};
     EM_T(e1);
+#if CPK_EM_MAP
+    msg_stage_pairs_map(m, words, lane, lds, incl - wl, lane < count && wl != 0);
+#else
     msg_stage_pairs(m, words, lane, lds);
+#endif
     wave_lds_sync();
     EM_T(e2);
     uint32_t cz = 0, cf = 0;
