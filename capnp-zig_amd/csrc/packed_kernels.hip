@@ -903,9 +903,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMsgMaxSegs = 512;  // Message.max_segment_count (message.zig:310)
 constexpr uint32_t kMsgOneSegs = 64;   // one-tile pass: a segment per lane (more: the tiled pass)
-#ifndef CPK_EM_MAP  // dev A/B: 1 = the one-tile gather finds segments through a per-word map
-#define CPK_EM_MAP 0
-#endif
+
 
 // PAD (the one-tile pass): the segments' word offsets and addresses live in the 16-B pads of the
 // tile's 80-B LDS rows (u32 slot s at row s / 4, bytes 64 + 4 (s % 4); offset s at slot s,
@@ -1022,80 +1020,16 @@ __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, ui
 }
 
 // One-tile staging by word pairs: lane l gathers framed words 2l + 128j and 2l + 1 + 128j with
-// one 16-B load when both lie in one segment (all but a segment's edges), else word by word,
-// and writes the pair to its row with one 16-B LDS store: half the load instructions and
-// address computations of msg_stage's word-per-load gather. All addresses first, then every
-// load, then the LDS stores, so the loads are in flight together.
-__device__ __forceinline__ void msg_stage_pairs(const MsgView<1>& m, uint32_t tw, uint32_t lane, uint8_t* lds) {
-    const uint64_t* pa[4];
-    const uint64_t* pb[4];
-    uint64_t ha[4], hb[4];
-    bool pair[4];
-    uint32_t hint = 0xFFFFFFFFu, hh = 0;
-    uint32_t wlo = 1, whi = 0;  // cached segment window [wlo, whi) of payload words (empty)
-    uint64_t wbase = 0;
-    auto seek = [&](uint32_t p) {  // address of payload word p (window cached)
-        if (p < wlo || p >= whi) {
-            if (hint >= m.count || p < m.wo(hint)) {
-                uint32_t lo = 0, hi = m.count;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (m.wo(mid) <= p) lo = mid;
-                    else hi = mid;
-                }
-                hint = lo;
-            }
-            while (p >= m.wo(hint + 1)) ++hint;
-            wlo = m.wo(hint);
-            whi = m.wo(hint + 1);
-            wbase = m.ba(hint);
-        }
-        return reinterpret_cast<const uint64_t*>(wbase + 8ull * (p - wlo));
-    };
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 2 * lane + 128 * j;
-        pa[j] = pb[j] = nullptr;
-        ha[j] = hb[j] = 0;
-        pair[j] = false;
-        if (i < tw) {
-            const bool two = i + 1 < tw;
-            if (i < m.hw) ha[j] = msg_word(m, i, hh);  // header word (no load)
-            else pa[j] = seek(i - m.hw);
-            if (two) {
-                if (i + 1 < m.hw) hb[j] = msg_word(m, i + 1, hh);
-                else if (i >= m.hw && i + 1 - m.hw < whi) pair[j] = true;  // same segment as word a
-                else pb[j] = seek(i + 1 - m.hw);
-            }
-        }
-    }
-    uint64_t xa[4], xb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (pair[j]) {
-            const u64x2_a8 v = gload16a8(pa[j]);
-            xa[j] = v.x;
-            xb[j] = v.y;
-        } else {
-            xa[j] = pa[j] ? gload8(pa[j]) : ha[j];
-            xb[j] = pb[j] ? gload8(pb[j]) : hb[j];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 2 * lane + 128 * j;
-        uint8_t* const d = lds + (i >> 3) * kEncRow + (i & 7) * 8;
-        if (i + 1 < tw) *reinterpret_cast<u32x4*>(d) = u32x4{(uint32_t)xa[j], (uint32_t)(xa[j] >> 32),
-                                                              (uint32_t)xb[j], (uint32_t)(xb[j] >> 32)};
-        else if (i < tw) *reinterpret_cast<uint64_t*>(d) = xa[j];
-    }
-}
-
-// One-tile pair gather with a per-word segment map: seg_of[p] (u8, payload word p -> its
-// segment + 1) is built once per message in the tile's row data (zeroed, each non-empty segment
-// marks its first word, a forward fill by lane and a wave max-scan: segment starts increase with
-// the index), so each pair finds its segments with one LDS byte read each and no search loop.
-// The map is read only while the addresses are formed, before any staged word is written.
+// one 16-B load when both lie in one segment (all but the segments' edges and the header), else
+// word by word, and writes the pair to its row with one 16-B LDS store: half the load
+// instructions of msg_stage's word-per-load gather. All addresses first, then every load, then
+// the LDS stores, so the loads are in flight together. Segments are found through a per-word
+// map, seg_of[p] (u8, payload word p -> its segment + 1), built once per message in the tile's
+// row data (zeroed, each non-empty segment marks its first word, a forward fill by lane and a
+// wave max-scan: segment starts increase with the index): one LDS byte read per word and no
+// search loop (a per-lane search with a cached window measured 2.37-2.38 ms on the framing leg
+// against 2.16 ms, same box). The map is read only while the addresses are formed, before any
+// staged word is written.
 __device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_t tw, uint32_t lane, uint8_t* lds,
                                                     uint32_t my_woff, bool my_mark) {
     auto map_at = [&](uint32_t p) -> uint8_t* { return lds + (p >> 6) * kEncRow + (p & 63); };
@@ -1239,11 +1173,7 @@ __device__ __forceinline__ void encode_message_tile1(uint32_t msg, uint32_t lane
     wave_lds_sync();
     const MsgView<1> m{reinterpret_cast<const uint32_t*>(lds), nullptr, count, hw};
     EM_T(e1);
-#if CPK_EM_MAP
     msg_stage_pairs_map(m, words, lane, lds, incl - wl, lane < count && wl != 0);
-#else
-    msg_stage_pairs(m, words, lane, lds);
-#endif
     wave_lds_sync();
     EM_T(e2);
     uint32_t cz = 0, cf = 0;
