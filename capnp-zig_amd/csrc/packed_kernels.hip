@@ -1260,8 +1260,12 @@ __global__ __launch_bounds__(kBlock) void encode_message_pf_kernel(const uint64_
                 ncap = out_cap[nx];
             }
         }
-        encode_message_tile1_body<WRITE>(msg, lane, lut, lds, c_in, len, ptr, ob, cap, out, out_len, status, [&] {
-            if (more && nc && nc <= kMsgOneSegs && lane < nc) {
+        // lane-derived values recomputed per message, not hoisted out of the loop and held in
+        // registers (the hoisted form spilled its SGPRs into VGPR lanes: 131 VGPRs)
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        encode_message_tile1_body<WRITE>(msg, ln, lut, lds, c_in, len, ptr, ob, cap, out, out_len, status, [&] {
+            if (more && nc && nc <= kMsgOneSegs && ln < nc) {
                 nlen = seg_len[nfirst + lane];
                 nptr = seg_ptr[nfirst + lane];
             }
