@@ -1122,14 +1122,15 @@ __device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_
 // Anything else (more segments or words, and the argument checks that come with them) is
 // marked for the tiled pass (kStNeedFull), which applies toBytes' checks in the reference order.
 // The message once its table is in registers: c_in segments (uniform), lane s holding segment
-// s's length and address; next() is called once, after this message's data loads have landed
-// (or on a decline), so a persistent caller can issue the next message's table loads there.
-template <bool WRITE, typename Next>
+// s's length and address. (A persistent form that loaded the next message's table while this
+// one was coded ran at 91 VGPRs, 5 waves/SIMD, and took 2.48-2.50 ms on the framing leg against
+// 2.15-2.16 ms for this one at 7: DESIGN.md §2.5.)
+template <bool WRITE>
 __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t lane, const uint64_t* lut,
                                                           uint8_t* lds, uint32_t c_in, uint64_t len, uint64_t ptr,
                                                           uint64_t ob, uint64_t cap, uint8_t* __restrict__ out,
                                                           uint64_t* __restrict__ out_len,
-                                                          int32_t* __restrict__ status, Next next) {
+                                                          int32_t* __restrict__ status) {
     EM_T(e0);
     const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
     // segments are whole words at 8-B aligned addresses (a MessageBuilder's always are); any
@@ -1138,7 +1139,6 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
     const bool big = (len >> 3) > kEncMaxWords;
     if (count > kMsgOneSegs || __builtin_amdgcn_ballot_w64(odd || big) != 0) {
         if (lane == 0) status[msg] = kStNeedFull;  // the tiled pass reports ST_ARG / codes it
-        next();
         return;
     }
     const uint32_t wl = (uint32_t)(len >> 3);
@@ -1148,10 +1148,8 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
     const uint32_t words = hw + payload;
     if (words > kEncMaxWords) {
         if (lane == 0) status[msg] = kStNeedFull;
-        next();
         return;
     }
-    wave_lds_sync();  // a persistent wave's previous message is done with the slice
     if (lane < count) {
         *reinterpret_cast<uint32_t*>(msg_pad(lds, lane)) = incl - wl;
         *reinterpret_cast<uint64_t*>(msg_pad(lds, 128 + 2 * lane)) = ptr;
@@ -1163,7 +1161,6 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
     msg_stage_pairs_map(m, words, lane, lds, incl - wl, lane < count && wl != 0);
     wave_lds_sync();
     EM_T(e2);
-    next();
     uint32_t cz = 0, cf = 0;
     const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
     EM_T(e3);
@@ -1198,88 +1195,9 @@ __device__ __forceinline__ void encode_message_tile1(uint32_t msg, uint32_t lane
         ob = out_off[msg];
         cap = out_cap[msg];
     }
-    encode_message_tile1_body<WRITE>(msg, lane, lut, lds, c_in, len, ptr, ob, cap, out, out_len, status, [] {});
+    encode_message_tile1_body<WRITE>(msg, lane, lut, lds, c_in, len, ptr, ob, cap, out, out_len, status);
 }
 
-// Persistent form (dev macro CPK_EM_PF2 until measured): each wave codes messages w, w + G, ...
-// The next message's count / first index / slot (scalar loads) are issued at the top of a
-// message, its segment lengths and addresses once this message's words are staged, so they land
-// while this message is coded: a message's data loads then wait for one level, not two.
-#ifndef CPK_EM_PF2
-#define CPK_EM_PF2 0
-#endif
-#ifndef CPK_EM_PF2_BLOCKS  // dev: cap the persistent grid (1 makes the tests' waves loop)
-#define CPK_EM_PF2_BLOCKS 0
-#endif
-#if CPK_EM_PF2
-template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void encode_message_pf_kernel(const uint64_t* __restrict__ seg_ptr,
-                                                                   const uint64_t* __restrict__ seg_len,
-                                                                   const uint32_t* __restrict__ seg_first,
-                                                                   const uint32_t* __restrict__ seg_count, uint32_t n,
-                                                                   uint8_t* __restrict__ out,
-                                                                   const uint64_t* __restrict__ out_off,
-                                                                   const uint64_t* __restrict__ out_cap,
-                                                                   uint64_t* __restrict__ out_len,
-                                                                   int32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint64_t lut[256];
-    const uint32_t lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WRITE) {
-        lut[threadIdx.x] = compact_selector(threadIdx.x);
-        __syncthreads();
-    }
-    uint8_t* const lds = smem + wave * kEncLds;
-    const uint32_t G = gridDim.x * kWavesPerBlock;
-    uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
-    if (msg >= n) return;  // wave-uniform
-    uint32_t c_in = seg_count[msg];
-    uint64_t len = 0, ptr = 0, ob = 0, cap = 0;
-    {
-        const uint32_t first = seg_first[msg];
-        if (c_in && c_in <= kMsgOneSegs && lane < c_in) {
-            len = seg_len[first + lane];
-            ptr = seg_ptr[first + lane];
-        }
-        if (WRITE) {
-            ob = out_off[msg];
-            cap = out_cap[msg];
-        }
-    }
-    for (;;) {
-        const bool more = (uint64_t)msg + G < n;  // wave-uniform
-        const uint32_t nx = more ? msg + G : msg;
-        uint32_t nc = 0, nfirst = 0;
-        uint64_t nob = 0, ncap = 0, nlen = 0, nptr = 0;
-        if (more) {
-            nc = seg_count[nx];
-            nfirst = seg_first[nx];
-            if (WRITE) {
-                nob = out_off[nx];
-                ncap = out_cap[nx];
-            }
-        }
-        // lane-derived values recomputed per message, not hoisted out of the loop and held in
-        // registers (the hoisted form spilled its SGPRs into VGPR lanes: 131 VGPRs)
-        uint32_t ln = lane;
-        asm volatile("" : "+v"(ln));
-        encode_message_tile1_body<WRITE>(msg, ln, lut, lds, c_in, len, ptr, ob, cap, out, out_len, status, [&] {
-            if (more && nc && nc <= kMsgOneSegs && ln < nc) {
-                nlen = seg_len[nfirst + lane];
-                nptr = seg_ptr[nfirst + lane];
-            }
-        });
-        if (!more) break;
-        msg = nx;
-        c_in = nc;
-        len = nlen;
-        ptr = nptr;
-        ob = nob;
-        cap = ncap;
-    }
-}
-#endif
 
 // One message (see encode_message_kernel); lds / woff / base are the wave's slices.
 template <bool WRITE, bool TILED>
@@ -5308,26 +5226,6 @@ hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_le
     if (n == 0) return hipSuccess;
     // every message, then the marked multi-tile ones (a grid striding over the statuses)
     const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
-#if CPK_EM_PF2
-    {  // one-tile messages by the persistent prefetching pass
-        static const uint32_t pf_res = resident_blocks(encode_message_pf_kernel<true>, kBlock, 7);
-        const uint32_t pf_blocks = CPK_EM_PF2_BLOCKS ? CPK_EM_PF2_BLOCKS : std::min(blocks_for(n), pf_res);
-        if (write)
-            encode_message_pf_kernel<true><<<pf_blocks, kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count, n,
-                                                                             out, out_off, out_cap, out_len, status);
-        else
-            encode_message_pf_kernel<false><<<pf_blocks, kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count,
-                                                                              n, out, out_off, out_cap, out_len, status);
-        const uint32_t tb = tiled_blocks;
-        if (write)
-            encode_message_kernel<true, true><<<tb, kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count, n, out,
-                                                                          out_off, out_cap, out_len, status);
-        else
-            encode_message_kernel<false, true><<<tb, kBlock, 0, stream>>>(seg_ptr, seg_len, seg_first, seg_count, n,
-                                                                           out, out_off, out_cap, out_len, status);
-        return hipGetLastError();
-    }
-#endif
     if (write) {
         encode_message_kernel<true, false><<<blocks_for(n), kBlock, 0, stream>>>(
                 seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
