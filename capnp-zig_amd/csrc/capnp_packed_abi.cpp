@@ -701,6 +701,8 @@ struct capnp_packed_framer {
     uint64_t stage_cap = 0;
     uint8_t* d_frames = nullptr;
     uint64_t frames_dcap = 0;
+    uint8_t* d_spec = nullptr;  // the walk's window tables (cpk::launch_frame_walk)
+    uint64_t spec_cap = 0;
     uint64_t uploaded = 0, moved = 0;  // bytes copied H2D (new reads) and moved between regions
 
     ~capnp_packed_framer() {
@@ -709,6 +711,7 @@ struct capnp_packed_framer {
         if (d_state) (void)hipFree(d_state);
         if (d_stage) (void)hipFree(d_stage);
         if (d_frames) (void)hipFree(d_frames);
+        if (d_spec) (void)hipFree(d_spec);
         if (s) (void)hipStreamDestroy(s);
     }
     static int grow(uint8_t** p, uint64_t* c, uint64_t need) {
@@ -946,6 +949,9 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
     int32_t* const d_st = reinterpret_cast<int32_t*>(d_base + 6ull * n);
     // round scratch past the copy-job area would be reallocated by run_jobs; a separate block:
     std::vector<uint64_t> h(6ull * n), hm(7ull * n);
+    std::vector<uint32_t> spec_h;  // window tables' first / count per listed connection
+    std::vector<uint64_t> spec_h64;  // their bytes: arena offset, length
+    uint64_t spec_T = 0;
     std::vector<int32_t> hst(n);
     std::vector<uint32_t> list;
     std::vector<uint8_t> dead(n, 0);  // an error this call: the connection was reset
@@ -1014,10 +1020,48 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
             h[4ull * n + c] = f->W[c];
         }
         uint32_t* const r_list = reinterpret_cast<uint32_t*>(r_in_off + 7ull * (n + 1));
+        // window tables for the connections whose bytes past the walk's start span more than
+        // one window (a message split over many reads: its new bytes are crossed by lookups)
+        const uint64_t wb = cpk::framer_window_bytes(), wcap = cpk::framer_window_cap(k);
+        spec_h.assign(2ull * k, 0);  // first, count per listed connection (u32); off, len (u64) below
+        spec_h64.assign(2ull * k, 0);
+        uint64_t T = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t c = list[j];
+            const uint64_t span = f->len[c] - f->m0[c] - f->X[c];
+            uint64_t cnt = span > wb ? (span + wb - 1) / wb : 0;
+            if (T + cnt > wcap) cnt = 0;
+            spec_h[j] = cnt ? (uint32_t)T : 0xFFFFFFFFu;
+            spec_h[k + j] = (uint32_t)cnt;
+            spec_h64[j] = f->off[c] + f->m0[c] + f->X[c];
+            spec_h64[k + j] = span;
+            T += cnt;
+        }
+        uint32_t* d_sq = nullptr;
+        const uint32_t *d_sfirst = nullptr, *d_scount = nullptr;
+        const uint64_t *d_soff = nullptr, *d_slen = nullptr;
+        if (T) {
+            const uint64_t qb = (cpk::framer_spec_bytes(k, T) + 15) & ~15ull;
+            const uint64_t ab = (8ull * k + 15) & ~15ull;
+            if ((st = capnp_packed_framer::grow(&f->d_spec, &f->spec_cap, qb + ab + 16ull * k + 64))) return st;
+            d_sq = reinterpret_cast<uint32_t*>(f->d_spec);
+            uint32_t* const a32 = reinterpret_cast<uint32_t*>(f->d_spec + qb);
+            uint64_t* const a64 = reinterpret_cast<uint64_t*>(f->d_spec + qb + ab);
+            d_sfirst = a32;
+            d_scount = a32 + k;
+            d_soff = a64;
+            d_slen = a64 + k;
+            spec_T = T;
+            e = hipMemcpyAsync(d_sq + 8, &spec_T, 8, hipMemcpyHostToDevice, s);  // q_tiles: the windows
+            if (e == hipSuccess) e = hipMemcpyAsync(a32, spec_h.data(), 8ull * k, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(a64, spec_h64.data(), 16ull * k, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) return hip_fail(e, "framer window tables");
+        }
         e = hipMemcpyAsync(d_base, h.data(), 5ull * n * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(r_list, list.data(), 4ull * k, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)
-            e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_cons, d_st, s);
+            e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_cons, d_st, d_sq, T,
+                                       d_sfirst, d_scount, d_soff, d_slen, s);
         if (e == hipSuccess) e = hipMemcpyAsync(h.data() + 3ull * n, d_X, 3ull * n * 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), d_st, 4ull * n, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -48,9 +48,18 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
 hipError_t launch_copy_jobs(const uint64_t* jobs, uint32_t nj, hipStream_t stream);
 hipError_t launch_read_header(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                               uint64_t* out_len, uint64_t* consumed, int32_t* status, hipStream_t stream);
+// Framer walk (capnp_packed_framer_read): spec_q (framer_spec_bytes(nl, windows) bytes, u64 at
+// u32 index 8 = windows) holds the window tables of the listed connections whose held bytes
+// span more than one window (spec_first / spec_count per list entry, spec_off / spec_len their
+// bytes from the walk's start); spec_q null or windows 0: every window walked exactly.
+size_t framer_spec_bytes(uint32_t nl, uint64_t windows);
+uint32_t framer_window_bytes();            // the windows' size (kWvWin)
+uint64_t framer_window_cap(uint32_t nl);   // windows a spec table of nl connections may hold
 hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_t nl, const uint64_t* base,
                              const uint64_t* avail, const uint64_t* need, uint64_t* X, uint64_t* W,
-                             uint64_t* consumed, int32_t* status, hipStream_t stream);
+                             uint64_t* consumed, int32_t* status, uint32_t* spec_q, uint64_t windows,
+                             const uint32_t* spec_first, const uint32_t* spec_count, const uint64_t* spec_off,
+                             const uint64_t* spec_len, hipStream_t stream);
 
 // MessageBuilder.toPackedBytes from segment lists (message.zig:2123-2179).
 hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_len, const uint32_t* seg_first,

@@ -4534,7 +4534,9 @@ __global__ __launch_bounds__(kWvBlock) void frame_walk_kernel(const uint8_t* __r
                                                               const uint64_t* __restrict__ need,
                                                               uint64_t* __restrict__ Xs, uint64_t* __restrict__ Ws,
                                                               uint64_t* __restrict__ consumed,
-                                                              int32_t* __restrict__ status) {
+                                                              int32_t* __restrict__ status,
+                                                              const WinEnt* __restrict__ spec,
+                                                              const uint32_t* __restrict__ spec_first) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
     __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
     const uint32_t lane = lane_id();
@@ -4549,10 +4551,37 @@ __global__ __launch_bounds__(kWvBlock) void frame_walk_kernel(const uint8_t* __r
         uint64_t x = Xs[c], wd = Ws[c];
         int32_t st = ST_EOS;
         uint64_t cons = 0;
+        // windows at fixed positions x0 + j * kWvWin; with a spec table (window_spec_kernel over
+        // [x0, P), computed for all windows at once), a window the message neither ends in nor
+        // runs out of bytes in is crossed by a table lookup: its exit and word count from the
+        // entry d the chain arrives at
+        const uint64_t x0 = x;
+        const uint32_t sf = spec_first ? __builtin_amdgcn_readfirstlane(spec_first[i]) : kWinNone;
         while (x < P) {
-            const WvWin w = wv_stage(pk, mk, src, P, x, lane);
+            const uint64_t j = (x - x0) / kWvWin;
+            const uint64_t Xj = x0 + j * kWvWin;
+            const uint32_t d = (uint32_t)(x - Xj);
+            if (sf != kWinNone) {
+                const WinEnt* const e = spec + sf + j;
+                const uint64_t vm = e->valid;
+                if (d < kWinD && ((vm >> d) & 1)) {
+                    const int32_t dl = e->delta[d];
+                    const uint32_t ex = e->exit;
+                    if (dl != kDeltaEof && ex != kEOFX) {
+                        const uint64_t words = (uint64_t)((int64_t)e->total + dl);
+                        if (wd + words < Lw) {
+                            wd += words;
+                            x = Xj + ex;
+                            continue;
+                        }
+                    }
+                }
+            }
+            // the window walked exactly from entry d: the message ends in it, the held bytes end
+            // in it, or the table does not know entry d
+            const WvWin w = wv_stage(pk, mk, src, P, Xj, lane);
             uint32_t ent, cs, ce;
-            const uint32_t xw = wv_resolve(pk, mk, w, 0, lane, ent, cs, ce);
+            const uint32_t xw = wv_resolve(pk, mk, w, d, lane, ent, cs, ce);
             // the lane's complete records (a record past the held bytes ends the chain)
             uint32_t words = 0, stop = kEOFX;
             for (uint32_t r = ent; r < ce;) {
@@ -4589,18 +4618,18 @@ __global__ __launch_bounds__(kWvBlock) void frame_walk_kernel(const uint8_t* __r
                 }
                 end = readlane(end, f);
                 over = readlane(over, f);
-                cons = x + end;
+                cons = Xj + end;
                 st = over ? ST_OVERSHOOT : ST_OK;
                 wd = Lw;
                 break;
             }
             if (xw == kEOFX) {  // the chain stops at a record the bytes do not hold yet
                 const uint64_t bm = __ballot(stop != kEOFX);
-                x += bm ? readlane(stop, (uint32_t)__builtin_ctzll(bm)) : 0u;
+                x = bm ? Xj + readlane(stop, (uint32_t)__builtin_ctzll(bm)) : x;
                 wd += total;
                 break;
             }
-            x += xw;
+            x = Xj + xw;
             wd += total;
         }
         if (lane == 0) {
@@ -5309,13 +5338,41 @@ hipError_t launch_read_header(const uint8_t* in, const uint64_t* in_off, const u
     return hipGetLastError();
 }
 
+// The framer's window table: entry g of list connection i's windows names i as its unit and
+// its first window (window_spec_kernel's WinEnt.unit / .first).
+__global__ __launch_bounds__(256) void framer_windows_kernel(const uint32_t* __restrict__ first,
+                                                             const uint32_t* __restrict__ count, uint32_t nl,
+                                                             uint32_t* q, uint32_t nq) {
+    WinEnt* const tab = win_tab(q, nq);
+    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x)
+        for (uint32_t w = threadIdx.x; w < count[i]; w += blockDim.x) {
+            tab[first[i] + w].unit = i;
+            tab[first[i] + w].first = first[i];
+        }
+}
+
+size_t framer_spec_bytes(uint32_t nl, uint64_t windows) { return 4 * win_tab_off(nl) + sizeof(WinEnt) * windows; }
+uint32_t framer_window_bytes() { return kWvWin; }
+uint64_t framer_window_cap(uint32_t nl) { return win_cap(nl); }
+
 hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_t nl, const uint64_t* base,
                              const uint64_t* avail, const uint64_t* need, uint64_t* X, uint64_t* W,
-                             uint64_t* consumed, int32_t* status, hipStream_t stream) {
+                             uint64_t* consumed, int32_t* status, uint32_t* spec_q, uint64_t windows,
+                             const uint32_t* spec_first, const uint32_t* spec_count, const uint64_t* spec_off,
+                             const uint64_t* spec_len, hipStream_t stream) {
     if (nl == 0) return hipSuccess;
+    const WinEnt* spec = nullptr;
+    if (spec_q && windows) {  // spec tables of every listed connection's windows, in parallel
+        framer_windows_kernel<<<std::min(nl, 1024u), 256, 0, stream>>>(spec_first, spec_count, nl, spec_q, nl);
+        static const uint32_t spec_res = resident_blocks(window_spec_kernel, kWvBlock, 4);
+        const uint32_t sb = (uint32_t)std::min<uint64_t>((windows + kWvWaves - 1) / kWvWaves, spec_res);
+        window_spec_kernel<<<sb, kWvBlock, 0, stream>>>(arena, spec_off, spec_len, nl, spec_q);
+        spec = reinterpret_cast<const WinEnt*>(spec_q + win_tab_off(nl));
+    }
     static const uint32_t res = resident_blocks(frame_walk_kernel, kWvBlock, 2);
     const uint32_t blocks = std::min((nl + kWvWaves - 1) / kWvWaves, res);
-    frame_walk_kernel<<<blocks, kWvBlock, 0, stream>>>(arena, list, nl, base, avail, need, X, W, consumed, status);
+    frame_walk_kernel<<<blocks, kWvBlock, 0, stream>>>(arena, list, nl, base, avail, need, X, W, consumed, status,
+                                                        spec, spec ? spec_first : nullptr);
     return hipGetLastError();
 }
 
