@@ -1033,6 +1033,8 @@ __device__ __forceinline__ void msg_stage(const MsgView<PAD>& m, uint32_t tb, ui
 __device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_t tw, uint32_t lane, uint8_t* lds,
                                                     uint32_t my_woff, bool my_mark) {
     auto map_at = [&](uint32_t p) -> uint8_t* { return lds + (p >> 6) * kEncRow + (p & 63); };
+    const bool one = m.count == 1;  // wave-uniform: a one-segment message needs no map
+    if (!one) {
     *reinterpret_cast<uint64_t*>(lds + (lane >> 3) * kEncRow + 8 * (lane & 7)) = 0;  // words 8l .. 8l+7
     wave_lds_sync();
     if (my_mark) *map_at(my_woff) = (uint8_t)(lane + 1);
@@ -1054,6 +1056,7 @@ __device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_
     }
     *reinterpret_cast<uint64_t*>(lds + (lane >> 3) * kEncRow + 8 * (lane & 7)) = fill;
     wave_lds_sync();
+    }
 
     const uint64_t* pa[4];
     const uint64_t* pb[4];
@@ -1078,7 +1081,7 @@ __device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_
                 ha[j] = msg_word(m, i, hh);
             } else {
                 const uint32_t p = i - m.hw;
-                sa = *map_at(p) - 1u;
+                sa = one ? 0u : *map_at(p) - 1u;
                 pa[j] = addr(p, sa);
             }
             if (two) {
@@ -1086,7 +1089,7 @@ __device__ __forceinline__ void msg_stage_pairs_map(const MsgView<1>& m, uint32_
                     hb[j] = msg_word(m, i + 1, hh);
                 } else {
                     const uint32_t p = i + 1 - m.hw;
-                    const uint32_t sb = *map_at(p) - 1u;
+                    const uint32_t sb = one ? 0u : *map_at(p) - 1u;
                     if (!hda && sb == sa) pair[j] = true;
                     else pb[j] = addr(p, sb);
                 }
