@@ -140,3 +140,34 @@ def test_decoded_size_batch_mixed_classes():
         es, en = oracle.decoded_size(p)
         assert int(st[i]) == es, (i, len(p))
         assert int(out_len[i]) == (en if es == 0 else 0), (i, len(p))
+
+
+def test_one_kernel_paths_around_their_limits():
+    """Single-buffer decode up to 24 KiB of packed bytes and encode up to 4 KiB take one kernel
+    (launch_decode_one / launch_encode_one); around both limits, at three
+    densities, with truncations, a short capacity, a zero-heavy unit whose first 4x guess is too
+    small, and an encode input that is not whole words: every result as the oracle's."""
+    rng = np.random.default_rng(0x51)
+    for thr in (26, 128, 230):
+        for target in (24 * 1024 - 8, 24 * 1024, 24 * 1024 + 8):
+            # grow the unpacked size until the packed size crosses the decode limit
+            nbytes = 8 * int(target / 8 / {26: 1.03, 128: 0.63, 230: 0.24}[thr])
+            data = message(nbytes, thr, seed=0xC0DE0B40 + thr + target)
+            _, packed = oracle.pack(data)
+            assert cp.unpack_packed(packed) == data, (thr, len(packed))
+            st, n, out = decode_raw(packed, len(data))
+            assert (st, n) == (cp.OK, len(data)) and out == data
+            st, n, out = decode_raw(packed, len(data) - 8)
+            assert (st, n) == (cp.OUT_OF_SPACE, len(data)) and out == bytes([0xAB]) * (len(data) - 8)
+            p = packed[:-int(rng.integers(1, 12))]
+            exp, esize = oracle.decoded_size(p)
+            st, n, _ = decode_raw(p, len(data))
+            assert st == (cp.UNEXPECTED_EOF if exp == oracle.UNEXPECTED_EOF else cp.OK)
+    zeros = bytes(64 << 10)  # 2 packed bytes per 256 words: far past the 4x first guess
+    _, pz = oracle.pack(zeros)
+    assert len(pz) < 24 * 1024 and cp.unpack_packed(pz) == zeros
+    for nbytes in (0, 8, 4088, 4096, 4104, 8192):
+        data = message(nbytes, 128, seed=0xC0DE0B60 + nbytes) if nbytes else b""
+        assert cp.pack_packed(data) == oracle.pack(data)[1], nbytes
+    with pytest.raises(cp.InvalidMessageSize):
+        cp.pack_packed(bytes(4092))
