@@ -2594,6 +2594,24 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// s_waitcnt needs an immediate: wait until at most min(c, 63) vector-memory operations are
+// outstanding (fewer than the true number of younger operations only waits longer).
+__device__ __forceinline__ void vmcnt_at_most63(uint32_t c) {
+#define CPK_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define CPK_VM8(B) CPK_VM(B) CPK_VM(B + 1) CPK_VM(B + 2) CPK_VM(B + 3) CPK_VM(B + 4) CPK_VM(B + 5) CPK_VM(B + 6) CPK_VM(B + 7)
+    switch (c < 63u ? c : 63u) {
+        CPK_VM8(0) CPK_VM8(8) CPK_VM8(16) CPK_VM8(24) CPK_VM8(32) CPK_VM8(40) CPK_VM8(48)
+        CPK_VM(56) CPK_VM(57) CPK_VM(58) CPK_VM(59) CPK_VM(60) CPK_VM(61) CPK_VM(62)
+        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    }
+#undef CPK_VM8
+#undef CPK_VM
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return __builtin_amdgcn_readlane(wave_incl_max(v, 0), kWave - 1);
+}
+
 // The single-read mid-unit decoders (fused, round 3; streaming, round 4) measured slower than
 // the two-pass decoder and live in a dev build only.
 #ifndef CPK_DEV_DECODERS
@@ -2631,7 +2649,8 @@ constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
 __device__ __forceinline__ uint32_t* q_blocks(uint32_t* q, uint32_t n) { return q + kQHead + 3ull * n; }
 
 // KIND 0: encode, 1: decode (small lane kernel + indexed / fused mid decoders), 2: decoded size
-// (no output: long by packed length alone), 3: decode by the streaming decoder (no small class)
+// (no output: long by packed length alone), 3: decode by the streaming decoder (no small class),
+// 4: encode with the streaming small-unit encoder (mid units bin 0, small units bins 4 .. 7)
 template <int KIND>
 __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
@@ -2642,10 +2661,13 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
         if (len > 0 && ((s + len + 15) >> 4) > kFlPieces) return len > kQHuge ? CL_HUGE : CL_LONG;
         return CL_MID;
     }
-    if (KIND == 0) {
+    if (KIND == 0 || KIND == 4) {
         if (encode_tiled_unit(in, off, len)) return len > kQHuge ? CL_HUGE : CL_LONG;
         const bool valid = !(reinterpret_cast<uintptr_t>(in + off) & 7) && !(len & 7);
-        return (!valid || (len >> 3) <= kSmEncWords) ? CL_SMALL : CL_MID;
+        const bool small = !valid || (len >> 3) <= kSmEncWords;
+        if (KIND == 0) return small ? CL_SMALL : CL_MID;
+        const uint64_t w = len >> 3;
+        return !small ? CL_MID : CL_MID + 4 + (valid && w > 8) + (valid && w > 16) + (valid && w > 32);
     }
     const uint64_t cap = out_cap[u];
     if (KIND == 3) {
@@ -3253,6 +3275,251 @@ __global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __
         uint64_t* const dst = reinterpret_cast<uint64_t*>(out + out_off[unit]) + wb;
         wv_expand(pk, mk, lut, w, ent, ce, incl - words, incl, total, dst, lane);
     }
+}
+
+// ---- small units, streaming encoder (round 4) -----------------------------
+// Lane per unit, 64 units per wave in lockstep rounds of 8 words, as decode_stream_kernel:
+// round k's 64-B blocks of the wave's units come in by quad-coalesced 16-B loads issued a
+// round ahead (a unit's block is read in one line fetch, at full occupancy: the persistent
+// lane kernel below re-fetched lines its lanes had read, ~4.5x its input), land in the
+// units' 64-B LDS rings, and each lane codes its unit's 8 words with the Zig encoder's word
+// step (message.zig:200-271; the small kernel's predicated state machine: a zero run is
+// emitted when it ends, a literal run's count byte patched when it ends). A step completes at
+// most one 16-B output chunk, which the lane stores at once (counted global stores); a chunk
+// completed in one round sits next to its neighbours of the previous one, so lines fill up in
+// L2 within a round or two. The small units come binned by length (<= 8, 16, 32, 64 words:
+// 1, 2, 4 or 8 rounds; unit_class<4>), so a wave's units take about as many rounds.
+#ifndef CPK_ES_STREAM  // dev A/B: 1 = small units by encode_stream_kernel, 0 = encode_small_kernel
+#define CPK_ES_STREAM 0
+#endif
+constexpr bool kEsStream = CPK_ES_STREAM;
+constexpr uint32_t kEsWaves = 4;
+constexpr uint32_t kEsBins = 4;   // small-unit bins of unit_class<4>: mid list bins 4 .. 7
+constexpr uint32_t kEsRing = 80;  // ring row per unit: 64 B + 16 B pad (spreads the lanes' banks)
+
+// AS1 (global) byte / 16-B stores: generic pointers would make FLAT instructions, which also
+// count on lgkmcnt (every LDS wait of the loop would wait for them).
+__device__ __forceinline__ void es_store16(uint8_t* p, uint64_t x0, uint64_t x1) {
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p),
+                 "v"(u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)})
+                 : "memory");
+}
+__device__ __forceinline__ void es_store_byte(uint8_t* p, uint32_t v) {
+    *reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(reinterpret_cast<uintptr_t>(p)) = (uint8_t)v;
+}
+// bytes [lo, hi) of a 16-B chunk at c16 (x0 = bytes 0-7, x1 = 8-15), global stores
+__device__ __forceinline__ void es_store_partial16(uint8_t* c16, uint32_t lo, uint32_t hi, uint64_t x0, uint64_t x1) {
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    typedef __attribute__((address_space(1))) uint16_t g16;
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    typedef __attribute__((address_space(1))) uint64_t g64;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(c16);
+    auto put = [&](uint32_t sz) {  // bytes [lo, lo + sz), lo aligned to sz
+        const uint64_t v = lo < 8 ? x0 >> (8 * lo) : x1 >> (8 * (lo - 8));
+        const uintptr_t p = base + lo;
+        if (sz == 8) *reinterpret_cast<g64*>(p) = v;
+        else if (sz == 4) *reinterpret_cast<g32*>(p) = (uint32_t)v;
+        else if (sz == 2) *reinterpret_cast<g16*>(p) = (uint16_t)v;
+        else *reinterpret_cast<g8*>(p) = (uint8_t)v;
+        lo += sz;
+    };
+    if ((lo & 1) && lo + 1 <= hi) put(1);
+    if ((lo & 2) && lo + 2 <= hi) put(2);
+    if ((lo & 4) && lo + 4 <= hi) put(4);
+    if (lo + 8 <= hi) put(8);
+    if (lo + 4 <= hi) put(4);
+    if (lo + 2 <= hi) put(2);
+    if (lo + 1 <= hi) put(1);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
+    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+    const uint32_t* __restrict__ q) {
+    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kEsWaves * kWave * kEsRing];
+    if (WRITE)
+        for (uint32_t t = threadIdx.x; t < 256; t += kEsWaves * kWave) lut[t] = compact_selector(t);
+    __syncthreads();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* const ring_all = ring_blk + wave * (kWave * kEsRing);
+    const uint32_t lane = lane_id();
+    // the small units: mid-list bins 4 .. 7 (unit_class<4>)
+    const uint32_t b0i = q[11 + CL_MID_BINS - kEsBins];
+    const uint32_t count = q[4] - b0i;
+    const uint32_t* const list = q + kQHead + 2ull * n + b0i;
+    const uint32_t wv = blockIdx.x * kEsWaves + wave;
+    if (wv * kWave >= count) return;  // wave-uniform
+    const uint32_t slot = wv * kWave + lane;
+    const bool valid = slot < count;
+    const uint32_t unit = valid ? list[slot] : 0u;
+
+    // ---- per-lane unit ---------------------------------------------------------------
+    const uint8_t* src = cpk_dummy16;
+    uint64_t len = 0, cap = 0;
+    uint8_t* dst = out;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        len = in_len[unit];
+        if (reinterpret_cast<uintptr_t>(src) & 7) st = ST_ARG;
+        else if (len & 7) st = ST_SIZE;  // message.zig:201
+        if (WRITE) {
+            dst = out + out_off[unit];
+            cap = out_cap[unit];
+        }
+    }
+    const bool take = valid && st == ST_OK && len > 0;
+    if (!take) src = cpk_dummy16;
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);  // 0 or 8
+    const uint32_t s8 = s >> 3;
+    const uint32_t nw = take ? s8 + (uint32_t)(len >> 3) : 0u;  // aligned-space word end (<= 65 words)
+    const uint32_t nr = (nw + 7) >> 3;                            // rounds of this unit
+    const uint32_t npieces = take ? (s + (uint32_t)len + 15) >> 4 : 0u;
+    const uint32_t maxr = __builtin_amdgcn_readfirstlane(wave_max_u32(nr));
+
+    const uint4* qsrc[4];
+    uint32_t qlast[4];
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m) {
+        const uint32_t r = 16 * m + lane / 4;
+        const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
+        const uint32_t rn = __shfl(npieces, r, kWave);
+        qsrc[m] = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16);
+        qlast[m] = rn ? rn - 1 : 0u;
+    }
+    const uint32_t qp = lane & 3;
+    u32x4 d0, d1, d2, d3;
+    // only pieces inside the unit are loaded (a lane past its unit's last piece skips the
+    // load: the ring keeps stale bytes the steps never read), and with the temporal hint, so a
+    // line read for one round is still in L2 for the next (round 4: clamped non-temporal
+    // re-loads of the last piece read 656 MB per C5 launch, 4.8x the small units' input)
+    auto load = [&](uint32_t k) {
+        if (4 * k + qp <= qlast[0]) ds_gload16(d0, qsrc[0] + 4 * k + qp);
+        if (4 * k + qp <= qlast[1]) ds_gload16(d1, qsrc[1] + 4 * k + qp);
+        if (4 * k + qp <= qlast[2]) ds_gload16(d2, qsrc[2] + 4 * k + qp);
+        if (4 * k + qp <= qlast[3]) ds_gload16(d3, qsrc[3] + 4 * k + qp);
+    };
+    uint8_t* const wq = ring_all + (lane / 4) * kEsRing + 16 * qp;  // unit 16m + l/4: + 16 * kEsRing * m
+    const uint64_t* const ring = reinterpret_cast<const uint64_t*>(ring_all + lane * kEsRing);
+
+    // ---- the encoder's state (encode_small_kernel's word step) ---------------------------
+    const uint32_t da = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
+    uint8_t* const db = dst - da;  // 16-B aligned base of the output slot
+    uint64_t op = 0;               // packed bytes so far
+    uint64_t b0 = 0, b1 = 0;       // the output chunk being assembled: chunk (da + op) >> 4
+    uint32_t mode = 0, run = 0;    // 0: none, 1: zero run, 2: literal run; its length
+    uint64_t cpos = 0;             // literal run: output offset of its count byte
+    uint64_t f0 = 0, f1 = 0, fch = 0;  // a chunk the step completed
+    bool fpend = false;
+    const uint64_t lim = cap > ~0ull - 16 ? ~0ull : da + cap;  // slot end (saturated)
+    auto app = [&](bool p, uint64_t v, uint32_t nb) {  // append nb <= 8 bytes of v when p
+        if (WRITE) {
+            const uint32_t k = (uint32_t)((da + op) & 15);
+            const uint32_t sh = 8 * (k & 7);
+            const uint64_t lo = v << sh, hi = (v >> 1) >> (63 - sh);
+            const bool low = k < 8;
+            if (p) {
+                b0 |= low ? lo : 0ull;
+                b1 |= low ? hi : lo;
+            }
+            if (p && k + nb >= 16) {
+                f0 = b0;
+                f1 = b1;
+                fch = (da + op) >> 4;
+                fpend = true;
+                b0 = hi;
+                b1 = 0;
+            }
+        }
+        op += p ? nb : 0u;
+    };
+    auto patch = [&](bool p, uint32_t c) {  // the open literal run's count byte = c
+        if (!WRITE || !p) return;
+        const uint64_t x = da + cpos;
+        const uint32_t k = (uint32_t)(x & 15);
+        const uint64_t m0 = k < 8 ? (uint64_t)c << (8 * k) : 0ull, m1 = k < 8 ? 0ull : (uint64_t)c << (8 * (k - 8));
+        if ((x >> 4) == ((da + op) >> 4)) {
+            b0 |= m0;
+            b1 |= m1;
+        } else if (fpend && (x >> 4) == fch) {
+            f0 |= m0;
+            f1 |= m1;
+        } else if (cpos < cap) {
+            es_store_byte(db + x, c);  // after the chunk's store (same wave, same address)
+        }
+    };
+    auto step = [&](uint64_t w, bool vw) {  // message.zig:206-266, one word
+        const uint32_t tg = nonzero_tag(w);
+        const bool isz = tg == 0u, isf = tg == 0xFFu;
+        const bool cz = vw && mode == 1 && isz && run < 256;
+        const bool cf = vw && mode == 2 && isf && run < 256;
+        const bool cl = vw && mode != 0 && !cz && !cf;
+        app(cl && mode == 1, (uint64_t)(run - 1) << 8, 2);  // 00 <count>
+        patch(cl && mode == 2, run - 1);
+        const bool nzr = vw && !cz && !cf && isz;
+        const bool nfr = vw && !cz && !cf && isf;
+        const bool mx = vw && !isz && !isf;
+        const uint64_t v = cf ? w : (nfr ? (0xFFull | (w << 8)) : ((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) << 8 : 0ull)));
+        app(cf || nfr || mx, v, (cf || nfr) ? 8u : 1u + __popc(tg));
+        app(nfr, w >> 56, 2);  // w7, then the count byte (0 until patched)
+        cpos = nfr ? op - 1 : cpos;
+        mode = (cz || nzr) ? 1u : ((cf || nfr) ? 2u : (vw ? 0u : mode));
+        run = (cz || cf) ? run + 1 : ((nzr || nfr) ? 1u : run);
+    };
+    uint32_t younger = 0;  // stores issued after the round's loads (counted ones)
+    // a completed chunk: one 16-B store when it lies inside the slot, else its slot bytes
+    auto flush_pending = [&]() {
+        if (!WRITE) return;
+        const bool full = fpend && 16 * fch >= da && 16 * fch + 16 <= lim;
+        if (__builtin_amdgcn_ballot_w64(full) != 0) {
+            if (full) es_store16(db + 16 * fch, f0, f1);
+            ++younger;
+        }
+        if (fpend && !full) {  // the slot's first chunk, or one past its capacity
+            const uint64_t cs = 16 * fch;
+            const uint64_t a = max(cs, (uint64_t)da), e = min(cs + 16, lim);
+            if (a < e) es_store_partial16(db + cs, (uint32_t)(a - cs), (uint32_t)(e - cs), f0, f1);
+        }
+        fpend = false;
+    };
+
+    if (maxr > 0) load(0);
+    for (uint32_t k = 0; k < maxr; ++k) {
+        vmcnt_at_most63(younger);  // round k's loads have landed
+        asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+        younger = 0;
+        wave_lds_sync();  // every lane is done with round k-1's ring reads
+        *reinterpret_cast<u32x4*>(wq) = d0;
+        *reinterpret_cast<u32x4*>(wq + 16 * kEsRing) = d1;
+        *reinterpret_cast<u32x4*>(wq + 32 * kEsRing) = d2;
+        *reinterpret_cast<u32x4*>(wq + 48 * kEsRing) = d3;
+        if (k + 1 < maxr) load(k + 1);
+        wave_lds_sync();
+#pragma unroll 2
+        for (uint32_t t = 0; t < 8; ++t) {
+            const uint32_t aw = 8 * k + t;
+            step(ring[t], take && aw >= s8 && aw < nw);
+            flush_pending();
+        }
+        if (take && k + 1 == nr) {  // the unit ends in this round
+            app(mode == 1, (uint64_t)(run - 1) << 8, 2);  // inside a run
+            patch(mode == 2, run - 1);
+            mode = 0;
+        }
+        flush_pending();
+        if (take && k + 1 == nr && WRITE && ((da + op) & 15)) {  // the last, partial chunk
+            const uint64_t cs = ((da + op) >> 4) << 4;
+            const uint64_t a = max(cs, (uint64_t)da), e = min(da + op, lim);
+            if (a < e) es_store_partial16(db + cs, (uint32_t)(a - cs), (uint32_t)(e - cs), b0, b1);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!valid) return;
+    out_len[unit] = st == ST_OK ? op : 0;
+    status[unit] = st != ST_OK ? st : ((WRITE && op > cap) ? ST_SPACE : ST_OK);
 }
 
 // ---- small units, lane per unit -----------------------------------------------------------
@@ -5028,12 +5295,17 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-    launch_classes<0>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    const bool es = kEsStream;  // small units: the streaming encoder (mid-list bins 4 .. 7)
+    if (es)
+        launch_classes<4>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    else
+        launch_classes<0>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
     const hipStream_t ss = side.stream();
     const uint32_t* const mid = q + kQHead + 2ull * n;
-    const uint32_t* const mid_count = q + 4;
+    const uint32_t* const mid_count = es ? q + 12 : q + 4;  // es: bin 0 (the units before bin 1)
+    const uint32_t es_blocks = (n + kEsWaves * kWave - 1) / (kEsWaves * kWave);  // waves past the count exit
     static const uint32_t tiles_res = resident_blocks(tile_encode_kernel<kTilesWrite, true>, kBlock, 4);
     long_tiles_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
     if (write) {
@@ -5043,7 +5315,11 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                               out_cap, out_len, status, q);
         encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, q);
-        encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+        if (es)
+            encode_stream_kernel<true><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
+                                                                                   out_off, out_cap, out_len, status, q);
+        else
+            encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                            out_cap, out_len, status, q);
         encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                                 status, mid, mid_count);
@@ -5054,7 +5330,11 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                                out_cap, out_len, status, q);
         encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status, q);
-        encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+        if (es)
+            encode_stream_kernel<false><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
+                                                                                    out_off, out_cap, out_len, status, q);
+        else
+            encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                             out_cap, out_len, status, q);
         encode_kernel<false><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                  out_len, status, mid, mid_count);
