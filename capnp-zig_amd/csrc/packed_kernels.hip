@@ -3278,10 +3278,11 @@ __global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __
 }
 
 // ---- small units, streaming encoder (round 4) -----------------------------
-// Lane per unit, 64 units per wave in lockstep rounds of 8 words, as decode_stream_kernel:
-// round k's 64-B blocks of the wave's units come in by quad-coalesced 16-B loads issued a
-// round ahead (a unit's block is read in one line fetch, at full occupancy: the persistent
-// lane kernel below re-fetched lines its lanes had read, ~4.5x its input), land in the
+// Lane per unit, 64 units per wave in lockstep rounds of 8 words: round k's 64-B blocks of
+// the wave's units come in by quad-coalesced 16-B loads issued a round ahead (only pieces
+// inside the unit, temporal: the lane-streaming kernel below re-fetched lines its lanes had
+// read, 4.2x its input; this one reads 3.6x, the neighbours of a unit's first and last lines
+// being other bins' units), land in the
 // units' 64-B LDS rings, and each lane codes its unit's 8 words with the Zig encoder's word
 // step (message.zig:200-271; the small kernel's predicated state machine: a zero run is
 // emitted when it ends, a literal run's count byte patched when it ends). A step completes at
@@ -3289,10 +3290,10 @@ __global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __
 // completed in one round sits next to its neighbours of the previous one, so lines fill up in
 // L2 within a round or two. The small units come binned by length (<= 8, 16, 32, 64 words:
 // 1, 2, 4 or 8 rounds; unit_class<4>), so a wave's units take about as many rounds.
-#ifndef CPK_ES_STREAM  // dev A/B: 1 = small units by encode_stream_kernel, 0 = encode_small_kernel
-#define CPK_ES_STREAM 0
+#ifndef CPK_ES_STREAM  // 1: small units by encode_stream_kernel; 0 (dev build): encode_small_kernel
+#define CPK_ES_STREAM 1
 #endif
-constexpr bool kEsStream = CPK_ES_STREAM;
+#if CPK_ES_STREAM
 constexpr uint32_t kEsWaves = 4;
 constexpr uint32_t kEsBins = 4;   // small-unit bins of unit_class<4>: mid list bins 4 .. 7
 constexpr uint32_t kEsRing = 80;  // ring row per unit: 64 B + 16 B pad (spreads the lanes' banks)
@@ -3522,7 +3523,11 @@ __global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
     status[unit] = st != ST_OK ? st : ((WRITE && op > cap) ? ST_SPACE : ST_OK);
 }
 
-// ---- small units, lane per unit -----------------------------------------------------------
+#endif  // CPK_ES_STREAM
+
+// ---- small units, lane per unit ----------------------------------------------------------
+// (encode_small_kernel is the dev build's, CPK_ES_STREAM=0: C5 encode 0.630 ms against the
+// streaming encoder's 0.588-0.603, same box; decode_small_kernel ships.)
 // A persistent grid: each wave owns a contiguous range of the small list and its lanes
 // take the range's next unit as they finish (a wave-uniform cursor, as in
 // validate_kernel), so one longer unit does not idle the rest of its wave. Every turn
@@ -3532,6 +3537,7 @@ __global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
 constexpr uint32_t kSmBlock = 256;
 enum : uint32_t { SM_IDLE, SM_EXIT, SM_META, SM_FIRST, SM_RUN };
 
+#if !CPK_ES_STREAM
 // Zig encoder rules (message.zig:200-271) as a word-at-a-time state machine, one word per
 // step on every lane with a predicated body (no per-word branches): a zero run (00 n-1) is
 // emitted when it ends; a literal run's count byte (FF w0 n-1 w1..) is patched when it ends
@@ -3750,6 +3756,8 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
         }
     }
 }
+#endif  // !CPK_ES_STREAM
+
 
 // unpackPacked (message.zig:88-145) for one unit per lane. Each lane keeps a 64-B ring of
 // its unit's packed bytes in LDS (piece p at slot p % 4). A turn codes the records that
@@ -5285,27 +5293,30 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     // classes (caller's stream), then the long units on the side stream (encode_tiled_kernel
     // over a grid taking units from the queue) beside the small units (a lane each) and the
     // mid units (a wave each) on the caller's stream
+#if !CPK_ES_STREAM
     static const uint32_t sm_res = resident_blocks(encode_small_kernel<true>, kSmBlock, 8);
+    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
+#endif
     // long-unit workers: up to one wave per unit, at most the resident grid (a batch of a
     // few long units must not get a grid sized by its unit count / 256)
     static const uint32_t tiled_res = resident_blocks(encode_tiled_kernel<true>, kBlock, 3);
     const uint32_t tiled_blocks = min((n + kWavesPerBlock - 1) / kWavesPerBlock, tiled_res);
-    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
     const uint32_t mid_blocks = blocks_for(n);  // waves past the mid count return at once
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-    const bool es = kEsStream;  // small units: the streaming encoder (mid-list bins 4 .. 7)
-    if (es)
-        launch_classes<4>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
-    else
-        launch_classes<0>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+#if CPK_ES_STREAM  // small units: the streaming encoder (mid-list bins 4 .. 7)
+    launch_classes<4>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    const uint32_t* const mid_count = q + 12;  // bin 0: the units before bin 1
+    const uint32_t es_blocks = (n + kEsWaves * kWave - 1) / (kEsWaves * kWave);  // waves past the count exit
+#else
+    launch_classes<0>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    const uint32_t* const mid_count = q + 4;
+#endif
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
     const hipStream_t ss = side.stream();
     const uint32_t* const mid = q + kQHead + 2ull * n;
-    const uint32_t* const mid_count = es ? q + 12 : q + 4;  // es: bin 0 (the units before bin 1)
-    const uint32_t es_blocks = (n + kEsWaves * kWave - 1) / (kEsWaves * kWave);  // waves past the count exit
     static const uint32_t tiles_res = resident_blocks(tile_encode_kernel<kTilesWrite, true>, kBlock, 4);
     long_tiles_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
     if (write) {
@@ -5315,12 +5326,13 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                               out_cap, out_len, status, q);
         encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, q);
-        if (es)
-            encode_stream_kernel<true><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                                   out_off, out_cap, out_len, status, q);
-        else
-            encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                           out_cap, out_len, status, q);
+#if CPK_ES_STREAM
+        encode_stream_kernel<true><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                               out_cap, out_len, status, q);
+#else
+        encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                       out_cap, out_len, status, q);
+#endif
         encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                                 status, mid, mid_count);
     } else {
@@ -5330,12 +5342,13 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                                out_cap, out_len, status, q);
         encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status, q);
-        if (es)
-            encode_stream_kernel<false><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out,
-                                                                                    out_off, out_cap, out_len, status, q);
-        else
-            encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                            out_cap, out_len, status, q);
+#if CPK_ES_STREAM
+        encode_stream_kernel<false><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                out_cap, out_len, status, q);
+#else
+        encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                        out_cap, out_len, status, q);
+#endif
         encode_kernel<false><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                  out_len, status, mid, mid_count);
     }
