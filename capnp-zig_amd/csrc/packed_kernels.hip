@@ -2670,6 +2670,12 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
         return !small ? CL_MID : CL_MID + 4 + (valid && w > 8) + (valid && w > 16) + (valid && w > 32);
     }
     const uint64_t cap = out_cap[u];
+    if (KIND == 5) {  // dev (CPK_DS_SMALL): small units binned for the streaming decoder, mid units bin 0
+        if (len <= kSmDecP && cap <= kSmDecCap)
+            return CL_MID + 4 + (len > 64) + (len > 128) + (len > 256);
+        if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
+        return CL_MID;
+    }
     if (KIND == 3) {
         if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
         return CL_MID + (len > 64) + (len > 128) + (len > 256) + (len > 512) + (len > 1280) + (len > 2048) +
@@ -5464,7 +5470,12 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-    if (streaming)  // small and mid units in one list, binned by packed length
+#ifndef CPK_DS_SMALL  // dev: 1 = the streaming decoder takes the small units only, mid units two-pass
+#define CPK_DS_SMALL 0
+#endif
+    if (streaming && CPK_DS_SMALL)
+        launch_classes<5>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    else if (streaming)  // small and mid units in one list, binned by packed length
         launch_classes<3>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
     else
         launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
@@ -5489,10 +5500,24 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                    out_len, status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
 #if CPK_DEV_DECODERS
+    if (streaming && CPK_DS_SMALL) {  // small units by the streaming decoder, mid units two-pass
+        const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);
+        decode_stream_kernel<true><<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                out_cap, out_len, status, q, nullptr);
+        uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);
+        decode_index_kernel<false><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(
+            in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 12, rec);
+        decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                              out_len, out_cap, status, mid, q + 12,
+                                                                              rec);
+        e = hipGetLastError();
+        const hipError_t j = side.join();
+        return e != hipSuccess ? e : j;
+    }
     if (streaming) {  // small and mid units, 64 per wave
         const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);  // waves past the count exit
-        decode_stream_kernel<<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                          out_cap, out_len, status, mid, q + 4);
+        decode_stream_kernel<false><<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
+                                                                                 out_cap, out_len, status, mid, q + 4);
         e = hipGetLastError();
         const hipError_t j = side.join();
         return e != hipSuccess ? e : j;
