@@ -6,6 +6,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
+# the streaming decoder exists in dev builds only (scripts/dev/build_all_variants.sh)
+export CPK_LIB=${CPK_LIB:-capnp-zig_amd/lib_exp/dev_decoders.so}
 O=gpurun_out/stream
 mkdir -p $O
 step() {  # name, then the command; stops the script on a crash / time limit
