@@ -5324,6 +5324,8 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     const hipStream_t ss = side.stream();
     const uint32_t* const mid = q + kQHead + 2ull * n;
     static const uint32_t tiles_res = resident_blocks(tile_encode_kernel<kTilesWrite, true>, kBlock, 4);
+    // mid units on a second side stream beside the small-unit kernel (LAUNCH_MID_SIDE_STREAM)
+    const hipStream_t ms = mid_side_stream() ? side.stream2() : stream;
     long_tiles_kernel<<<list_blocks(n), 256, 0, ss>>>(in_len, n, q);
     if (write) {
         tile_encode_kernel<kTilesSize, true><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
@@ -5332,6 +5334,9 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                               out_cap, out_len, status, q);
         encode_tiled_kernel<true><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, q);
+        if (ms != stream)  // LAUNCH_MID_SIDE_STREAM: the mid units beside the small ones
+            encode_kernel<true><<<mid_blocks, kBlock, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
+                                                                status, mid, mid_count);
 #if CPK_ES_STREAM
         encode_stream_kernel<true><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                                out_cap, out_len, status, q);
@@ -5339,8 +5344,9 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
         encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                        out_cap, out_len, status, q);
 #endif
-        encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
-                                                                status, mid, mid_count);
+        if (ms == stream)
+            encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                    out_len, status, mid, mid_count);
     } else {
         tile_encode_kernel<kTilesSize, false><<<tiles_res, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off,
                                                                               out_cap, out_len, status, q);
@@ -5348,6 +5354,9 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                                out_cap, out_len, status, q);
         encode_tiled_kernel<false><<<tiled_blocks, kBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status, q);
+        if (ms != stream)
+            encode_kernel<false><<<mid_blocks, kBlock, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                 out_len, status, mid, mid_count);
 #if CPK_ES_STREAM
         encode_stream_kernel<false><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                                 out_cap, out_len, status, q);
@@ -5355,8 +5364,9 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
         encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                         out_cap, out_len, status, q);
 #endif
-        encode_kernel<false><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                 out_len, status, mid, mid_count);
+        if (ms == stream)
+            encode_kernel<false><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                     out_len, status, mid, mid_count);
     }
     e = hipGetLastError();
     const hipError_t j = side.join();
