@@ -374,9 +374,10 @@ int capnp_packed_set_all_or_nothing(int on);
  * unknown bits are ignored). No result depends on it, only where the kernels run:
  *   CAPNP_PACKED_LAUNCH_LONG_INLINE      long units run after the main grid on the caller's stream
  *                                        instead of on a side stream forked from and joined into it;
- *   CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM  decode: mid units on a second side stream beside the small
- *                                        units' kernel (helps batches of mostly small units with a
- *                                        few mid ones; costs a fork/join otherwise). */
+ *   CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM  encode and decode: mid units on a second side stream beside
+ *                                        the small units' kernel (helps batches of mostly small units
+ *                                        with a few mid ones; costs a fork/join
+ *                                        otherwise). */
 #define CAPNP_PACKED_LAUNCH_LONG_INLINE 0x1u
 #define CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM 0x2u
 uint32_t capnp_packed_set_launch_flags(uint32_t flags);
