@@ -484,15 +484,20 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
     streams = {c: b"".join(pk_h[i * slot:i * slot + int(pl_h[i])].tobytes() for i in range(c * msgs, (c + 1) * msgs))
                for c in range(conns)}
     packed_bytes = sum(len(v) for v in streams.values())
-    best, ok = None, True
-    for _ in range(reps):
-        pc = cp.PackedConnections(conns, device=dev)
+    # one long-lived session, as an event loop keeps it: the first read also pays the session's
+    # device allocations (reported as first_read_ms), later reads of the same batch shape reuse them
+    best, ok, first = None, True, None
+    pc = cp.PackedConnections(conns, device=dev)
+    for r in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res = pc.handle_read(streams)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
+        if r == 0:
+            first = dt
+        else:
+            best = dt if best is None else min(best, dt)
         for c in (0, conns // 2, conns - 1):
             fr = res[c]
             ok &= isinstance(fr, list) and len(fr) == msgs and all(
@@ -500,8 +505,9 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
         ok &= all(isinstance(v, list) and len(v) == msgs for v in res.values())
     return {"connections": conns, "messages_per_read": msgs, "framed_bytes": 4096, "packed_bytes": packed_bytes,
             "ms": round(best * 1e3, 2), "framed_GiB_s": round(n * 4096 / best / 2 ** 30, 2),
-            "frames_per_s": round(n / best), "bit_exact": bool(ok),
-            "note": "host buffers in and out (PCIe + host-side framing), rounds of read_message_batch"}
+            "frames_per_s": round(n / best), "first_read_ms": round(first * 1e3, 2), "bit_exact": bool(ok),
+            "note": "host buffers in and out (PCIe + host-side framing); one framer session, best of the reads "
+                    "after its first (first_read_ms includes the session's device allocations)"}
 
 
 def framer_split_leg(args, dev, read_bytes=65536, sizes_words=(1 << 17, 1 << 19, 1 << 21, 1 << 23)):
