@@ -464,9 +464,12 @@ def skewed_leg(args, dev, n=1 << 20, reps=10):
 def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
     """SURVEY §8(f) row 3, RPC framer batching: `conns` connections, each with one socket
     read holding `msgs` packed 1-segment messages (framed 4096 B, p = zero_thresh/256).
-    PackedConnections.handle_read pops every frame: one read_message_batch per round, one
-    unit per connection, H2D of the buffered bytes and D2H of the frames included (a
-    host-memory path: reported beside `value`, never as it)."""
+    PackedConnections.handle_read pops every frame: one walk pass finds every held message
+    of every connection and one decode pass frames them, H2D of the bytes and D2H of the frames
+    included (a host-memory path: reported beside `value`, never as it). `ms` is the Python
+    mirror's read; native_ms the capnp_packed_framer_read call a C / Zig caller makes on an
+    assembled page-locked input (FramerSession.read_raw), assemble_ms the mirror's gathering of
+    the per-connection bytes objects into that input."""
     n = conns * msgs
     words = 511
     d_fr = cp.generate(n, 4096, seed=0xC0DE0007, zero_thresh=args.zero_thresh, device=dev)
@@ -503,9 +506,24 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
             ok &= isinstance(fr, list) and len(fr) == msgs and all(
                 fr[k] == fr_h[(c * msgs + k) * 4096:(c * msgs + k + 1) * 4096].tobytes() for k in range(msgs))
         ok &= all(isinstance(v, list) and len(v) == msgs for v in res.values())
+    del res
+    sess = pc.session
+    t0 = time.perf_counter()
+    inp = sess.assemble(streams)
+    asm = time.perf_counter() - t0
+    nat = None
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        parts, status = sess.read_raw(*inp)
+        dt = time.perf_counter() - t0
+        nat = dt if nat is None else min(nat, dt)
+        ok &= sum(len(p[1]) for p in parts) == n and bool((status == cp.END_OF_STREAM).all())
+        del parts
     return {"connections": conns, "messages_per_read": msgs, "framed_bytes": 4096, "packed_bytes": packed_bytes,
             "ms": round(best * 1e3, 2), "framed_GiB_s": round(n * 4096 / best / 2 ** 30, 2),
-            "frames_per_s": round(n / best), "first_read_ms": round(first * 1e3, 2), "bit_exact": bool(ok),
+            "frames_per_s": round(n / best), "first_read_ms": round(first * 1e3, 2),
+            "native_ms": round(nat * 1e3, 2), "native_framed_GiB_s": round(n * 4096 / nat / 2 ** 30, 2),
+            "assemble_ms": round(asm * 1e3, 2), "bit_exact": bool(ok),
             "note": "host buffers in and out (PCIe + host-side framing); one framer session, best of the reads "
                     "after its first (first_read_ms includes the session's device allocations)"}
 

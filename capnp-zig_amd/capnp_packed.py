@@ -483,6 +483,19 @@ def read_packed_message_bytes(data) -> tuple:
 # Framing for packed byte streams
 # ---------------------------------------------------------------------------
 
+_PIN_MIN = 1 << 20
+
+
+def _host_bytes(nbytes: int, pin: bool = True) -> np.ndarray:
+    """A host byte buffer for a framer call. With `pin`, from 1 MiB up it is page-locked memory
+    from torch's caching host allocator: the session's H2D / D2H copies then run at the link's
+    DMA rate instead of through the runtime's pageable staging, and a freed buffer (its last
+    frame view dropped) goes back to torch's cache for the next read."""
+    if pin and nbytes >= _PIN_MIN and torch is not None and torch.cuda.is_available():
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+    return np.empty(max(nbytes, 1), dtype=np.uint8)
+
+
 class FramerSession:
     """A capnp_packed_framer: the Framer state of n connections kept on the device between
     reads (include/capnp_packed.h). Each connection's unconsumed packed bytes
@@ -510,23 +523,46 @@ class FramerSession:
         (frames, status): frames[c] lists connection c's frames in order (read-only
         memoryviews of the call's frame buffers), status an int32 array: END_OF_STREAM, or the
         reader's error after which the connection's bytes were dropped."""
+        gc_on = gc.isenabled()
+        gc.disable()  # no cycles among the views; the collector's passes cost more (DESIGN.md §2.7)
+        try:
+            return self._read(reads)
+        finally:
+            if gc_on:
+                gc.enable()
+
+    def assemble(self, reads: dict):
+        """The connections' new bytes as one host buffer (page-locked from 1 MiB up) with
+        per-connection offsets and lengths: the input of read_raw."""
         n = self.n
         lens = np.zeros(n, dtype=np.uint64)
         for c, d in reads.items():
             lens[c] = len(d)
         off = np.zeros(n, dtype=np.uint64)
         off[1:] = np.cumsum(lens)[:-1]
-        total = int(lens.sum())
-        host = np.empty(max(total, 1), dtype=np.uint8)
+        host = _host_bytes(int(lens.sum()))
         for c, d in reads.items():
             if len(d):
                 host[int(off[c]):int(off[c]) + len(d)] = np.frombuffer(d, dtype=np.uint8)
-        frames = {}
+        return host, off, lens
+
+    def read_raw(self, host, off, lens):
+        """capnp_packed_framer_read over an assembled input (a server that receives into one
+        buffer skips assemble()). Returns (parts, status): parts lists (buf, f_off, f_len,
+        f_conn) per native call, frame i of a part being buf[f_off[i]:f_off[i] + f_len[i]] of
+        connection f_conn[i], a connection's frames in order over the parts; status as read()."""
+        n = self.n
+        total = int(lens.sum())
         status = np.zeros(n, dtype=np.int32)
-        cap, max_frames = max(1 << 16, 4 * total), max(1024, total // 2 + 64)
+        parts = []
+        # frames of 2x the read's bytes: the buffer runs out only for messages packed below
+        # half their size, and then the loop below pops the rest into a larger one
+        cap, max_frames = max(1 << 16, 2 * total + (1 << 16)), max(1024, total // 2 + 64)
         first = True
         while True:
-            buf = np.empty(cap, dtype=np.uint8)
+            # a retry's buffer is sized for one large message: pageable, as pinning it fresh
+            # costs more than the runtime's staged copy of it
+            buf = _host_bytes(cap, pin=first)
             f_off = np.empty(max_frames, dtype=np.uint64)
             f_len = np.empty(max_frames, dtype=np.uint64)
             f_conn = np.empty(max_frames, dtype=np.uint32)
@@ -534,17 +570,17 @@ class FramerSession:
             nf = ctypes.c_uint32(0)
             rc = lib().capnp_packed_framer_read(  # later calls pop what is held, no new bytes
                 self.handle, host.ctypes.data if first else None, total if first else 0,
-                off.ctypes.data if first else None, lens.ctypes.data if first else None, buf.ctypes.data, cap, f_off.ctypes.data, f_len.ctypes.data,
-                f_conn.ctypes.data, max_frames, st_call.ctypes.data, ctypes.byref(nf))
+                off.ctypes.data if first else None, lens.ctypes.data if first else None, buf.ctypes.data, cap,
+                f_off.ctypes.data, f_len.ctypes.data, f_conn.ctypes.data, max_frames, st_call.ctypes.data,
+                ctypes.byref(nf))
             if rc not in (OK, OUT_OF_SPACE):
                 _raise(rc, "framer_read")
             first = False
             err = st_call != END_OF_STREAM
             status[err] = st_call[err]
-            view = memoryview(buf).toreadonly()
             k = nf.value
-            for o, ln, c in zip(f_off[:k].tolist(), f_len[:k].tolist(), f_conn[:k].tolist()):
-                frames.setdefault(c, []).append(view[o:o + ln])
+            if k:
+                parts.append((buf, f_off[:k], f_len[:k], f_conn[:k]))
             if rc == OK:
                 break
             # frames or the table filled up: pop the rest into larger ones; a buffer of the
@@ -553,6 +589,22 @@ class FramerSession:
             cap = max(cap * 2 if k == 0 else cap, (big + 7) // 8 * 8 + 64)
             max_frames *= 2
         status[status == 0] = END_OF_STREAM
+        return parts, status
+
+    def _read(self, reads: dict):
+        parts, status = self.read_raw(*self.assemble(reads))
+        frames = {}
+        for buf, f_off, f_len, f_conn in parts:
+            # a connection's frames are in order within a call: group them by a stable sort
+            view = memoryview(buf).toreadonly()
+            order = np.argsort(f_conn, kind="stable")
+            conn_s = f_conn[order]
+            fo = f_off[order]
+            fo_l, fe_l = fo.tolist(), (fo + f_len[order]).tolist()
+            cuts = (np.flatnonzero(np.diff(conn_s)) + 1).tolist()
+            starts = [0] + cuts
+            for c, a, b in zip(conn_s[starts].tolist(), starts, cuts + [len(conn_s)]):
+                frames.setdefault(c, []).extend(map(view.__getitem__, map(slice, fo_l[a:b], fe_l[a:b])))
         return frames, status
 
     def buffered(self, c: int) -> int:
@@ -667,13 +719,7 @@ class PackedConnections:
         message is popped, and the frames come back as read-only memoryviews of the call's
         frame buffer (no per-frame copy; the buffer lives as long as its frames)."""
         live = {c: d for c, d in reads.items() if not self.closed[c] and len(d)}
-        gc_on = gc.isenabled()
-        gc.disable()  # no cycles among the views; the collector's passes cost more (DESIGN.md §2.7)
-        try:
-            frames, status = self.session.read(live)
-        finally:
-            if gc_on:
-                gc.enable()
+        frames, status = self.session.read(live)
         result = {c: [] for c in live}
         result.update(frames)
         for c in np.nonzero(status != END_OF_STREAM)[0].tolist():

@@ -703,7 +703,12 @@ struct capnp_packed_framer {
     uint64_t frames_dcap = 0;
     uint8_t* d_spec = nullptr;  // the walk's window tables (cpk::launch_frame_walk)
     uint64_t spec_cap = 0;
+    uint8_t* d_round = nullptr;  // a walk pass's list, counts and message table
+    uint64_t round_cap = 0;
+    uint8_t* d_units = nullptr;  // a decode pass's unit metadata (6 u64 per message)
+    uint64_t units_cap = 0;
     uint64_t uploaded = 0, moved = 0;  // bytes copied H2D (new reads) and moved between regions
+    static constexpr uint32_t kWalkMessages = 64;  // messages a walk pass finds per connection
 
     ~capnp_packed_framer() {
         if (s) (void)hipStreamSynchronize(s);
@@ -712,6 +717,8 @@ struct capnp_packed_framer {
         if (d_stage) (void)hipFree(d_stage);
         if (d_frames) (void)hipFree(d_frames);
         if (d_spec) (void)hipFree(d_spec);
+        if (d_round) (void)hipFree(d_round);
+        if (d_units) (void)hipFree(d_units);
         if (s) (void)hipStreamDestroy(s);
     }
     static int grow(uint8_t** p, uint64_t* c, uint64_t need) {
@@ -936,35 +943,31 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
         if ((st = f->run_jobs(jobs, false))) return st;  // ordered before the passes below
     }
 
-    // ---- 2. rounds: headers, walks from the saved positions, decodes of whole messages ------
-    // state scratch: base, avail, need, X, W, consumed (u64 x n), status (i32 x n), then round
-    // lists / unit metadata (7 u64 x n) and the copy jobs (run_jobs) past them
+    // ---- 2. passes: a walk over every connection's held messages, then one decode of them ----
+    // state scratch: base, avail, need, X, W (u64 x n), status (i32 x n), then the copy jobs
+    // (run_jobs) past them; the pass's list / counts / message table and the decode metadata
+    // live in blocks of their own
     if ((st = capnp_packed_framer::grow(&f->d_state, &f->state_cap, (uint64_t)n * 56 + 256 + 64ull * n + 4096))) return st;
     uint64_t* const d_base = reinterpret_cast<uint64_t*>(f->d_state);
     uint64_t* const d_avail = d_base + n;
     uint64_t* const d_need = d_base + 2ull * n;
     uint64_t* const d_X = d_base + 3ull * n;
     uint64_t* const d_W = d_base + 4ull * n;
-    uint64_t* const d_cons = d_base + 5ull * n;
     int32_t* const d_st = reinterpret_cast<int32_t*>(d_base + 6ull * n);
-    // round scratch past the copy-job area would be reallocated by run_jobs; a separate block:
-    std::vector<uint64_t> h(6ull * n), hm(7ull * n);
-    std::vector<uint32_t> spec_h;  // window tables' first / count per listed connection
+    constexpr uint32_t M = capnp_packed_framer::kWalkMessages;
+    std::vector<uint64_t> h(7ull * n);  // base, avail, need, X, W, (free), status (i32)
+    std::vector<uint32_t> spec_h;    // window tables' first / count per listed connection
     std::vector<uint64_t> spec_h64;  // their bytes: arena offset, length
     uint64_t spec_T = 0;
-    std::vector<int32_t> hst(n);
-    std::vector<uint32_t> list;
-    std::vector<uint8_t> dead(n, 0);  // an error this call: the connection was reset
+    const int32_t* const hst = reinterpret_cast<const int32_t*>(h.data() + 6ull * n);
+    std::vector<uint32_t> list, hcnt;
+    std::vector<uint8_t> dead(n, 0), more(n, 0);  // dead: an error this call (the connection was reset)
+    std::vector<uint64_t> adv(n), um;             // adv: packed bytes of the pass's accepted messages
+    std::vector<uint32_t> uconn;                  // the pass's accepted messages: connection
+    std::vector<int32_t> perr(n);                 // an error to report once the pass's frames are out
+    for (uint32_t c = 0; c < n; ++c) more[c] = f->len[c] > f->m0[c];
     uint64_t fcur = 0;
     uint32_t nf = 0;
-    uint8_t* d_round = nullptr;  // unit metadata of the header and decode passes (7 u64 x k + list)
-    uint64_t round_cap = 0;
-    struct Free {
-        uint8_t** p;
-        ~Free() {
-            if (*p) (void)hipFree(*p);
-        }
-    } free_round{&d_round};
     auto fail_conn = [&](uint32_t c, int32_t code) {
         status[c] = code;
         dead[c] = 1;
@@ -973,44 +976,10 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
     };
     bool full = false;
     while (!full) {
-        // headers of the connections whose current message has none yet
         list.clear();
         for (uint32_t c = 0; c < n; ++c)
-            if (!dead[c] && f->need[c] == 0 && f->len[c] > f->m0[c]) list.push_back(c);
+            if (!dead[c] && more[c]) list.push_back(c);
         uint32_t k = (uint32_t)list.size();
-        if ((st = capnp_packed_framer::grow(&d_round, &round_cap, 7ull * 8 * (n + 1) + 4ull * n + 256))) return st;
-        uint64_t* const r_in_off = reinterpret_cast<uint64_t*>(d_round);
-        if (k) {
-            for (uint32_t j = 0; j < k; ++j) {
-                const uint32_t c = list[j];
-                hm[j] = f->off[c] + f->m0[c];
-                hm[k + j] = f->len[c] - f->m0[c];
-            }
-            e = hipMemcpyAsync(r_in_off, hm.data(), 2ull * k * 8, hipMemcpyHostToDevice, s);
-            uint64_t* const r_len = r_in_off + 2ull * k;
-            uint64_t* const r_cons = r_in_off + 3ull * k;
-            int32_t* const r_st = reinterpret_cast<int32_t*>(r_in_off + 4ull * k);
-            if (e == hipSuccess) e = cpk::launch_read_header(f->arena, r_in_off, r_in_off + k, k, r_len, r_cons, r_st, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 2ull * k, r_len, 3ull * k * 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return hip_fail(e, "framer header pass");
-            f->jobs_inflight = false;
-            const int32_t* const hs = reinterpret_cast<const int32_t*>(hm.data() + 4ull * k);
-            for (uint32_t j = 0; j < k; ++j) {
-                const uint32_t c = list[j];
-                if (hs[j] == CAPNP_PACKED_OK) {
-                    f->need[c] = hm[2ull * k + j];
-                    f->X[c] = f->W[c] = 0;
-                } else if (hs[j] != CAPNP_PACKED_END_OF_STREAM) {
-                    fail_conn(c, hs[j]);
-                }
-            }
-        }
-        // walks of the connections whose framed length is known, from where they stopped
-        list.clear();
-        for (uint32_t c = 0; c < n; ++c)
-            if (!dead[c] && f->need[c] != 0 && f->len[c] > f->m0[c]) list.push_back(c);
-        k = (uint32_t)list.size();
         if (k == 0) break;
         for (uint32_t c = 0; c < n; ++c) {
             h[c] = f->off[c] + f->m0[c];
@@ -1019,9 +988,13 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
             h[3ull * n + c] = f->X[c];
             h[4ull * n + c] = f->W[c];
         }
-        uint32_t* const r_list = reinterpret_cast<uint32_t*>(r_in_off + 7ull * (n + 1));
+        const uint64_t tab_words = 2ull * k * M;
+        if ((st = capnp_packed_framer::grow(&f->d_round, &f->round_cap, 4ull * (2ull * k + tab_words) + 256))) return st;
+        uint32_t* const r_list = reinterpret_cast<uint32_t*>(f->d_round);
+        uint32_t* const r_cnt = r_list + k;
+        uint32_t* const r_tab = r_cnt + k;
         // window tables for the connections whose bytes past the walk's start span more than
-        // one window (a message split over many reads: its new bytes are crossed by lookups)
+        // one window (a message split over many reads, or many messages: crossed by lookups)
         const uint64_t wb = cpk::framer_window_bytes(), wcap = cpk::framer_window_cap(k);
         spec_h.assign(2ull * k, 0);  // first, count per listed connection (u32); off, len (u64) below
         spec_h64.assign(2ull * k, 0);
@@ -1057,70 +1030,88 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
             if (e == hipSuccess) e = hipMemcpyAsync(a64, spec_h64.data(), 16ull * k, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) return hip_fail(e, "framer window tables");
         }
+        hcnt.resize(k + tab_words);  // the counts, then the message table
         e = hipMemcpyAsync(d_base, h.data(), 5ull * n * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(r_list, list.data(), 4ull * k, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)
-            e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_cons, d_st, d_sq, T,
-                                       d_sfirst, d_scount, d_soff, d_slen, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(h.data() + 3ull * n, d_X, 3ull * n * 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), d_st, 4ull * n, hipMemcpyDeviceToHost, s);
+            e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_st, M, r_cnt, r_tab,
+                                       d_sq, T, d_sfirst, d_scount, d_soff, d_slen, s);
+        // need, X, W, (a free slot), status: one copy; the counts and the table: another
+        if (e == hipSuccess) e = hipMemcpyAsync(h.data() + 2ull * n, d_need, 3ull * n * 8 + n * 8 + 4ull * n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hcnt.data(), r_cnt, 4ull * (k + tab_words), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "framer walk pass");
         f->jobs_inflight = false;
-        // whole messages: decoded from the arena into frame slots, then to the caller's buffer
-        std::vector<uint32_t> done;
+        // whole messages, in order per connection, while the frames buffer and table hold them:
+        // decoded from the arena into frame slots, then to the caller's buffer
+        um.clear();  // per message: in_off, in_len, out_off, out_cap
+        uconn.clear();
         uint64_t slots = 0;
-        for (uint32_t c : list) {
-            const int32_t ws = hst[c];
-            if (ws == CAPNP_PACKED_END_OF_STREAM) {  // the walk stopped at the held bytes' end
-                f->X[c] = h[3ull * n + c];
-                f->W[c] = h[4ull * n + c];
-            } else if (ws == CAPNP_PACKED_OK) {
-                const uint64_t L = f->need[c];
-                if (nf + done.size() + 1 > max_frames || fcur + slots + L > frames_cap) {
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t c = list[j];
+            const uint32_t* const tj = hcnt.data() + k + 2ull * j * M;
+            uint64_t at = 0;
+            uint32_t m = 0;
+            for (; m < hcnt[j]; ++m) {
+                const uint64_t L = tj[2 * m + 1];
+                if (nf + uconn.size() + 1 > max_frames || fcur + slots + L > frames_cap) {
                     full = true;  // stays whole in its region: the next call pops it
-                    continue;
+                    break;
                 }
-                done.push_back(c);
+                um.insert(um.end(), {f->off[c] + f->m0[c] + at, tj[2 * m], slots, L});
+                uconn.push_back(c);
                 slots += (L + 7) & ~7ull;
-            } else {
-                fail_conn(c, ws);
+                at += tj[2 * m];
+            }
+            adv[c] = at;
+            perr[c] = CAPNP_PACKED_OK;
+            more[c] = 0;
+            if (m < hcnt[j]) {  // the frames ran out: message m stays found whole (X at its end)
+                h[2ull * n + c] = tj[2 * m + 1];
+                h[3ull * n + c] = tj[2 * m];
+                h[4ull * n + c] = tj[2 * m + 1] / 8;
+            } else if (hst[c] == CAPNP_PACKED_OK) {
+                more[c] = 1;  // M messages: the next pass walks on from the last one's end
+            } else if (hst[c] != CAPNP_PACKED_END_OF_STREAM) {
+                perr[c] = hst[c];
             }
         }
-        k = (uint32_t)done.size();
-        if (k == 0) break;
-        if ((st = capnp_packed_framer::grow(&f->d_frames, &f->frames_dcap, slots + 16))) return st;
-        uint64_t so = 0;
-        for (uint32_t j = 0; j < k; ++j) {
-            const uint32_t c = done[j];
-            hm[j] = f->off[c] + f->m0[c];         // in_off
-            hm[k + j] = h[5ull * n + c];          // in_len = consumed
-            hm[2ull * k + j] = so;                // out_off
-            hm[3ull * k + j] = f->need[c];        // out_cap
-            so += (f->need[c] + 7) & ~7ull;
+        const uint32_t U = (uint32_t)uconn.size();
+        if (U) {
+            if ((st = capnp_packed_framer::grow(&f->d_frames, &f->frames_dcap, slots + 16))) return st;
+            if ((st = capnp_packed_framer::grow(&f->d_units, &f->units_cap, 48ull * U + 64))) return st;
+            uint64_t* const u = reinterpret_cast<uint64_t*>(f->d_units);
+            std::vector<uint64_t> hm(6ull * U);
+            for (uint32_t q = 0; q < U; ++q)
+                for (uint32_t a = 0; a < 4; ++a) hm[a * (uint64_t)U + q] = um[4ull * q + a];
+            e = hipMemcpyAsync(u, hm.data(), 4ull * U * 8, hipMemcpyHostToDevice, s);
+            int32_t* const u_st = reinterpret_cast<int32_t*>(u + 5ull * U);
+            if (e == hipSuccess)
+                e = cpk::launch_decode(f->arena, u, u + U, U, f->d_frames, u + 2ull * U, u + 3ull * U, u + 4ull * U,
+                                       u_st, true, nullptr, 0, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(frames + fcur, f->d_frames, slots, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 4ull * U, u + 4ull * U, 2ull * U * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hip_fail(e, "framer decode pass");
+            const int32_t* const us = reinterpret_cast<const int32_t*>(hm.data() + 5ull * U);
+            for (uint32_t q = 0; q < U; ++q) {
+                if (us[q] != CAPNP_PACKED_OK || hm[4ull * U + q] != hm[3ull * U + q])  // the walk verified the bytes
+                    return fail(CAPNP_PACKED_DEVICE_ERROR, "framer: a walked message did not decode to its framed length");
+                frame_off[nf] = fcur + hm[2ull * U + q];
+                frame_len[nf] = hm[3ull * U + q];
+                frame_conn[nf] = uconn[q];
+                ++nf;
+            }
+            fcur += slots;
         }
-        e = hipMemcpyAsync(r_in_off, hm.data(), 4ull * k * 8, hipMemcpyHostToDevice, s);
-        int32_t* const u_st = reinterpret_cast<int32_t*>(r_in_off + 5ull * k);
-        if (e == hipSuccess)
-            e = cpk::launch_decode(f->arena, r_in_off, r_in_off + k, k, f->d_frames, r_in_off + 2ull * k,
-                                   r_in_off + 3ull * k, r_in_off + 4ull * k, u_st, true, nullptr, 0, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(frames + fcur, f->d_frames, so, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 4ull * k, r_in_off + 4ull * k, 2ull * k * 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(e, "framer decode pass");
-        const int32_t* const us = reinterpret_cast<const int32_t*>(hm.data() + 5ull * k);
         for (uint32_t j = 0; j < k; ++j) {
-            const uint32_t c = done[j];
-            if (us[j] != CAPNP_PACKED_OK || hm[4ull * k + j] != f->need[c])  // the walk verified the bytes
-                return fail(CAPNP_PACKED_DEVICE_ERROR, "framer: a walked message did not decode to its framed length");
-            frame_off[nf] = fcur + hm[2ull * k + j];
-            frame_len[nf] = f->need[c];
-            frame_conn[nf] = c;
-            ++nf;
-            f->m0[c] += h[5ull * n + c];
-            f->need[c] = f->X[c] = f->W[c] = 0;
+            const uint32_t c = list[j];
+            f->m0[c] += adv[c];
+            f->need[c] = h[2ull * n + c];
+            f->X[c] = h[3ull * n + c];
+            f->W[c] = h[4ull * n + c];
+            if (perr[c] != CAPNP_PACKED_OK) fail_conn(c, perr[c]);  // after the frames before it
         }
-        fcur += so;
     }
     *n_frames = nf;
     if ((st = f->settle())) return st;  // no pass ran after the upload: the caller's bytes are consumed

@@ -55,9 +55,12 @@ hipError_t launch_read_header(const uint8_t* in, const uint64_t* in_off, const u
 size_t framer_spec_bytes(uint32_t nl, uint64_t windows);
 uint32_t framer_window_bytes();            // the windows' size (kWvWin)
 uint64_t framer_window_cap(uint32_t nl);   // windows a spec table of nl connections may hold
+// The walk goes on message after message, up to M per connection: cnt[i] messages found, their
+// packed and framed lengths at tab[2 (i M + m)] / [+ 1] (u32); need / X / W / status then hold
+// the current message's state (frame_walk_kernel).
 hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_t nl, const uint64_t* base,
-                             const uint64_t* avail, const uint64_t* need, uint64_t* X, uint64_t* W,
-                             uint64_t* consumed, int32_t* status, uint32_t* spec_q, uint64_t windows,
+                             const uint64_t* avail, uint64_t* need, uint64_t* X, uint64_t* W, int32_t* status,
+                             uint32_t M, uint32_t* cnt, uint32_t* tab, uint32_t* spec_q, uint64_t windows,
                              const uint32_t* spec_first, const uint32_t* spec_count, const uint64_t* spec_off,
                              const uint64_t* spec_len, hipStream_t stream);
 

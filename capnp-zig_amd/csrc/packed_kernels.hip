@@ -4699,43 +4699,34 @@ constexpr uint64_t kHdrMaxWords = 257;                   // (1 + 512 + pad) u32 
 // the stream (EndOfStream), then after the first record InvalidSegmentCount /
 // SegmentCountLimitExceeded (reader.zig:121-125), then once header_bytes are
 // decoded MessageTooLarge (:140). Segment sizes are summed from the header's
-// words as the records produce them (zero words add nothing).
-__global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __restrict__ in,
-                                                             const uint64_t* __restrict__ in_off,
-                                                             const uint64_t* __restrict__ in_len, uint32_t n,
-                                                             uint64_t* __restrict__ out_len,
-                                                             uint64_t* __restrict__ consumed,
-                                                             int32_t* __restrict__ status) {
-    const uint32_t unit = blockIdx.x * kBlock + threadIdx.x;
-    if (unit >= n) return;
-    const uint8_t* const p = in + in_off[unit];
-    const uint64_t P = in_len[unit];
+// words as the records produce them (zero words add nothing). packed_header returns the
+// status and, when OK, the framed length in `needed`.
+__device__ int32_t packed_header(const uint8_t* __restrict__ p, uint64_t P, uint64_t& needed) {
     uint64_t r = 0;          // read cursor
     uint64_t words = 0;      // decoded words (out.items.len / 8)
     uint64_t count = 0;      // segment count (set by word 0)
     uint32_t count_m1 = 0;
     uint64_t total = 0;      // sum of the sizes decoded so far
-    uint64_t needed = 0;
-    int32_t st = ST_OK;
+    needed = 0;
     for (;;) {
-        if (r >= P) { st = ST_EOS; break; }  // :95 readByte
+        if (r >= P) return ST_EOS;  // :95 readByte
         const uint32_t t = p[r++];
         uint64_t w0 = 0;
         uint32_t c = 0;
         const uint8_t* lit = p;
         if (t == 0x00) {  // :96-99
-            if (r >= P) { st = ST_EOS; break; }
+            if (r >= P) return ST_EOS;
             c = p[r++];
         } else if (t == 0xFF) {  // :100-110
-            if (P - r < 9) { st = ST_EOS; break; }
+            if (P - r < 9) return ST_EOS;
             w0 = gload_u64_unaligned(p + r);
             c = p[r + 8];
             r += 9;
-            if (P - r < 8ull * c) { st = ST_EOS; break; }
+            if (P - r < 8ull * c) return ST_EOS;
             lit = p + r;
             r += 8ull * c;
         } else {  // :111-119
-            if (P - r < (uint64_t)__popc(t)) { st = ST_EOS; break; }
+            if (P - r < (uint64_t)__popc(t)) return ST_EOS;
             for (uint32_t k = 0; k < 8; ++k)
                 if ((t >> k) & 1u) w0 |= (uint64_t)p[r++] << (8 * k);
         }
@@ -4756,15 +4747,27 @@ __global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __re
         }
         words += nw;
         // :121-144 (out.items.len >= 4 after any record)
-        if (count_m1 == 0xFFFFFFFFu) { st = ST_SEGCOUNT; break; }
-        if (count > kMaxSegments) { st = ST_SEGLIMIT; break; }
+        if (count_m1 == 0xFFFFFFFFu) return ST_SEGCOUNT;
+        if (count > kMaxSegments) return ST_SEGLIMIT;
         const uint64_t header_bytes = 4 * (1 + count + ((count & 1) ? 0 : 1));
         if (8 * words >= header_bytes) {
-            if (total > kMaxTotalWords) { st = ST_TOOLARGE; break; }
+            if (total > kMaxTotalWords) return ST_TOOLARGE;
             needed = header_bytes + 8 * total;
-            break;
+            return ST_OK;
         }
     }
+}
+
+__global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ in_off,
+                                                             const uint64_t* __restrict__ in_len, uint32_t n,
+                                                             uint64_t* __restrict__ out_len,
+                                                             uint64_t* __restrict__ consumed,
+                                                             int32_t* __restrict__ status) {
+    const uint32_t unit = blockIdx.x * kBlock + threadIdx.x;
+    if (unit >= n) return;
+    uint64_t needed = 0;
+    const int32_t st = packed_header(in + in_off[unit], in_len[unit], needed);
     status[unit] = st;
     out_len[unit] = st == ST_OK ? needed : 0;
     consumed[unit] = 0;
@@ -4803,24 +4806,31 @@ __global__ __launch_bounds__(256) void copy_jobs_kernel(const uint64_t* __restri
     }
 }
 
-// The walk of a connection's current message (its framed length `need` known from
-// read_header_kernel) from packed byte X, where the previous read left it, over the bytes
-// the connection now holds: window by window (wv_stage / wv_resolve: a wave per connection,
-// 4.6-KB windows resolved in parallel), counting the words of complete records only. It
-// stops at the first record after which the words reach need / 8 (reader.zig:90-93 and
-// 146-153: OK with consumed = that record's end, or InvalidPackedMessage when the record
-// produced more), or at the last complete record the bytes hold (EndOfStream: X and W saved
-// for the next read). base / avail: the message's start in the arena and its bytes.
+// The walk of a connection's held bytes, message after message: a wave per
+// listed connection. Each message's framed length comes from its header (packed_header on lane
+// 0; need[c] already holds it when the previous read decoded the header), then the walk to its
+// end goes window by window (wv_stage / wv_resolve: 4.6-KB windows resolved in parallel),
+// counting the words of complete records only, from packed byte X of the message, where the
+// previous read left it. A message ends at the first record after which the words reach
+// need / 8 (reader.zig:90-93 and 146-153: OK with the packed bytes up to that record's end, or
+// InvalidPackedMessage when the record produced more); its packed length and framed length go
+// to tab[2 (i M + m)] / [+ 1] and the next message starts there. The walk stops after M
+// messages (status OK: the host walks again), at an error, or at the held bytes' end
+// (EndOfStream): need / X / W then describe the current message for the next read (X from
+// its start; need 0 while its header is incomplete) and cnt[i] the messages found. A message
+// found whole that the caller's frames buffer could not take comes back with W = need / 8 and
+// X at its end: the next walk takes it as found without walking it again.
+// base / avail: the connection's first held byte in the arena and the bytes it holds.
 __global__ __launch_bounds__(kWvBlock) void frame_walk_kernel(const uint8_t* __restrict__ arena,
                                                               const uint32_t* __restrict__ list, uint32_t nl,
                                                               const uint64_t* __restrict__ base,
                                                               const uint64_t* __restrict__ avail,
-                                                              const uint64_t* __restrict__ need,
+                                                              uint64_t* __restrict__ need,
                                                               uint64_t* __restrict__ Xs, uint64_t* __restrict__ Ws,
-                                                              uint64_t* __restrict__ consumed,
                                                               int32_t* __restrict__ status,
                                                               const WinEnt* __restrict__ spec,
-                                                              const uint32_t* __restrict__ spec_first) {
+                                                              const uint32_t* __restrict__ spec_first, uint32_t M,
+                                                              uint32_t* __restrict__ cnt, uint32_t* __restrict__ tab) {
     __shared__ __attribute__((aligned(16))) uint8_t pk_all[kWvWaves * kWvPk];
     __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
     const uint32_t lane = lane_id();
@@ -4831,96 +4841,129 @@ __global__ __launch_bounds__(kWvBlock) void frame_walk_kernel(const uint8_t* __r
         const uint32_t c = __builtin_amdgcn_readfirstlane(list[i]);
         const uint8_t* const src = arena + base[c];
         const uint64_t P = avail[c];
-        const uint64_t Lw = need[c] >> 3;  // framed words (need is a multiple of 8)
+        uint64_t L = need[c];   // the current message's framed bytes (0: header not decoded)
+        uint64_t m0 = 0;        // its first packed byte
         uint64_t x = Xs[c], wd = Ws[c];
+        uint32_t nm = 0;
         int32_t st = ST_EOS;
-        uint64_t cons = 0;
         // windows at fixed positions x0 + j * kWvWin; with a spec table (window_spec_kernel over
         // [x0, P), computed for all windows at once), a window the message neither ends in nor
         // runs out of bytes in is crossed by a table lookup: its exit and word count from the
         // entry d the chain arrives at
         const uint64_t x0 = x;
         const uint32_t sf = spec_first ? __builtin_amdgcn_readfirstlane(spec_first[i]) : kWinNone;
-        while (x < P) {
-            const uint64_t j = (x - x0) / kWvWin;
-            const uint64_t Xj = x0 + j * kWvWin;
-            const uint32_t d = (uint32_t)(x - Xj);
-            if (sf != kWinNone) {
-                const WinEnt* const e = spec + sf + j;
-                const uint64_t vm = e->valid;
-                if (d < kWinD && ((vm >> d) & 1)) {
-                    const int32_t dl = e->delta[d];
-                    const uint32_t ex = e->exit;
-                    if (dl != kDeltaEof && ex != kEOFX) {
-                        const uint64_t words = (uint64_t)((int64_t)e->total + dl);
-                        if (wd + words < Lw) {
-                            wd += words;
-                            x = Xj + ex;
-                            continue;
-                        }
-                    }
-                }
-            }
-            // the window walked exactly from entry d: the message ends in it, the held bytes end
-            // in it, or the table does not know entry d
-            const WvWin w = wv_stage(pk, mk, src, P, Xj, lane);
-            uint32_t ent, cs, ce;
-            const uint32_t xw = wv_resolve(pk, mk, w, d, lane, ent, cs, ce);
-            // the lane's complete records (a record past the held bytes ends the chain)
-            uint32_t words = 0, stop = kEOFX;
-            for (uint32_t r = ent; r < ce;) {
-                uint32_t t = pk[w.sh + r];
-                uint32_t b1 = pk[w.sh + r + 1];
-                uint32_t c9 = pk[w.sh + r + 9];
-                asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
-                const uint32_t len = wv_len(t, c9);
-                if ((uint64_t)r + len > w.rem) {
-                    stop = r;
+        for (;;) {
+            if (L == 0) {  // the next message's header (x == m0, wd == 0)
+                if (nm == M) {
+                    st = ST_OK;
                     break;
                 }
-                words += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
-                r += len;
+                uint64_t nd = 0;
+                int32_t hs = ST_EOS;
+                if (lane == 0) hs = packed_header(src + m0, P - m0, nd);
+                hs = (int32_t)readlane((uint32_t)hs, 0);
+                if (hs != ST_OK) {
+                    st = hs;
+                    break;
+                }
+                L = ((uint64_t)readlane((uint32_t)(nd >> 32), 0) << 32) | readlane((uint32_t)nd, 0);
             }
-            const uint32_t incl = wave_incl_sum(words, lane);
-            const uint32_t total = readlane(incl, kWave - 1);
-            if (wd + total >= Lw) {  // the message ends in this window
-                const uint64_t bm = __ballot(wd + incl >= Lw);
-                const uint32_t f = (uint32_t)__builtin_ctzll(bm);
-                uint32_t end = 0, over = 0;
-                if (lane == f) {
-                    uint64_t acc = wd + incl - words;
-                    for (uint32_t r = ent;;) {
-                        const uint32_t t = pk[w.sh + r], b1 = pk[w.sh + r + 1], c9 = pk[w.sh + r + 9];
-                        acc += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
-                        r += wv_len(t, c9);
-                        if (acc >= Lw) {
-                            end = r;
-                            over = acc != Lw;
-                            break;
+            const uint64_t Lw = L >> 3;  // framed words (L is a multiple of 8)
+            bool ended = wd >= Lw;       // walked whole by an earlier pass (X at its end)
+            while (!ended && x < P) {
+                const uint64_t j = (x - x0) / kWvWin;
+                const uint64_t Xj = x0 + j * kWvWin;
+                const uint32_t d = (uint32_t)(x - Xj);
+                if (sf != kWinNone) {
+                    const WinEnt* const e = spec + sf + j;
+                    const uint64_t vm = e->valid;
+                    if (d < kWinD && ((vm >> d) & 1)) {
+                        const int32_t dl = e->delta[d];
+                        const uint32_t ex = e->exit;
+                        if (dl != kDeltaEof && ex != kEOFX) {
+                            const uint64_t words = (uint64_t)((int64_t)e->total + dl);
+                            if (wd + words < Lw) {
+                                wd += words;
+                                x = Xj + ex;
+                                continue;
+                            }
                         }
                     }
                 }
-                end = readlane(end, f);
-                over = readlane(over, f);
-                cons = Xj + end;
-                st = over ? ST_OVERSHOOT : ST_OK;
-                wd = Lw;
-                break;
-            }
-            if (xw == kEOFX) {  // the chain stops at a record the bytes do not hold yet
-                const uint64_t bm = __ballot(stop != kEOFX);
-                x = bm ? Xj + readlane(stop, (uint32_t)__builtin_ctzll(bm)) : x;
+                // the window walked exactly from entry d: the message ends in it, the held bytes
+                // end in it, or the table does not know entry d
+                const WvWin w = wv_stage(pk, mk, src, P, Xj, lane);
+                uint32_t ent, cs, ce;
+                const uint32_t xw = wv_resolve(pk, mk, w, d, lane, ent, cs, ce);
+                // the lane's complete records (a record past the held bytes ends the chain)
+                uint32_t words = 0, stop = kEOFX;
+                for (uint32_t r = ent; r < ce;) {
+                    uint32_t t = pk[w.sh + r];
+                    uint32_t b1 = pk[w.sh + r + 1];
+                    uint32_t c9 = pk[w.sh + r + 9];
+                    asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));
+                    const uint32_t len = wv_len(t, c9);
+                    if ((uint64_t)r + len > w.rem) {
+                        stop = r;
+                        break;
+                    }
+                    words += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+                    r += len;
+                }
+                const uint32_t incl = wave_incl_sum(words, lane);
+                const uint32_t total = readlane(incl, kWave - 1);
+                if (wd + total >= Lw) {  // the message ends in this window
+                    const uint64_t bm = __ballot(wd + incl >= Lw);
+                    const uint32_t f = (uint32_t)__builtin_ctzll(bm);
+                    uint32_t end = 0, over = 0;
+                    if (lane == f) {
+                        uint64_t acc = wd + incl - words;
+                        for (uint32_t r = ent;;) {
+                            const uint32_t t = pk[w.sh + r], b1 = pk[w.sh + r + 1], c9 = pk[w.sh + r + 9];
+                            acc += 1u + ((t == 0u) ? b1 : 0u) + ((t == 0xFFu) ? c9 : 0u);
+                            r += wv_len(t, c9);
+                            if (acc >= Lw) {
+                                end = r;
+                                over = acc != Lw;
+                                break;
+                            }
+                        }
+                    }
+                    end = readlane(end, f);
+                    over = readlane(over, f);
+                    if (over) {
+                        st = ST_OVERSHOOT;
+                    } else {
+                        x = Xj + end;
+                        ended = true;
+                    }
+                    break;
+                }
+                if (xw == kEOFX) {  // the chain stops at a record the bytes do not hold yet
+                    const uint64_t bm = __ballot(stop != kEOFX);
+                    x = bm ? Xj + readlane(stop, (uint32_t)__builtin_ctzll(bm)) : x;
+                    wd += total;
+                    break;
+                }
+                x = Xj + xw;
                 wd += total;
-                break;
             }
-            x = Xj + xw;
-            wd += total;
+            if (!ended) break;  // EndOfStream (x / wd saved) or the overshoot
+            if (lane == 0) {
+                tab[2 * ((uint64_t)i * M + nm)] = (uint32_t)(x - m0);
+                tab[2 * ((uint64_t)i * M + nm) + 1] = (uint32_t)L;
+            }
+            ++nm;
+            m0 = x;
+            wd = 0;
+            L = 0;
         }
         if (lane == 0) {
-            Xs[c] = x;
-            Ws[c] = wd;
-            consumed[c] = cons;
+            need[c] = st == ST_EOS ? L : 0;
+            Xs[c] = st == ST_EOS ? x - m0 : 0;
+            Ws[c] = st == ST_EOS ? wd : 0;
             status[c] = st;
+            cnt[i] = nm;
         }
     }
 }
@@ -5687,8 +5730,8 @@ uint32_t framer_window_bytes() { return kWvWin; }
 uint64_t framer_window_cap(uint32_t nl) { return win_cap(nl); }
 
 hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_t nl, const uint64_t* base,
-                             const uint64_t* avail, const uint64_t* need, uint64_t* X, uint64_t* W,
-                             uint64_t* consumed, int32_t* status, uint32_t* spec_q, uint64_t windows,
+                             const uint64_t* avail, uint64_t* need, uint64_t* X, uint64_t* W, int32_t* status,
+                             uint32_t M, uint32_t* cnt, uint32_t* tab, uint32_t* spec_q, uint64_t windows,
                              const uint32_t* spec_first, const uint32_t* spec_count, const uint64_t* spec_off,
                              const uint64_t* spec_len, hipStream_t stream) {
     if (nl == 0) return hipSuccess;
@@ -5702,8 +5745,8 @@ hipError_t launch_frame_walk(const uint8_t* arena, const uint32_t* list, uint32_
     }
     static const uint32_t res = resident_blocks(frame_walk_kernel, kWvBlock, 2);
     const uint32_t blocks = std::min((nl + kWvWaves - 1) / kWvWaves, res);
-    frame_walk_kernel<<<blocks, kWvBlock, 0, stream>>>(arena, list, nl, base, avail, need, X, W, consumed, status,
-                                                        spec, spec ? spec_first : nullptr);
+    frame_walk_kernel<<<blocks, kWvBlock, 0, stream>>>(arena, list, nl, base, avail, need, X, W, status, spec,
+                                                        spec ? spec_first : nullptr, M, cnt, tab);
     return hipGetLastError();
 }
 

@@ -256,7 +256,9 @@ int capnp_packed_framer_destroy(capnp_packed_framer* f);
  * popFrame's null), or the reader's error, after which the connection's bytes are dropped (the
  * reset handleRead does, connection.zig:175-184; frames popped before it are listed).
  * OUT_OF_SPACE: `frames` or the frame table filled up; the listed frames are valid and popped,
- * the other whole messages stay buffered: call again (in_bytes = 0) to pop them. */
+ * the other whole messages stay buffered: call again (in_bytes = 0) to pop them.
+ * One walk pass finds every whole message a connection holds (up to 64 per pass), one decode
+ * pass frames them all; page-locked `in` and `frames` let the copies run at the link's rate. */
 int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
                              const uint64_t* in_len, uint8_t* frames, uint64_t frames_cap, uint64_t* frame_off,
                              uint64_t* frame_len, uint32_t* frame_conn, uint32_t max_frames, int32_t* status,
