@@ -405,3 +405,55 @@ def test_framer_session_fuzz_reads():
         assert sess.buffered(c) == 0 and sess.expected(c) == 0
     assert sess.stats()["uploaded_bytes"] == uploaded == sum(len(s) for s in streams)
     sess.close()
+
+
+def test_framer_session_many_messages_per_read():
+    """One read holding more messages than a walk pass finds per connection (64): the pass
+    repeats from where it stopped. Connections with 200 empty messages (2 packed bytes each),
+    130 ordinary ones, 70 then a bad header (the 70 are popped, then the error), exactly 64,
+    and 65 plus part of a 66th (popped once the rest arrives). Then a frame table of 50 entries
+    over 150 messages: three calls (two OUT_OF_SPACE) pop them in order."""
+    import ctypes
+    rng = np.random.default_rng(0x64D5)
+    empty = pyref.frame([b""])
+    m0 = [empty] * 200
+    m1 = [random_message(rng) for _ in range(130)]
+    m2 = [random_message(rng) for _ in range(70)]
+    m3 = [random_message(rng) for _ in range(64)]
+    m4 = [random_message(rng) for _ in range(66)]
+    pk = lambda ms: b"".join(oracle.pack(m)[1] for m in ms)
+    bad = bytes([0x03, 0x57, 0x02])  # 600 segments
+    tail = oracle.pack(m4[65])[1]
+    sess = cp.FramerSession(5)
+    fr, st = sess.read({0: pk(m0), 1: pk(m1), 2: pk(m2) + bad + pk(m3[:2]), 3: pk(m3), 4: pk(m4[:65]) + tail[:3]})
+    got = {c: [bytes(x) for x in v] for c, v in fr.items()}
+    assert got[0] == m0 and got[1] == m1 and got[2] == m2 and got[3] == m3 and got[4] == m4[:65]
+    assert [int(x) for x in st] == [cp.END_OF_STREAM, cp.END_OF_STREAM, cp.SEGMENT_COUNT_LIMIT_EXCEEDED,
+                                    cp.END_OF_STREAM, cp.END_OF_STREAM]
+    assert sess.buffered(4) == 3 and sess.buffered(2) == 0
+    fr, st = sess.read({4: tail[3:]})
+    assert [bytes(x) for x in fr[4]] == [m4[65]] and (st == cp.END_OF_STREAM).all()
+    # a frame table of 50 entries over 150 messages of one connection
+    ms = [random_message(rng) for _ in range(150)]
+    data = pk(ms)
+    host = np.frombuffer(data, dtype=np.uint8).copy()
+    off = np.zeros(5, dtype=np.uint64)
+    ln = np.array([len(data), 0, 0, 0, 0], dtype=np.uint64)
+    buf = np.zeros(sum(len(m) for m in ms) + 64, dtype=np.uint8)
+    fo, fl = np.zeros(50, dtype=np.uint64), np.zeros(50, dtype=np.uint64)
+    fc, stc = np.zeros(50, dtype=np.uint32), np.zeros(5, dtype=np.int32)
+    nf = ctypes.c_uint32(0)
+    L = cp.lib()
+    out, first, calls = [], True, 0
+    while True:
+        rc = L.capnp_packed_framer_read(sess.handle, host.ctypes.data if first else None, len(data) if first else 0,
+                                        off.ctypes.data if first else None, ln.ctypes.data if first else None,
+                                        buf.ctypes.data, buf.size, fo.ctypes.data, fl.ctypes.data, fc.ctypes.data,
+                                        50, stc.ctypes.data, ctypes.byref(nf))
+        first, calls = False, calls + 1
+        assert rc in (cp.OK, cp.OUT_OF_SPACE) and (fc[:nf.value] == 0).all()
+        out += [buf[int(fo[i]):int(fo[i]) + int(fl[i])].tobytes() for i in range(nf.value)]
+        if rc == cp.OK:
+            break
+    assert out == ms and calls == 3 and sess.buffered(0) == 0
+    sess.close()
