@@ -213,6 +213,8 @@ SIGNATURES = {
     "capnp_packed_framer_destroy": (ctypes.c_int, [_vp]),
     "capnp_packed_framer_read": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp,
                                                 _vp, ctypes.c_uint32, _vp, ctypes.POINTER(ctypes.c_uint32)]),
+    "capnp_packed_framer_readv": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
+                                                 ctypes.c_uint32, _vp, ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_framer_reset": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "capnp_packed_framer_buffered": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "capnp_packed_framer_expected": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
@@ -551,8 +553,34 @@ class FramerSession:
         buffer skips assemble()). Returns (parts, status): parts lists (buf, f_off, f_len,
         f_conn) per native call, frame i of a part being buf[f_off[i]:f_off[i] + f_len[i]] of
         connection f_conn[i], a connection's frames in order over the parts; status as read()."""
-        n = self.n
         total = int(lens.sum())
+
+        def first(*out):
+            return lib().capnp_packed_framer_read(self.handle, host.ctypes.data, total, off.ctypes.data,
+                                                  lens.ctypes.data, *out)
+        return self._pop(first, total)
+
+    def readv_raw(self, reads: dict):
+        """read_raw over the connections' own bytes objects (capnp_packed_framer_readv: the
+        library gathers them into its page-locked staging, no host-side layout)."""
+        n = self.n
+        ptrs = (ctypes.c_char_p * n)()
+        lens = np.zeros(n, dtype=np.uint64)
+        keep = []
+        for c, d in reads.items():
+            if len(d):
+                d = d if isinstance(d, bytes) else bytes(d)
+                keep.append(d)  # alive through the call
+                ptrs[c] = d
+                lens[c] = len(d)
+        total = int(lens.sum())
+
+        def first(*out):
+            return lib().capnp_packed_framer_readv(self.handle, ptrs, lens.ctypes.data, *out)
+        return self._pop(first, total)
+
+    def _pop(self, first_call, total: int):
+        n = self.n
         status = np.zeros(n, dtype=np.int32)
         parts = []
         # frames of 2x the read's bytes: the buffer runs out only for messages packed below
@@ -568,11 +596,12 @@ class FramerSession:
             f_conn = np.empty(max_frames, dtype=np.uint32)
             st_call = np.zeros(n, dtype=np.int32)
             nf = ctypes.c_uint32(0)
-            rc = lib().capnp_packed_framer_read(  # later calls pop what is held, no new bytes
-                self.handle, host.ctypes.data if first else None, total if first else 0,
-                off.ctypes.data if first else None, lens.ctypes.data if first else None, buf.ctypes.data, cap,
-                f_off.ctypes.data, f_len.ctypes.data, f_conn.ctypes.data, max_frames, st_call.ctypes.data,
-                ctypes.byref(nf))
+            out = (buf.ctypes.data, cap, f_off.ctypes.data, f_len.ctypes.data, f_conn.ctypes.data, max_frames,
+                   st_call.ctypes.data, ctypes.byref(nf))
+            if first:
+                rc = first_call(*out)
+            else:  # later calls pop what is held, no new bytes
+                rc = lib().capnp_packed_framer_read(self.handle, None, 0, None, None, *out)
             if rc not in (OK, OUT_OF_SPACE):
                 _raise(rc, "framer_read")
             first = False
@@ -592,7 +621,7 @@ class FramerSession:
         return parts, status
 
     def _read(self, reads: dict):
-        parts, status = self.read_raw(*self.assemble(reads))
+        parts, status = self.readv_raw(reads)
         frames = {}
         for buf, f_off, f_len, f_conn in parts:
             # a connection's frames are in order within a call: group them by a stable sort

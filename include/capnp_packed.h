@@ -263,6 +263,16 @@ int capnp_packed_framer_read(capnp_packed_framer* f, const uint8_t* in, uint64_t
                              const uint64_t* in_len, uint8_t* frames, uint64_t frames_cap, uint64_t* frame_off,
                              uint64_t* frame_len, uint32_t* frame_conn, uint32_t max_frames, int32_t* status,
                              uint32_t* n_frames);
+/* capnp_packed_framer_read over the connections' own buffers (the reference keeps one
+ * Framer.buffer per connection, framing.zig:6-8): connection c's new bytes are
+ * in_ptr[c][0 .. in_len[c]) (in_len[c] = 0: none, in_ptr[c] may then be NULL). The library
+ * gathers them into a page-locked staging buffer of the session (by byte range over up to 8
+ * threads from 4 MiB up) and uploads that; no caller-side layout or pinning is needed. Frames,
+ * status and OUT_OF_SPACE as capnp_packed_framer_read (call that, with in_bytes = 0, to pop the
+ * rest). */
+int capnp_packed_framer_readv(capnp_packed_framer* f, const uint8_t* const* in_ptr, const uint64_t* in_len,
+                              uint8_t* frames, uint64_t frames_cap, uint64_t* frame_off, uint64_t* frame_len,
+                              uint32_t* frame_conn, uint32_t max_frames, int32_t* status, uint32_t* n_frames);
 /* Framer.reset (framing.zig:34-37) of one connection: its buffered bytes and state dropped. */
 int capnp_packed_framer_reset(capnp_packed_framer* f, uint32_t conn);
 /* Framer.bufferedBytes (framing.zig:30-32): packed bytes held for the connection. */

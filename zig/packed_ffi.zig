@@ -67,6 +67,12 @@ pub extern "capnp_packed" fn capnp_packed_framer_read(
     frames: [*]u8, frames_cap: u64, frame_off: [*]u64, frame_len: [*]u64, frame_conn: [*]u32,
     max_frames: u32, status: [*]i32, n_frames: *u32,
 ) c_int;
+// the same over each connection's own buffer (Framer.buffer, framing.zig:6-8): no layout needed
+pub extern "capnp_packed" fn capnp_packed_framer_readv(
+    f: *capnp_packed_framer, in_ptr: [*]const ?[*]const u8, in_len: [*]const u64,
+    frames: [*]u8, frames_cap: u64, frame_off: [*]u64, frame_len: [*]u64, frame_conn: [*]u32,
+    max_frames: u32, status: [*]i32, n_frames: *u32,
+) c_int;
 pub extern "capnp_packed" fn capnp_packed_framer_reset(f: *capnp_packed_framer, conn: u32) c_int;
 pub extern "capnp_packed" fn capnp_packed_framer_buffered(f: *capnp_packed_framer, conn: u32, bytes: *u64) c_int;
 pub extern "capnp_packed" fn capnp_packed_framer_expected(f: *capnp_packed_framer, conn: u32, framed_bytes: *u64) c_int;
