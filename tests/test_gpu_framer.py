@@ -457,3 +457,46 @@ def test_framer_session_many_messages_per_read():
             break
     assert out == ms and calls == 3 and sess.buffered(0) == 0
     sess.close()
+
+
+def test_framer_readv_threaded_gather_and_arguments():
+    """capnp_packed_framer_readv: 96 connections holding ~8 MiB of packed messages in all (the
+    threaded gather, by byte range across connection boundaries), a connection with a NULL
+    pointer and length 0, a connection whose read ends inside a message; frames bit-exact
+    against the messages; a NULL pointer with a length is INVALID_ARGUMENT."""
+    import ctypes
+    rng = np.random.default_rng(0x7EAD)
+    n = 96
+    expect, reads = {}, {}
+    for c in range(n):
+        if c == 5:
+            continue  # no bytes: NULL pointer, length 0
+        msgs = [pyref.frame([rng.integers(0, 256, 8 * int(rng.integers(500, 3000))).astype(np.uint8).tobytes()])
+                for _ in range(int(rng.integers(4, 12)))]
+        data = b"".join(oracle.pack(m)[1] for m in msgs)
+        if c == 7:
+            data += oracle.pack(msgs[0])[1][:100]  # a partial message stays buffered
+        expect[c], reads[c] = msgs, data
+    total = sum(len(d) for d in reads.values())
+    assert total > 4 << 20
+    sess = cp.FramerSession(n)
+    parts, status = sess.readv_raw(reads)
+    got = {}
+    for buf, fo, fl, fc in parts:
+        for o, ln, c in zip(fo.tolist(), fl.tolist(), fc.tolist()):
+            got.setdefault(c, []).append(buf[o:o + ln].tobytes())
+    assert got == expect and (status == cp.END_OF_STREAM).all()
+    assert sess.buffered(7) == 100 and sess.buffered(5) == 0
+    ptrs = (ctypes.c_char_p * n)()
+    lens = np.zeros(n, dtype=np.uint64)
+    lens[3] = 10  # bytes claimed behind a NULL pointer
+    buf = np.zeros(64, dtype=np.uint8)
+    fo, fl = np.zeros(4, dtype=np.uint64), np.zeros(4, dtype=np.uint64)
+    fc, stc = np.zeros(4, dtype=np.uint32), np.zeros(n, dtype=np.int32)
+    nf = ctypes.c_uint32(0)
+    rc = cp.lib().capnp_packed_framer_readv(sess.handle, ptrs, lens.ctypes.data, buf.ctypes.data, buf.size,
+                                            fo.ctypes.data, fl.ctypes.data, fc.ctypes.data, 4, stc.ctypes.data,
+                                            ctypes.byref(nf))
+    assert rc == cp.INVALID_ARGUMENT and nf.value == 0
+    assert sess.buffered(7) == 100  # nothing appended
+    sess.close()
