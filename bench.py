@@ -461,7 +461,7 @@ def skewed_leg(args, dev, n=1 << 20, reps=10):
             "note": "SURVEY config C5: truncated Pareto unit sizes 64 B..256 KiB, p = zero_thresh/256"}
 
 
-def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
+def framer_leg(args, dev, conns=4096, msgs=16, reps=int(os.environ.get("CPK_FRAMER_REPS", "5"))):
     """SURVEY §8(f) row 3, RPC framer batching: `conns` connections, each with one socket
     read holding `msgs` packed 1-segment messages (framed 4096 B, p = zero_thresh/256).
     PackedConnections.handle_read pops every frame: one walk pass finds every held message
@@ -490,14 +490,26 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
     packed_bytes = sum(len(v) for v in streams.values())
     # one long-lived session, as an event loop keeps it: the first read also pays the session's
     # device allocations (reported as first_read_ms), later reads of the same batch shape reuse them
-    best, ok, first = None, True, None
+    best, ok, first, all_ms = None, True, None, []
     pc = cp.PackedConnections(conns, device=dev)
+    # the share of each read spent in the native call (FramerSession.readv_raw) vs the views
+    raw_ms, raw0 = [], pc.session.readv_raw
+
+    def timed_raw(reads):
+        t = time.perf_counter()
+        r = raw0(reads)
+        raw_ms.append(round((time.perf_counter() - t) * 1e3, 2))
+        return r
+    pc.session.readv_raw = timed_raw
+    res = None
     for r in range(reps + 1):
+        res = None  # the previous read's frames are handled and dropped before the next read
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res = pc.handle_read(streams)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        all_ms.append(round(dt * 1e3, 2))
         if r == 0:
             first = dt
         else:
@@ -509,6 +521,7 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
         ok &= all(isinstance(v, list) and len(v) == msgs for v in res.values())
     del res
     sess = pc.session
+    del sess.readv_raw
     t0 = time.perf_counter()
     inp = sess.assemble(streams)
     asm = time.perf_counter() - t0
@@ -530,7 +543,7 @@ def framer_leg(args, dev, conns=4096, msgs=16, reps=3):
         del parts
     return {"connections": conns, "messages_per_read": msgs, "framed_bytes": 4096, "packed_bytes": packed_bytes,
             "ms": round(best * 1e3, 2), "framed_GiB_s": round(n * 4096 / best / 2 ** 30, 2),
-            "frames_per_s": round(n / best), "first_read_ms": round(first * 1e3, 2),
+            "frames_per_s": round(n / best), "first_read_ms": round(first * 1e3, 2), "reads_ms": all_ms, "reads_readv_ms": raw_ms,
             "native_ms": round(nat * 1e3, 2), "native_framed_GiB_s": round(n * 4096 / nat / 2 ** 30, 2),
             "readv_ms": round(rv * 1e3, 2), "assemble_ms": round(asm * 1e3, 2), "bit_exact": bool(ok),
             "note": "host buffers in and out (PCIe + host-side framing); one framer session, best of the reads "

@@ -747,6 +747,15 @@ class PackedConnections:
         """One native call: the connections' new bytes go to the device once, every whole
         message is popped, and the frames come back as read-only memoryviews of the call's
         frame buffer (no per-frame copy; the buffer lives as long as its frames)."""
+        gc_on = gc.isenabled()
+        gc.disable()  # the result's lists and views hold no cycles (DESIGN.md §2.7)
+        try:
+            return self._handle_read(reads)
+        finally:
+            if gc_on:
+                gc.enable()
+
+    def _handle_read(self, reads: dict) -> dict:
         live = {c: d for c, d in reads.items() if not self.closed[c] and len(d)}
         frames, status = self.session.read(live)
         result = {c: [] for c in live}

@@ -747,7 +747,8 @@ struct capnp_packed_framer {
         const hipError_t e = hipStreamSynchronize(s);
         return e == hipSuccess ? CAPNP_PACKED_OK : hip_fail(e, "framer copy jobs");
     }
-    int run_jobs(std::vector<uint64_t>& jobs, bool wait = true) {
+    // The first `first` jobs run as a launch of their own, before the others (stream order).
+    int run_jobs(std::vector<uint64_t>& jobs, bool wait = true, uint32_t first = 0) {
         if (jobs.empty()) return CAPNP_PACKED_OK;
         const uint32_t nj = (uint32_t)(jobs.size() / 3);
         // the jobs go after the per-connection arrays in the state scratch
@@ -756,7 +757,8 @@ struct capnp_packed_framer {
         if (st) return st;
         uint64_t* const dj = reinterpret_cast<uint64_t*>(d_state + at);
         hipError_t e = hipMemcpyAsync(dj, jobs.data(), jobs.size() * 8, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = cpk::launch_copy_jobs(dj, nj, s);
+        if (e == hipSuccess && first) e = cpk::launch_copy_jobs(dj, first, s);
+        if (e == hipSuccess) e = cpk::launch_copy_jobs(dj + 3ull * first, nj - first, s);
         if (e == hipSuccess && wait) e = hipStreamSynchronize(s);  // `jobs` is reused by the caller
         if (e != hipSuccess) return hip_fail(e, "framer copy jobs");
         if (wait) jobs.clear();
@@ -936,24 +938,45 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         e = hipMemcpyAsync(f->d_stage, in, in_bytes, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
         f->uploaded += in_bytes;
-        // regions: a connection whose bytes would pass its region's end gets a new one
+        // regions: a connection whose bytes would pass its region's end slides its held bytes to
+        // the region's start when they and the new bytes fit there and the slide's source and
+        // target do not overlap (held <= m0; a drained connection just restarts there), else it
+        // gets a new region. The slides run as a launch of their own before the appends, which may
+        // overwrite their source.
+        auto slides = [&](uint32_t c) {
+            const uint64_t held = f->len[c] - f->m0[c];
+            return in_len[c] && f->len[c] + in_len[c] > f->cap[c] && held + in_len[c] <= f->cap[c] && held <= f->m0[c];
+        };
         std::vector<uint64_t> want(n, 0);
         uint64_t grow_bytes = 0;
         bool any_grow = false;
         for (uint32_t c = 0; c < n; ++c) {
             const uint64_t live = f->len[c] - f->m0[c] + in_len[c];
             want[c] = live;
-            if (in_len[c] && f->len[c] + in_len[c] > f->cap[c]) {
+            if (in_len[c] && f->len[c] + in_len[c] > f->cap[c] && !slides(c)) {
                 any_grow = true;
                 grow_bytes += capnp_packed_framer::region_for(live);
             }
         }
         std::vector<uint64_t>& jobs = f->hjobs;
         jobs.clear();
+        uint32_t n_slides = 0;
         if (any_grow && f->top + grow_bytes > f->acap) {
             if ((st = f->rearena(want))) return st;  // every region sized for its bytes after this read
-        } else if (any_grow) {
+        } else {
             for (uint32_t c = 0; c < n; ++c) {
+                if (!slides(c)) continue;
+                const uint64_t held = f->len[c] - f->m0[c];
+                if (held) {
+                    jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + f->off[c]),
+                                             reinterpret_cast<uint64_t>(f->arena + f->off[c] + f->m0[c]), held});
+                    f->moved += held;
+                    ++n_slides;
+                }
+                f->m0[c] = 0;
+                f->len[c] = held;
+            }
+            for (uint32_t c = 0; any_grow && c < n; ++c) {  // the slid ones fit now
                 if (!in_len[c] || f->len[c] + in_len[c] <= f->cap[c]) continue;
                 const uint64_t live = f->len[c] - f->m0[c];
                 const uint64_t rc = capnp_packed_framer::region_for(want[c]);
@@ -975,7 +998,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
                                      reinterpret_cast<uint64_t>(f->d_stage + in_off[c]), in_len[c]});
             f->len[c] += in_len[c];
         }
-        if ((st = f->run_jobs(jobs, false))) return st;  // ordered before the passes below
+        if ((st = f->run_jobs(jobs, false, n_slides))) return st;  // ordered before the passes below
     }
 
     // ---- 2. passes: a walk over every connection's held messages, then one decode of them ----
