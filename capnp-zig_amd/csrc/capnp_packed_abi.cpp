@@ -1051,8 +1051,10 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         uint32_t* const r_list = reinterpret_cast<uint32_t*>(f->d_round);
         uint32_t* const r_cnt = r_list + k;
         uint32_t* const r_tab = r_cnt + k;
-        // window tables for the connections whose bytes past the walk's start span more than
-        // one window (a message split over many reads, or many messages: crossed by lookups)
+        // window tables for the connections whose walk will cross whole windows inside one
+        // message (crossed by lookups): the current message's framed bytes still to walk span
+        // more than two windows, or, with its header not decoded yet, the held bytes span 64
+        // windows. Many small messages end in nearly every window, where a table only costs.
         const uint64_t wb = cpk::framer_window_bytes(), wcap = cpk::framer_window_cap(k);
         spec_h.assign(2ull * k, 0);  // first, count per listed connection (u32); off, len (u64) below
         spec_h64.assign(2ull * k, 0);
@@ -1060,7 +1062,9 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         for (uint32_t j = 0; j < k; ++j) {
             const uint32_t c = list[j];
             const uint64_t span = f->len[c] - f->m0[c] - f->X[c];
-            uint64_t cnt = span > wb ? (span + wb - 1) / wb : 0;
+            const uint64_t left = f->need[c] > 8 * f->W[c] ? f->need[c] - 8 * f->W[c] : 0;
+            const bool lookups = f->need[c] ? left > 2 * wb : span > 64 * wb;
+            uint64_t cnt = lookups && span > wb ? (span + wb - 1) / wb : 0;
             if (T + cnt > wcap) cnt = 0;
             spec_h[j] = cnt ? (uint32_t)T : 0xFFFFFFFFu;
             spec_h[k + j] = (uint32_t)cnt;
