@@ -461,7 +461,7 @@ def skewed_leg(args, dev, n=1 << 20, reps=10):
             "note": "SURVEY config C5: truncated Pareto unit sizes 64 B..256 KiB, p = zero_thresh/256"}
 
 
-def framer_leg(args, dev, conns=4096, msgs=16, reps=int(os.environ.get("CPK_FRAMER_REPS", "5"))):
+def framer_leg(args, dev, conns=4096, msgs=16, reps=5):
     """SURVEY §8(f) row 3, RPC framer batching: `conns` connections, each with one socket
     read holding `msgs` packed 1-segment messages (framed 4096 B, p = zero_thresh/256).
     PackedConnections.handle_read pops every frame: one walk pass finds every held message

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -883,6 +884,25 @@ int capnp_packed_framer_stats(capnp_packed_framer* f, uint64_t* uploaded, uint64
 
 namespace {
 
+#if CPK_FRAMER_PROF  // dev builds: wall-time marks of a framer read on stderr
+struct FrProf {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+    std::string line;
+    void mark(const char* what) {
+        const auto t = std::chrono::steady_clock::now();
+        char b[64];
+        std::snprintf(b, sizeof b, " %s %.2f", what, std::chrono::duration<double, std::milli>(t - last).count());
+        line += b;
+        last = t;
+    }
+    ~FrProf() { std::fprintf(stderr, "[framer_read]%s\n", line.c_str()); }
+};
+#define FR_MARK(p, w) (p).mark(w)
+#else
+struct FrProf {};
+#define FR_MARK(p, w) ((void)(p))
+#endif
+
 // The gather of capnp_packed_framer_readv: the connections' reads into the session's page-locked
 // staging at their prefix offsets, by byte range over up to 8 threads from 4 MiB up.
 void gather_reads(uint8_t* dst, const uint8_t* const* ptr, const uint64_t* len, const uint64_t* off, uint32_t n,
@@ -927,6 +947,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
                        uint32_t* n_frames) {
     const uint32_t n = f->n;
     const hipStream_t s = f->s;
+    FrProf prof;
     hipError_t e = hipSuccess;
     int st = CAPNP_PACKED_OK;
     for (uint32_t c = 0; c < n; ++c) status[c] = CAPNP_PACKED_END_OF_STREAM;
@@ -1000,6 +1021,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         }
         if ((st = f->run_jobs(jobs, false, n_slides))) return st;  // ordered before the passes below
     }
+    FR_MARK(prof, "upload");
 
     // ---- 2. passes: a walk over every connection's held messages, then one decode of them ----
     // state scratch: base, avail, need, X, W (u64 x n), status (i32 x n), then the copy jobs
@@ -1103,6 +1125,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         if (e == hipSuccess) e = hipMemcpyAsync(hcnt.data(), r_cnt, 4ull * (k + tab_words), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "framer walk pass");
+        FR_MARK(prof, "walk");
         f->jobs_inflight = false;
         // whole messages, in order per connection, while the frames buffer and table hold them:
         // decoded from the arena into frame slots, then to the caller's buffer
@@ -1155,6 +1178,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
             if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 4ull * U, u + 4ull * U, 2ull * U * 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) return hip_fail(e, "framer decode pass");
+            FR_MARK(prof, "decode");
             const int32_t* const us = reinterpret_cast<const int32_t*>(hm.data() + 5ull * U);
             for (uint32_t q = 0; q < U; ++q) {
                 if (us[q] != CAPNP_PACKED_OK || hm[4ull * U + q] != hm[3ull * U + q])  // the walk verified the bytes
@@ -1176,6 +1200,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         }
     }
     *n_frames = nf;
+    FR_MARK(prof, "host");
     if ((st = f->settle())) return st;  // no pass ran after the upload: the caller's bytes are consumed
     return full ? fail(CAPNP_PACKED_OUT_OF_SPACE, "frames buffer or frame table full: call again to pop the rest")
                 : CAPNP_PACKED_OK;
@@ -1231,7 +1256,15 @@ int capnp_packed_framer_readv(capnp_packed_framer* f, const uint8_t* const* in_p
             }
             f->h_stage_cap = want;
         }
+#if CPK_FRAMER_PROF  // dev builds: the gather's wall time per call on stderr
+        const auto g0 = std::chrono::steady_clock::now();
+#endif
         gather_reads(f->h_stage, in_ptr, in_len, off.data(), n, total);
+#if CPK_FRAMER_PROF
+        std::fprintf(stderr, "[framer_readv] gather %.3f ms for %llu bytes\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count(),
+                     (unsigned long long)total);
+#endif
     }
     return framer_read_locked(f, total ? f->h_stage : nullptr, total, total ? off.data() : nullptr,
                               total ? in_len : nullptr, frames, frames_cap, frame_off, frame_len, frame_conn,

@@ -70,6 +70,9 @@ for r in range(5):
     t1 = time.perf_counter()
     res = new
     t2 = time.perf_counter()
+    if os.environ.get("FR_VERIFY"):  # the bench leg's check between reads: CPU reads of a few frames
+        for c in (0, conns // 2, conns - 1):
+            assert all(len(bytes(x)) == 4096 for x in res[c])
     print(f"read {r}: handle_read {1e3 * (t1 - t0):.2f} ms (readv_raw {1e3 * T['readv_raw']:.2f}, grouping "
           f"{1e3 * (T['_read'] - T['readv_raw']):.2f}, result {1e3 * (t1 - t0 - T['_read']):.2f}), "
           f"drop previous {1e3 * (t2 - t1):.2f} ms", flush=True)
