@@ -711,6 +711,29 @@ struct capnp_packed_framer {
     uint64_t units_cap = 0;
     uint8_t* h_stage = nullptr;  // page-locked gather of capnp_packed_framer_readv's reads
     uint64_t h_stage_cap = 0;
+    // page-locked host sides of a read's metadata copies: per-connection state, a walk pass's
+    // counts and message table, a decode pass's unit metadata (no pageable staging per copy)
+    struct Pinned {
+        uint8_t* p = nullptr;
+        uint64_t cap = 0;
+        int reserve(uint64_t bytes) {
+            if (p && bytes <= cap) return CAPNP_PACKED_OK;
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            const uint64_t want = std::max<uint64_t>(bytes + bytes / 2, 4096);
+            const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault);
+            if (e != hipSuccess) {
+                p = nullptr;
+                return hip_fail(e, "hipHostMalloc(framer metadata)");
+            }
+            cap = want;
+            return CAPNP_PACKED_OK;
+        }
+        ~Pinned() {
+            if (p) (void)hipHostFree(p);
+        }
+    } pin_state, pin_tab, pin_units;
     uint64_t uploaded = 0, moved = 0;  // bytes copied H2D (new reads) and moved between regions
     static constexpr uint32_t kWalkMessages = 64;  // messages a walk pass finds per connection
 
@@ -1035,12 +1058,13 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
     uint64_t* const d_W = d_base + 4ull * n;
     int32_t* const d_st = reinterpret_cast<int32_t*>(d_base + 6ull * n);
     constexpr uint32_t M = capnp_packed_framer::kWalkMessages;
-    std::vector<uint64_t> h(7ull * n);  // base, avail, need, X, W, (free), status (i32)
+    if ((st = f->pin_state.reserve(56ull * n))) return st;
+    uint64_t* const h = reinterpret_cast<uint64_t*>(f->pin_state.p);  // base, avail, need, X, W, (free), status (i32)
     std::vector<uint32_t> spec_h;    // window tables' first / count per listed connection
     std::vector<uint64_t> spec_h64;  // their bytes: arena offset, length
     uint64_t spec_T = 0;
-    const int32_t* const hst = reinterpret_cast<const int32_t*>(h.data() + 6ull * n);
-    std::vector<uint32_t> list, hcnt;
+    const int32_t* const hst = reinterpret_cast<const int32_t*>(h + 6ull * n);
+    std::vector<uint32_t> list;
     std::vector<uint8_t> dead(n, 0), more(n, 0);  // dead: an error this call (the connection was reset)
     std::vector<uint64_t> adv(n), um;             // adv: packed bytes of the pass's accepted messages
     std::vector<uint32_t> uconn;                  // the pass's accepted messages: connection
@@ -1114,15 +1138,16 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
             if (e == hipSuccess) e = hipMemcpyAsync(a64, spec_h64.data(), 16ull * k, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) return hip_fail(e, "framer window tables");
         }
-        hcnt.resize(k + tab_words);  // the counts, then the message table
-        e = hipMemcpyAsync(d_base, h.data(), 5ull * n * 8, hipMemcpyHostToDevice, s);
+        if ((st = f->pin_tab.reserve(4ull * (k + tab_words)))) return st;
+        const uint32_t* const hcnt = reinterpret_cast<const uint32_t*>(f->pin_tab.p);  // counts, then the table
+        e = hipMemcpyAsync(d_base, h, 5ull * n * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(r_list, list.data(), 4ull * k, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)
             e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_st, M, r_cnt, r_tab,
                                        d_sq, T, d_sfirst, d_scount, d_soff, d_slen, s);
         // need, X, W, (a free slot), status: one copy; the counts and the table: another
-        if (e == hipSuccess) e = hipMemcpyAsync(h.data() + 2ull * n, d_need, 3ull * n * 8 + n * 8 + 4ull * n, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(hcnt.data(), r_cnt, 4ull * (k + tab_words), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(h + 2ull * n, d_need, 3ull * n * 8 + n * 8 + 4ull * n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(f->pin_tab.p, r_cnt, 4ull * (k + tab_words), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "framer walk pass");
         FR_MARK(prof, "walk");
@@ -1134,7 +1159,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         uint64_t slots = 0;
         for (uint32_t j = 0; j < k; ++j) {
             const uint32_t c = list[j];
-            const uint32_t* const tj = hcnt.data() + k + 2ull * j * M;
+            const uint32_t* const tj = hcnt + k + 2ull * j * M;
             uint64_t at = 0;
             uint32_t m = 0;
             for (; m < hcnt[j]; ++m) {
@@ -1166,20 +1191,21 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
             if ((st = capnp_packed_framer::grow(&f->d_frames, &f->frames_dcap, slots + 16))) return st;
             if ((st = capnp_packed_framer::grow(&f->d_units, &f->units_cap, 48ull * U + 64))) return st;
             uint64_t* const u = reinterpret_cast<uint64_t*>(f->d_units);
-            std::vector<uint64_t> hm(6ull * U);
+            if ((st = f->pin_units.reserve(48ull * U))) return st;
+            uint64_t* const hm = reinterpret_cast<uint64_t*>(f->pin_units.p);
             for (uint32_t q = 0; q < U; ++q)
                 for (uint32_t a = 0; a < 4; ++a) hm[a * (uint64_t)U + q] = um[4ull * q + a];
-            e = hipMemcpyAsync(u, hm.data(), 4ull * U * 8, hipMemcpyHostToDevice, s);
+            e = hipMemcpyAsync(u, hm, 4ull * U * 8, hipMemcpyHostToDevice, s);
             int32_t* const u_st = reinterpret_cast<int32_t*>(u + 5ull * U);
             if (e == hipSuccess)
                 e = cpk::launch_decode(f->arena, u, u + U, U, f->d_frames, u + 2ull * U, u + 3ull * U, u + 4ull * U,
                                        u_st, true, nullptr, 0, s);
             if (e == hipSuccess) e = hipMemcpyAsync(frames + fcur, f->d_frames, slots, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(hm.data() + 4ull * U, u + 4ull * U, 2ull * U * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hm + 4ull * U, u + 4ull * U, 2ull * U * 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) return hip_fail(e, "framer decode pass");
             FR_MARK(prof, "decode");
-            const int32_t* const us = reinterpret_cast<const int32_t*>(hm.data() + 5ull * U);
+            const int32_t* const us = reinterpret_cast<const int32_t*>(hm + 5ull * U);
             for (uint32_t q = 0; q < U; ++q) {
                 if (us[q] != CAPNP_PACKED_OK || hm[4ull * U + q] != hm[3ull * U + q])  // the walk verified the bytes
                     return fail(CAPNP_PACKED_DEVICE_ERROR, "framer: a walked message did not decode to its framed length");
