@@ -926,10 +926,11 @@ struct FrProf {};
 #define FR_MARK(p, w) ((void)(p))
 #endif
 
-// The gather of capnp_packed_framer_readv: the connections' reads into the session's page-locked
-// staging at their prefix offsets, by byte range over up to 8 threads from 4 MiB up.
+// The gather of capnp_packed_framer_readv: bytes [r0, r1) of the connections' reads, laid end
+// to end at their prefix offsets, into the session's page-locked staging, by byte range over up
+// to 8 threads from 4 MiB up.
 void gather_reads(uint8_t* dst, const uint8_t* const* ptr, const uint64_t* len, const uint64_t* off, uint32_t n,
-                  uint64_t total) {
+                  uint64_t r0, uint64_t r1) {
     auto copy_range = [=](uint64_t b0, uint64_t b1) {
         // the first connection whose bytes end past b0
         uint32_t c = (uint32_t)(std::upper_bound(off, off + n, b0) - off);
@@ -940,16 +941,16 @@ void gather_reads(uint8_t* dst, const uint8_t* const* ptr, const uint64_t* len, 
             if (lo < hi) std::memcpy(dst + lo, ptr[c] + (lo - off[c]), hi - lo);
         }
     };
+    const uint64_t total = r1 - r0;
     const unsigned hw = std::thread::hardware_concurrency();
     const unsigned T = total < (4ull << 20) ? 1u : std::max(1u, std::min(8u, hw ? hw : 1u));
     std::vector<std::thread> th;
     try {
-        for (unsigned t = 1; t < T; ++t) th.emplace_back(copy_range, total * t / T, total * (t + 1) / T);
+        for (unsigned t = 1; t < T; ++t) th.emplace_back(copy_range, r0 + total * t / T, r0 + total * (t + 1) / T);
     } catch (...) {  // no threads: the rest on this one
-        const uint64_t done_from = total * (th.size() + 1) / T;
-        copy_range(done_from, total);
+        copy_range(r0 + total * (th.size() + 1) / T, r1);
     }
-    copy_range(0, total / T);
+    copy_range(r0, r0 + total / T);
     for (auto& x : th) x.join();
 }
 
@@ -964,10 +965,11 @@ int framer_args(capnp_packed_framer* f, uint8_t* frames, uint64_t frames_cap, ui
 }
 
 // capnp_packed_framer_read with f->mu held and its arguments checked
+// (staged: the caller already put the input's bytes into d_stage on the session's stream)
 int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
                        const uint64_t* in_len, uint8_t* frames, uint64_t frames_cap, uint64_t* frame_off,
                        uint64_t* frame_len, uint32_t* frame_conn, uint32_t max_frames, int32_t* status,
-                       uint32_t* n_frames) {
+                       uint32_t* n_frames, bool staged = false) {
     const uint32_t n = f->n;
     const hipStream_t s = f->s;
     FrProf prof;
@@ -978,9 +980,11 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
     // ---- 1. the new bytes: one H2D into the staging buffer, appended to the regions ---------
     if ((st = f->settle())) return st;  // a previous read's copies are done with d_stage / hjobs
     if (in_bytes && in_len) {
-        if ((st = capnp_packed_framer::grow(&f->d_stage, &f->stage_cap, in_bytes + 32))) return st;
-        e = hipMemcpyAsync(f->d_stage, in, in_bytes, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
+        if (!staged) {
+            if ((st = capnp_packed_framer::grow(&f->d_stage, &f->stage_cap, in_bytes + 32))) return st;
+            e = hipMemcpyAsync(f->d_stage, in, in_bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
+        }
         f->uploaded += in_bytes;
         // regions: a connection whose bytes would pass its region's end slides its held bytes to
         // the region's start when they and the new bytes fit there and the slide's source and
@@ -1282,19 +1286,28 @@ int capnp_packed_framer_readv(capnp_packed_framer* f, const uint8_t* const* in_p
             }
             f->h_stage_cap = want;
         }
+        // gather and upload in 32-MiB pieces: piece i's H2D runs while piece i + 1 is gathered
+        if ((st = f->settle())) return st;  // the previous read's copies are done with d_stage
+        if ((st = capnp_packed_framer::grow(&f->d_stage, &f->stage_cap, total + 32))) return st;
 #if CPK_FRAMER_PROF  // dev builds: the gather's wall time per call on stderr
         const auto g0 = std::chrono::steady_clock::now();
 #endif
-        gather_reads(f->h_stage, in_ptr, in_len, off.data(), n, total);
+        constexpr uint64_t kPiece = 32ull << 20;
+        for (uint64_t r0 = 0; r0 < total; r0 += kPiece) {
+            const uint64_t r1 = std::min(total, r0 + kPiece);
+            gather_reads(f->h_stage, in_ptr, in_len, off.data(), n, r0, r1);
+            const hipError_t e = hipMemcpyAsync(f->d_stage + r0, f->h_stage + r0, r1 - r0, hipMemcpyHostToDevice, f->s);
+            if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
+        }
 #if CPK_FRAMER_PROF
-        std::fprintf(stderr, "[framer_readv] gather %.3f ms for %llu bytes\n",
+        std::fprintf(stderr, "[framer_readv] gather + upload enqueue %.3f ms for %llu bytes\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count(),
                      (unsigned long long)total);
 #endif
     }
     return framer_read_locked(f, total ? f->h_stage : nullptr, total, total ? off.data() : nullptr,
                               total ? in_len : nullptr, frames, frames_cap, frame_off, frame_len, frame_conn,
-                              max_frames, status, n_frames);
+                              max_frames, status, n_frames, true);
 }
 
 }  // extern "C"
