@@ -733,7 +733,7 @@ struct capnp_packed_framer {
         ~Pinned() {
             if (p) (void)hipHostFree(p);
         }
-    } pin_state, pin_tab, pin_units;
+    } pin_state, pin_tab, pin_units, pin_jobs;
     uint64_t uploaded = 0, moved = 0;  // bytes copied H2D (new reads) and moved between regions
     static constexpr uint32_t kWalkMessages = 64;  // messages a walk pass finds per connection
 
@@ -780,7 +780,9 @@ struct capnp_packed_framer {
         int st = grow(&d_state, &state_cap, at + jobs.size() * 8 + 64 * (uint64_t)n + 4096);
         if (st) return st;
         uint64_t* const dj = reinterpret_cast<uint64_t*>(d_state + at);
-        hipError_t e = hipMemcpyAsync(dj, jobs.data(), jobs.size() * 8, hipMemcpyHostToDevice, s);
+        if ((st = pin_jobs.reserve(jobs.size() * 8))) return st;  // page-locked: no staged copy
+        std::memcpy(pin_jobs.p, jobs.data(), jobs.size() * 8);
+        hipError_t e = hipMemcpyAsync(dj, pin_jobs.p, jobs.size() * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess && first) e = cpk::launch_copy_jobs(dj, first, s);
         if (e == hipSuccess) e = cpk::launch_copy_jobs(dj + 3ull * first, nj - first, s);
         if (e == hipSuccess && wait) e = hipStreamSynchronize(s);  // `jobs` is reused by the caller
@@ -1062,7 +1064,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
     uint64_t* const d_W = d_base + 4ull * n;
     int32_t* const d_st = reinterpret_cast<int32_t*>(d_base + 6ull * n);
     constexpr uint32_t M = capnp_packed_framer::kWalkMessages;
-    if ((st = f->pin_state.reserve(56ull * n))) return st;
+    if ((st = f->pin_state.reserve(60ull * n))) return st;  // 7 u64 then the pass's list (u32) per connection
     uint64_t* const h = reinterpret_cast<uint64_t*>(f->pin_state.p);  // base, avail, need, X, W, (free), status (i32)
     std::vector<uint32_t> spec_h;    // window tables' first / count per listed connection
     std::vector<uint64_t> spec_h64;  // their bytes: arena offset, length
@@ -1145,7 +1147,9 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         if ((st = f->pin_tab.reserve(4ull * (k + tab_words)))) return st;
         const uint32_t* const hcnt = reinterpret_cast<const uint32_t*>(f->pin_tab.p);  // counts, then the table
         e = hipMemcpyAsync(d_base, h, 5ull * n * 8, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(r_list, list.data(), 4ull * k, hipMemcpyHostToDevice, s);
+        uint32_t* const plist = reinterpret_cast<uint32_t*>(f->pin_state.p + 56ull * n);
+        std::memcpy(plist, list.data(), 4ull * k);
+        if (e == hipSuccess) e = hipMemcpyAsync(r_list, plist, 4ull * k, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)
             e = cpk::launch_frame_walk(f->arena, r_list, k, d_base, d_avail, d_need, d_X, d_W, d_st, M, r_cnt, r_tab,
                                        d_sq, T, d_sfirst, d_scount, d_soff, d_slen, s);
