@@ -40,6 +40,9 @@ if os.environ.get("FR_PRE"):
         legs[name](args, dev)
         torch.cuda.empty_cache()
         print(f"pre-leg {name} {time.perf_counter() - t:.1f} s", flush=True)
+    if os.environ.get("FR_RELEASE"):  # drop the side streams the legs' batches created
+        rc = cp.lib().capnp_packed_stream_release(torch.cuda.current_stream().cuda_stream)
+        print(f"stream_release rc={rc}", flush=True)
 print(f"ballast {len(ballast)} objects", flush=True)
 T = {}
 sess_cls = cp.FramerSession
