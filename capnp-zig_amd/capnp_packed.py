@@ -626,10 +626,12 @@ class FramerSession:
         for buf, f_off, f_len, f_conn in parts:
             # a connection's frames are in order within a call: group them by a stable sort
             view = memoryview(buf).toreadonly()
-            order = np.argsort(f_conn, kind="stable")
-            conn_s = f_conn[order]
-            fo = f_off[order]
-            fo_l, fe_l = fo.tolist(), (fo + f_len[order]).tolist()
+            if len(f_conn) > 1 and bool((f_conn[1:] < f_conn[:-1]).any()):  # a later pass's frames
+                order = np.argsort(f_conn, kind="stable")
+                conn_s, fo, fl = f_conn[order], f_off[order], f_len[order]
+            else:  # one walk pass: already grouped by connection, in order
+                conn_s, fo, fl = f_conn, f_off, f_len
+            fo_l, fe_l = fo.tolist(), (fo + fl).tolist()
             cuts = (np.flatnonzero(np.diff(conn_s)) + 1).tolist()
             starts = [0] + cuts
             for c, a, b in zip(conn_s[starts].tolist(), starts, cuts + [len(conn_s)]):
