@@ -138,3 +138,26 @@ def test_packed_framer_host_logic(monkeypatch):
     assert e.value.status == cp.INVALID_SEGMENT_COUNT
     f.reset()
     assert f.buffered_bytes() == 0 and f.pop_frame() is None
+
+
+def test_framer_session_groups_frames_per_connection():
+    """FramerSession.read's grouping of the native calls' frame tables (no device): frames of a
+    connection in order across calls, whether a call's table is already grouped by connection
+    (one walk pass) or interleaved (several passes), as read-only views of the call's buffer."""
+    sess = object.__new__(cp.FramerSession)
+    sess.n, sess.handle = 4, None
+    buf1 = np.frombuffer(b"".join(bytes([i]) * 8 for i in range(6)), dtype=np.uint8).copy()
+    buf2 = np.frombuffer(b"".join(bytes([100 + i]) * 8 for i in range(5)), dtype=np.uint8).copy()
+    u64 = lambda xs: np.array(xs, dtype=np.uint64)  # noqa: E731
+    parts = [  # call 1: grouped (connections 0, 0, 1, 3, 3, 3); call 2: interleaved passes
+        (buf1, u64([0, 8, 16, 24, 32, 40]), u64([8] * 6), np.array([0, 0, 1, 3, 3, 3], dtype=np.uint32)),
+        (buf2, u64([0, 8, 16, 24, 32]), u64([8] * 5), np.array([1, 3, 0, 1, 3], dtype=np.uint32)),
+    ]
+    status = np.full(4, cp.END_OF_STREAM, dtype=np.int32)
+    sess.readv_raw = lambda reads: (parts, status)
+    frames, st = sess.read({0: b"x"})
+    got = {c: [bytes(v) for v in fr] for c, fr in frames.items()}
+    assert got == {0: [bytes([0]) * 8, bytes([1]) * 8, bytes([102]) * 8],
+                   1: [bytes([2]) * 8, bytes([100]) * 8, bytes([103]) * 8],
+                   3: [bytes([3]) * 8, bytes([4]) * 8, bytes([5]) * 8, bytes([101]) * 8, bytes([104]) * 8]}
+    assert all(v.readonly for fr in frames.values() for v in fr) and (st == cp.END_OF_STREAM).all()
