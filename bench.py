@@ -949,8 +949,8 @@ def main():
             torch.cuda.empty_cache()
             extra["message_framing"] = message_leg(args, dev)
         if not args.no_read_message:
-            # before C5: right after the C5 leg the framer's first reads run 2x slower, an
-            # interaction between the legs that is not understood yet
+            # before C5 (the framer's first reads in a bench process sometimes run
+            # 2x slower, cause open; reads_ms shows which case a run hit)
             torch.cuda.empty_cache()
             extra["rpc_framer"] = framer_leg(args, dev)
             torch.cuda.empty_cache()
