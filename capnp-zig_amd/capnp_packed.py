@@ -204,6 +204,7 @@ SIGNATURES = {
                                                       ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                                       ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_stream_release": (ctypes.c_int, [_vp]),
+    "capnp_packed_stream_contexts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_stream_queue_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t),
                                                       ctypes.POINTER(ctypes.c_uint32)]),
     "capnp_packed_set_decoder": (ctypes.c_int, [ctypes.c_int]),
@@ -223,7 +224,7 @@ SIGNATURES = {
 }
 
 # capnp_packed_set_decoder values (include/capnp_packed.h)
-DECODERS = {"auto": 0, "twopass": 1, "fused": 2, "stream": 3}
+DECODERS = {"auto": 0, "twopass": 1, "fused": 2, "stream": 3, "words": 4}
 # capnp_packed_set_launch_flags bits (include/capnp_packed.h)
 LAUNCH_LONG_INLINE = 0x1
 LAUNCH_MID_SIDE_STREAM = 0x2
@@ -603,7 +604,15 @@ class FramerSession:
             else:  # later calls pop what is held, no new bytes
                 rc = lib().capnp_packed_framer_read(self.handle, None, 0, None, None, *out)
             if rc not in (OK, OUT_OF_SPACE):
-                _raise(rc, "framer_read")
+                try:
+                    _raise(rc, "framer_read")
+                except PackedError as exc:
+                    # the session already advanced past the frames of earlier calls of this read:
+                    # hand them over with the error instead of losing them (exc.partial, as read_raw
+                    # returns them: (parts, status))
+                    status[status == 0] = END_OF_STREAM
+                    exc.partial = (parts, status)
+                    raise
             first = False
             err = st_call != END_OF_STREAM
             status[err] = st_call[err]
@@ -621,7 +630,16 @@ class FramerSession:
         return parts, status
 
     def _read(self, reads: dict):
-        parts, status = self.readv_raw(reads)
+        try:
+            parts, status = self.readv_raw(reads)
+        except PackedError as exc:
+            if hasattr(exc, "partial"):  # frames popped before the failing call: exc.frames
+                exc.frames = self._group(*exc.partial)[0]
+            raise
+        return self._group(parts, status)
+
+    @staticmethod
+    def _group(parts, status):
         frames = {}
         for buf, f_off, f_len, f_conn in parts:
             # a connection's frames are in order within a call: group them by a stable sort
@@ -679,20 +697,28 @@ class PackedFramer:
         self.session = FramerSession(1)
         self.pending = []      # pushed bytes not yet handed to the session
         self.ready = deque()   # frames popped from the device (then the error that ended them)
+        self.error = None      # the framing error once raised: raised again until reset()
 
     def push(self, data) -> None:
         if len(data):
             self.pending.append(bytes(data))
 
     def buffered_bytes(self) -> int:
+        """Framer.bufferedBytes (framing.zig:30-32): pushed bytes not yet framed. One difference:
+        pop_frame takes every whole message off the device at once, and the packed bytes of the
+        frames it holds for later pop_frame calls are no longer counted (the device does not
+        report each frame's packed length)."""
         return self.session.buffered(0) + sum(len(d) for d in self.pending)
 
     def reset(self) -> None:
         self.session.reset(0)
         self.pending.clear()
         self.ready.clear()
+        self.error = None
 
     def pop_frame(self):
+        if self.error is not None:  # framing.zig: the corrupt bytes keep failing until reset
+            raise self.error
         if not self.ready and self.pending:
             data = b"".join(self.pending)
             self.pending.clear()
@@ -706,6 +732,7 @@ class PackedFramer:
             return None
         v = self.ready.popleft()
         if isinstance(v, Exception):
+            self.error = v
             raise v
         return v
 
@@ -849,6 +876,13 @@ def stream_queue_info(stream=None):
     _raise(lib().capnp_packed_stream_queue_info(_stream(stream), ctypes.byref(b), ctypes.byref(k)),
            "stream_queue_info")
     return b.value, k.value
+
+
+def stream_contexts() -> int:
+    """How many caller streams the library holds a context for (capnp_packed_stream_contexts)."""
+    k = ctypes.c_uint32()
+    _raise(lib().capnp_packed_stream_contexts(ctypes.byref(k)), "stream_contexts")
+    return k.value
 
 
 def _ptr(t) -> int:

@@ -350,7 +350,7 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
 size_t capnp_packed_batch_workspace_bytes(uint32_t n) { return cpk::queue_bytes(n); }
 
 int capnp_packed_set_decoder(int decoder) {
-    if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_STREAM)
+    if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_WORDS)
         return fail(CAPNP_PACKED_INVALID_ARGUMENT, "unknown decoder");
     if (!cpk::decoder_built(decoder))
         return fail(CAPNP_PACKED_INVALID_ARGUMENT, "decoder not in this build (dev builds: CPK_DEV_DECODERS=1)");
@@ -377,6 +377,15 @@ int capnp_packed_stream_queue_info(void* stream, size_t* bytes, uint32_t* kept) 
     int st = ensure_device();
     if (st) return st;
     cpk::stream_queue_info(static_cast<hipStream_t>(stream), bytes, kept);
+    return CAPNP_PACKED_OK;
+}
+
+int capnp_packed_stream_contexts(uint32_t* count) {
+    if (!count) return fail(CAPNP_PACKED_INVALID_ARGUMENT, "null output");
+    *count = 0;
+    int st = ensure_device();
+    if (st) return st;
+    *count = cpk::stream_context_count();
     return CAPNP_PACKED_OK;
 }
 
@@ -738,7 +747,12 @@ struct capnp_packed_framer {
     static constexpr uint32_t kWalkMessages = 64;  // messages a walk pass finds per connection
 
     ~capnp_packed_framer() {
-        if (s) (void)hipStreamSynchronize(s);
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            // the decode passes ran on s: drop the library's context of it (side stream, events,
+            // class queue), or every session ever created would keep one
+            (void)cpk::release_stream(s);
+        }
         if (arena) (void)hipFree(arena);
         if (d_state) (void)hipFree(d_state);
         if (d_stage) (void)hipFree(d_stage);
@@ -792,43 +806,63 @@ struct capnp_packed_framer {
         return CAPNP_PACKED_OK;
     }
     static uint64_t region_for(uint64_t bytes) { return std::max<uint64_t>(65536, (2 * bytes + 255) & ~255ull); }
-    // Every connection's live bytes into a new arena sized for `extra` more bytes of regions.
-    int rearena(const std::vector<uint64_t>& want) {
+    // A read's region layout, built on copies and committed (commit) only once every copy job
+    // of the read is enqueued: a failed allocation or launch leaves the session as it was.
+    struct Layout {
+        std::vector<uint64_t> off, cap, m0, len;
+        uint64_t top = 0, moved = 0;
+        uint8_t* arena = nullptr;  // a new arena (rearena), freed unless committed
+        uint64_t acap = 0;
+        ~Layout() {
+            if (arena) (void)hipFree(arena);
+        }
+    };
+    void commit(Layout& L) {
+        off.swap(L.off);
+        cap.swap(L.cap);
+        m0.swap(L.m0);
+        len.swap(L.len);
+        top = L.top;
+        moved = L.moved;
+        if (L.arena) {
+            if (arena) (void)hipFree(arena);
+            arena = L.arena;
+            acap = L.acap;
+            L.arena = nullptr;
+        }
+    }
+    // Every connection's live bytes into a new arena (L.arena) with a region sized for want[c]
+    // bytes each; the moves run (and complete) now, from the current arena, which stays valid.
+    int rearena(const std::vector<uint64_t>& want, Layout& L) {
         uint64_t total = 0;
         for (uint32_t c = 0; c < n; ++c) total += want[c] ? region_for(want[c]) : 0;
         const uint64_t ncap = std::max<uint64_t>(2 * total, 1u << 20);
         uint8_t* na = nullptr;
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&na), ncap + 64);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(framer arena)");
+        L.arena = na;
+        L.acap = ncap;
         std::vector<uint64_t> jobs;
         uint64_t t = 0;
         for (uint32_t c = 0; c < n; ++c) {
-            const uint64_t live = len[c] - m0[c];
+            const uint64_t live = L.len[c] - L.m0[c];
             if (!want[c]) {
-                off[c] = cap[c] = m0[c] = len[c] = 0;
+                L.off[c] = L.cap[c] = L.m0[c] = L.len[c] = 0;
                 continue;
             }
             const uint64_t rc = region_for(want[c]);
             if (live) {
-                jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(na + t), reinterpret_cast<uint64_t>(arena + off[c] + m0[c]), live});
-                moved += live;
+                jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(na + t), reinterpret_cast<uint64_t>(arena + L.off[c] + L.m0[c]), live});
+                L.moved += live;
             }
-            off[c] = t;
-            cap[c] = rc;
-            m0[c] = 0;
-            len[c] = live;
+            L.off[c] = t;
+            L.cap[c] = rc;
+            L.m0[c] = 0;
+            L.len[c] = live;
             t += rc;
         }
-        int st = run_jobs(jobs);
-        if (st) {
-            (void)hipFree(na);
-            return st;
-        }
-        if (arena) (void)hipFree(arena);
-        arena = na;
-        acap = ncap;
-        top = t;
-        return CAPNP_PACKED_OK;
+        L.top = t;
+        return run_jobs(jobs);
     }
 };
 
@@ -987,7 +1021,6 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
             e = hipMemcpyAsync(f->d_stage, in, in_bytes, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
         }
-        f->uploaded += in_bytes;
         // regions: a connection whose bytes would pass its region's end slides its held bytes to
         // the region's start when they and the new bytes fit there and the slide's source and
         // target do not overlap (held <= m0; a drained connection just restarts there), else it
@@ -996,7 +1029,7 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         auto slides = [&](uint32_t c) {
             const uint64_t held = f->len[c] - f->m0[c];
             return in_len[c] && f->len[c] + in_len[c] > f->cap[c] && held + in_len[c] <= f->cap[c] && held <= f->m0[c];
-        };
+        };  // (on the session's layout, before this read)
         std::vector<uint64_t> want(n, 0);
         uint64_t grow_bytes = 0;
         bool any_grow = false;
@@ -1008,47 +1041,56 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
                 grow_bytes += capnp_packed_framer::region_for(live);
             }
         }
+        capnp_packed_framer::Layout L;  // the session's layout after this read, committed below
+        L.off = f->off;
+        L.cap = f->cap;
+        L.m0 = f->m0;
+        L.len = f->len;
+        L.top = f->top;
+        L.moved = f->moved;
         std::vector<uint64_t>& jobs = f->hjobs;
         jobs.clear();
         uint32_t n_slides = 0;
         if (any_grow && f->top + grow_bytes > f->acap) {
-            if ((st = f->rearena(want))) return st;  // every region sized for its bytes after this read
+            if ((st = f->rearena(want, L))) return st;  // every region sized for its bytes after this read
         } else {
             for (uint32_t c = 0; c < n; ++c) {
                 if (!slides(c)) continue;
-                const uint64_t held = f->len[c] - f->m0[c];
+                const uint64_t held = L.len[c] - L.m0[c];
                 if (held) {
-                    jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + f->off[c]),
-                                             reinterpret_cast<uint64_t>(f->arena + f->off[c] + f->m0[c]), held});
-                    f->moved += held;
+                    jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + L.off[c]),
+                                             reinterpret_cast<uint64_t>(f->arena + L.off[c] + L.m0[c]), held});
+                    L.moved += held;
                     ++n_slides;
                 }
-                f->m0[c] = 0;
-                f->len[c] = held;
+                L.m0[c] = 0;
+                L.len[c] = held;
             }
             for (uint32_t c = 0; any_grow && c < n; ++c) {  // the slid ones fit now
-                if (!in_len[c] || f->len[c] + in_len[c] <= f->cap[c]) continue;
-                const uint64_t live = f->len[c] - f->m0[c];
+                if (!in_len[c] || L.len[c] + in_len[c] <= L.cap[c]) continue;
+                const uint64_t live = L.len[c] - L.m0[c];
                 const uint64_t rc = capnp_packed_framer::region_for(want[c]);
                 if (live) {
-                    jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + f->top),
-                                             reinterpret_cast<uint64_t>(f->arena + f->off[c] + f->m0[c]), live});
-                    f->moved += live;
+                    jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + L.top),
+                                             reinterpret_cast<uint64_t>(f->arena + L.off[c] + L.m0[c]), live});
+                    L.moved += live;
                 }
-                f->off[c] = f->top;
-                f->cap[c] = rc;
-                f->m0[c] = 0;
-                f->len[c] = live;
-                f->top += rc;
+                L.off[c] = L.top;
+                L.cap[c] = rc;
+                L.m0[c] = 0;
+                L.len[c] = live;
+                L.top += rc;
             }
         }
         for (uint32_t c = 0; c < n; ++c) {
             if (!in_len[c]) continue;
-            jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>(f->arena + f->off[c] + f->len[c]),
+            jobs.insert(jobs.end(), {reinterpret_cast<uint64_t>((L.arena ? L.arena : f->arena) + L.off[c] + L.len[c]),
                                      reinterpret_cast<uint64_t>(f->d_stage + in_off[c]), in_len[c]});
-            f->len[c] += in_len[c];
+            L.len[c] += in_len[c];
         }
         if ((st = f->run_jobs(jobs, false, n_slides))) return st;  // ordered before the passes below
+        f->commit(L);  // every copy of this read is enqueued: the regions describe the arena now
+        f->uploaded += in_bytes;
     }
     FR_MARK(prof, "upload");
 

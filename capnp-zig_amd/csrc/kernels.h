@@ -27,6 +27,7 @@ int set_all_or_nothing(int on);
 uint32_t set_launch_flags(uint32_t flags);
 hipError_t release_stream(hipStream_t stream);
 void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept);
+uint32_t stream_context_count();  // caller streams with a library context (current device)
 
 // Reader.readPackedMessage over a batch of reader streams (reader.zig:84-156).
 // One unit (the single-buffer calls): the unit's status must be kStNeedFull (decode_one_status())

@@ -2612,6 +2612,221 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_incl_max(v, 0), kWave - 1);
 }
 
+// ---------------------------------------------------------------------------
+// Single-read decoder (round 5): lane per unit, one output word per step
+// ---------------------------------------------------------------------------
+// unpackPacked (message.zig:88-145) with the size pass's truncation checks (152-191) made on
+// the way. A wave owns 64 units. Their packed bytes stream through the index pass's ring
+// (quad-coalesced 16-B loads issued a round ahead: every packed byte is fetched from HBM
+// once); round k's window holds the unit's bytes [64k - 16, 64k + 64), and its lane emits
+// every output word whose source lies in [64k - 16, 64k + 48), ONE word per step:
+//   r == 0          a record at pos: tag t, then (00) a zero word and a zero run of b1 more,
+//                   (FF) the word at pos+1 and a literal run of c9 more, (mixed) the word
+//                   scattered from the popc(t) bytes after the tag (message.zig:101-141);
+//   r > 0, kind 0   one more zero word of a zero run (no bytes, any round);
+//   r > 0, kind 1   one more literal word, the 8 bytes at pos.
+// The step is the same code for all three (a literal word reads as the payload of an FF tag
+// one byte earlier; a zero word as the payload of tag 00), so no lane branches. Steps run
+// in sub-rounds of kLwS: each lane keeps its words in registers, then writes them and its
+// store address to a staging row, and quad q of the wave stores unit 16m + q's words as one
+// 64-B run per store instruction (16 units per instruction), the way decode_index_kernel
+// stores its records. A record that runs past the input is UNEXPECTED_EOF: the unit's
+// earlier words may already be in its slot (the two-pass decoder writes nothing for a failed
+// unit; capnp_packed_set_all_or_nothing routes mid units to it). Words past out_cap are
+// never stored; the unit reports OUT_OF_SPACE with the size it needs.
+constexpr uint32_t kLwWaves = 2;   // waves per block (a block shares one selector table)
+constexpr uint32_t kLwRing = 80;   // ring bytes per lane, as decode_index_kernel
+constexpr uint32_t kLwS = 8;       // words per sub-round
+constexpr uint32_t kLwStg = 80;    // staging bytes per lane: kLwS words + {address, count}
+
+__global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
+    uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+    const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kLwWaves * kWave * kLwRing];
+    __shared__ __attribute__((aligned(16))) uint8_t stg_blk[kLwWaves * kWave * kLwStg];
+    __shared__ uint64_t lut[256];  // tag -> v_perm selector (00: zero word, FF: the 8 bytes)
+    for (uint32_t i = threadIdx.x; i < 256; i += kLwWaves * kWave) lut[i] = expand_selector(i);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wave = threadIdx.x >> 6;
+    uint8_t* const ring_all = ring_blk + wave * (kWave * kLwRing);
+    uint8_t* const stg_all = stg_blk + wave * (kWave * kLwStg);
+    const uint32_t wv = blockIdx.x * kLwWaves + wave;
+    const uint32_t count = list ? *list_count : n;
+    if (wv * kWave >= count) return;  // wave-uniform
+    const uint32_t slot = wv * kWave + lane;
+    const bool valid = slot < count;
+    const uint32_t unit = valid ? ((list && count != n) ? list[slot] : slot) : 0u;
+
+    // ---- per-lane unit ---------------------------------------------------------------
+    const uint8_t* src = cpk_dummy16;
+    uint64_t P64 = 0, cap = 0;
+    uint8_t* dstb = nullptr;
+    int32_t st = ST_OK;
+    if (valid) {
+        src = in + in_off[unit];
+        P64 = in_len[unit];
+        dstb = out + out_off[unit];
+        cap = out_cap[unit];
+        if (P64 > 0 && (reinterpret_cast<uintptr_t>(dstb) & 7)) st = ST_ARG;  // an empty unit writes nothing
+        if (P64 >= kIxSizeMax) st = kStNeedFull;  // positions are u32 (the long-unit decoders own these)
+    }
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+    const bool take = valid && st == ST_OK && P64 > 0;
+    const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
+    const uint32_t npieces = (end + 15) >> 4;
+    uint32_t maxr = (end + 63) >> 6;  // rounds with data for this lane
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
+    maxr = __builtin_amdgcn_readfirstlane(maxr);
+    const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0xFFFFFFFFu);
+
+    // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block ----------
+    const uint4* qsrc[4];
+    uint32_t qlast[4];
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m) {
+        const uint32_t r = 16 * m + lane / 4;
+        const uint64_t rb = __shfl(reinterpret_cast<uint64_t>(src - s), r, kWave);
+        const uint32_t rn = __shfl(npieces, r, kWave);
+        qsrc[m] = reinterpret_cast<const uint4*>(rn ? reinterpret_cast<const uint8_t*>(rb) : cpk_dummy16);
+        qlast[m] = rn ? rn - 1 : 0u;
+    }
+    const uint32_t qp = lane & 3;
+    u32x4 d0, d1, d2, d3;
+    auto load = [&](uint32_t k) {
+        ds_gload16(d0, qsrc[0] + min(4 * k + qp, qlast[0]));
+        ds_gload16(d1, qsrc[1] + min(4 * k + qp, qlast[1]));
+        ds_gload16(d2, qsrc[2] + min(4 * k + qp, qlast[2]));
+        ds_gload16(d3, qsrc[3] + min(4 * k + qp, qlast[3]));
+    };
+    uint8_t* const wq = ring_all + (lane / 4) * kLwRing + 16 + 16 * qp;
+    uint8_t* const ring = ring_all + lane * kLwRing;
+    uint8_t* const stg = stg_all + lane * kLwStg;
+
+    uint32_t pos = take ? s : kIxDead;  // next source (aligned space)
+    uint32_t zrem = 0, lrem = 0;        // zero / literal words left in the current run
+    uint32_t apos = pos;                // pos, or 0 during a zero run (its words need no bytes)
+    uint32_t W = 0;                     // words emitted
+    uint32_t younger = 0;               // store instructions issued after the ring loads in flight
+    if (maxr > 0) load(0);
+    for (uint32_t k = 0; k <= maxr; ++k) {
+        if (k < maxr) {
+            vmcnt_at_most63(younger);  // round k's loads are in
+            asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+        }
+        younger = 0;
+        if (k > 0) {
+            wave_lds_sync();
+            *reinterpret_cast<uint4*>(ring) = *reinterpret_cast<const uint4*>(ring + 64);
+            wave_lds_sync();
+        }
+        if (k < maxr) {
+            *reinterpret_cast<u32x4*>(wq) = d0;
+            *reinterpret_cast<u32x4*>(wq + 16 * kLwRing) = d1;
+            *reinterpret_cast<u32x4*>(wq + 32 * kLwRing) = d2;
+            *reinterpret_cast<u32x4*>(wq + 48 * kLwRing) = d3;
+            if (k + 1 < maxr) load(k + 1);
+            wave_lds_sync();
+        }
+        const uint32_t base = 64 * k - 16;          // aligned-space position of ring offset 0
+        const uint32_t lim = min(64 * k + 48, end);  // sources of this round: < lim
+        for (;;) {  // sub-rounds
+            // step j leaves the word's 8 payload bytes in pw[j] and its selector's tag in byte
+            // j % 4 of ts[j / 4]; the selectors are looked up and applied when the words are
+            // staged, off the chain pos -> tag -> length -> pos
+            uint64_t pw[kLwS];
+            uint32_t ts[kLwS / 4] = {0u, 0u};
+            uint32_t e = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < kLwS; ++j) {
+                const bool act = apos < lim;
+                if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                if (act) {
+                    // 16 bytes from the dword at or below the source (a zero word reads anywhere)
+                    const uint32_t o = min(pos - base, 64u);
+                    const uint32_t* const rw = reinterpret_cast<const uint32_t*>(ring + (o & ~3u));
+                    const uint32_t D0 = rw[0], D1 = rw[1], D2 = rw[2], D3 = rw[3];
+                    const uint32_t sh = o & 3u;
+                    const uint32_t X0 = __builtin_amdgcn_alignbyte(D1, D0, sh);  // bytes o .. o+3
+                    const uint32_t X1 = __builtin_amdgcn_alignbyte(D2, D1, sh);  // o+4 .. o+7
+                    const uint32_t X2 = __builtin_amdgcn_alignbyte(D3, D2, sh);  // o+8 .. o+11
+                    const bool inrec = (zrem | lrem) == 0u;
+                    const uint32_t lit = min(lrem, 1u), zw = min(zrem, 1u);
+                    const uint32_t t = X0 & 0xFFu, b1 = (X0 >> 8) & 0xFFu, c9 = (X2 >> 8) & 0xFFu;
+                    const uint32_t sh1 = 1u - lit;  // payload: o+1 .. o+8 (record), o .. o+7 (literal)
+                    pw[j] = (uint64_t)__builtin_amdgcn_alignbyte(X1, X0, sh1) |
+                            ((uint64_t)__builtin_amdgcn_alignbyte(X2, X1, sh1) << 32);
+                    const uint32_t tsel = inrec ? t : lit * 0xFFu;  // zero word: tag 00
+                    ts[j / 4] |= tsel << (8 * (j % 4));
+                    const bool tz = t == 0u, tf = t == 0xFFu;
+                    const uint32_t len = (uint32_t)__popc(t) + 1u + (uint32_t)(tz | tf);
+                    const uint32_t need = tf ? len + 8u * c9 : len;
+                    // message.zig:152-191: a record that runs past the input
+                    const bool eof = inrec && pos + need > end;
+                    st = eof ? ST_EOF : st;
+                    pos = eof ? kIxDead : pos + (inrec ? len : 8u * lit);
+                    zrem = (eof || !inrec) ? zrem - zw : (tz ? b1 : 0u);
+                    lrem = (eof || !inrec) ? lrem - lit : (tf ? c9 : 0u);
+                    apos = zrem ? 0u : pos;
+                    e += eof ? 0u : 1u;
+                }
+            }
+            // ---- store the sub-round: lane u's words go out as one run, by its unit's quad ----
+            if (__builtin_amdgcn_ballot_w64(e != 0) != 0) {
+                const uint32_t room = W < capw ? capw - W : 0u;
+                const uint32_t nst = min(e, room);
+                const uint64_t a = reinterpret_cast<uint64_t>(dstb) + 8ull * W;
+                uint64_t w[kLwS];
+#pragma unroll
+                for (uint32_t j = 0; j < kLwS; ++j) w[j] = perm64(pw[j], lut[(ts[j / 4] >> (8 * (j % 4))) & 0xFFu]);
+                wave_lds_sync();  // the previous sub-round's staging reads are done
+                u32x4* const sv = reinterpret_cast<u32x4*>(stg);
+#pragma unroll
+                for (uint32_t j = 0; j < kLwS; j += 2)
+                    sv[j / 2] = u32x4{(uint32_t)w[j], (uint32_t)(w[j] >> 32), (uint32_t)w[j + 1],
+                                      (uint32_t)(w[j + 1] >> 32)};
+                sv[kLwS / 2] = u32x4{(uint32_t)a, (uint32_t)(a >> 32), nst, 0u};
+                wave_lds_sync();
+#pragma unroll
+                for (uint32_t m = 0; m < 4; ++m) {
+                    const uint8_t* const row = stg_all + (16 * m + lane / 4) * kLwStg;
+                    const u32x4 mt = *reinterpret_cast<const u32x4*>(row + 64);
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(row + 16 * qp);
+                    uint8_t* const p = reinterpret_cast<uint8_t*>((uint64_t)mt.x | ((uint64_t)mt.y << 32)) + 16 * qp;
+                    const bool two = 2 * qp + 1 < mt.z, one = 2 * qp + 1 == mt.z;
+                    if (__builtin_amdgcn_ballot_w64(two) != 0) {
+                        ++younger;
+                        if (two) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+                    }
+                    if (__builtin_amdgcn_ballot_w64(one) != 0) {
+                        ++younger;
+                        const uint64_t x = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                        if (one) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(x) : "memory");
+                    }
+                }
+                W += e;
+            }
+            if (__builtin_amdgcn_ballot_w64(apos < lim) == 0) break;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!valid) return;
+    if (st == kStNeedFull) {  // the long-unit decoders' (launch_decode never lists these here)
+        status[unit] = st;
+        return;
+    }
+    if (st != ST_OK) {
+        out_len[unit] = 0;
+        status[unit] = st;
+        return;
+    }
+    out_len[unit] = 8ull * W;
+    status[unit] = 8ull * W > cap ? ST_SPACE : ST_OK;
+}
+
 // The single-read mid-unit decoders (fused, round 3; streaming, round 4) measured slower than
 // the two-pass decoder and live in a dev build only.
 #ifndef CPK_DEV_DECODERS
@@ -5335,6 +5550,15 @@ void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept) {
     *kept = (uint32_t)it->second->retired.size();
 }
 
+uint32_t stream_context_count() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    uint32_t k = 0;
+    for (const auto& kv : g_ctx) k += kv.first.first == dev;
+    return k;
+}
+
 hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                          int32_t* status, bool write, void* ws, size_t ws_bytes, hipStream_t stream) {
@@ -5458,13 +5682,14 @@ static std::atomic<int> g_decoder{CAPNP_PACKED_DECODER_AUTO};
 static std::atomic<int> g_small{1};
 static int small_variant() { return g_small.load(std::memory_order_relaxed); }
 int set_all_or_nothing(int on) { return g_small.exchange(on ? 0 : 1) == 0 ? 1 : 0; }
-[[maybe_unused]] static int decoder_variant() {
+static int decoder_variant() {
     const int v = g_decoder.load(std::memory_order_relaxed);
     return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
 }
 int set_decoder(int v) { return g_decoder.exchange(v); }
 bool decoder_built(int v) {
-    return v == CAPNP_PACKED_DECODER_AUTO || v == CAPNP_PACKED_DECODER_TWO_PASS || CPK_DEV_DECODERS;
+    return v == CAPNP_PACKED_DECODER_AUTO || v == CAPNP_PACKED_DECODER_TWO_PASS || v == CAPNP_PACKED_DECODER_WORDS ||
+           CPK_DEV_DECODERS;
 }
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
@@ -5589,8 +5814,12 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
                                                                      out_len, status, q);
         }
     }
-    // mid units: the indexed two-pass decoder (index pass + fill pass), or in a dev build the
-    // fused single-pass decoder when selected (capnp_packed_set_decoder)
+    // mid units: the indexed two-pass decoder (index pass + fill pass), the single-read words
+    // decoder, or in a dev build the fused single-pass decoder (capnp_packed_set_decoder)
+    if (decoder_variant() == CAPNP_PACKED_DECODER_WORDS && small_variant() != 0) {
+        decode_words_kernel<<<(n + kLwWaves * kWave - 1) / (kLwWaves * kWave), kLwWaves * kWave, 0, ms>>>(
+            in, in_off, in_len, n, out, out_off, out_cap, out_len, status, mid, q + 4);
+    } else
 #if CPK_DEV_DECODERS
     if (dv == CAPNP_PACKED_DECODER_FUSED) {
         static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);

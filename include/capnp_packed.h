@@ -36,7 +36,12 @@
 extern "C" {
 #endif
 
-#define CAPNP_PACKED_ABI_VERSION 1u
+/* ABI version (INTEGRATION.md §5 lists what changed):
+ *   2 (round 5): capnp_packed_framer_* and capnp_packed_set_launch_flags (added in round 4),
+ *     capnp_packed_stream_contexts, CAPNP_PACKED_DECODER_WORDS; CAPNP_PACKED_DECODER_FUSED /
+ *     _STREAM answer INVALID_ARGUMENT outside dev builds, and the CPK_DECODE environment
+ *     variable is gone (capnp_packed_set_decoder is the only selector). */
+#define CAPNP_PACKED_ABI_VERSION 2u
 
 /* Status codes. The first four mirror the reference's error set
  * (message.zig:201 InvalidMessageSize, :105/:115/:121/:127/:137 UnexpectedEof,
@@ -166,6 +171,10 @@ int capnp_packed_stream_release(void* stream);
 /* The queue the library holds for a caller stream: its size in bytes (0: none) and how
  * many replaced queues it keeps because a hipGraph capture used them. */
 int capnp_packed_stream_queue_info(void* stream, size_t* bytes, uint32_t* kept);
+
+/* How many caller streams the library holds a context for (on the current device): a leak
+ * check. A framer session's own stream is released with the session (round 5). */
+int capnp_packed_stream_contexts(uint32_t* count);
 
 /* capnp_packed_encode_batch with a caller-owned device workspace of at least
  * capnp_packed_batch_workspace_bytes(n) bytes (NULL = the library's per-stream
@@ -357,6 +366,9 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
 /* Decoder selection for the batch decode of mid-size units (a tuning knob, not a
  * semantic one: every decoder is bit-exact):
  *   CAPNP_PACKED_DECODER_TWO_PASS  index pass + fill pass (the packed bytes are read twice);
+ *   CAPNP_PACKED_DECODER_WORDS     single read: lane per unit, one output word per step
+ *                                  (round 5; a failed unit may hold a prefix
+ *                                  of its output unless capnp_packed_set_all_or_nothing(1));
  *   CAPNP_PACKED_DECODER_AUTO      the library's default (the two-pass decoder).
  * Dev builds only (built with CPK_DEV_DECODERS=1; the shipped library returns
  * CAPNP_PACKED_INVALID_ARGUMENT for them): the single-read decoders, both measured slower
@@ -369,7 +381,8 @@ enum {
     CAPNP_PACKED_DECODER_AUTO = 0,
     CAPNP_PACKED_DECODER_TWO_PASS = 1,
     CAPNP_PACKED_DECODER_FUSED = 2,
-    CAPNP_PACKED_DECODER_STREAM = 3
+    CAPNP_PACKED_DECODER_STREAM = 3,
+    CAPNP_PACKED_DECODER_WORDS = 4
 };
 int capnp_packed_set_decoder(int decoder);
 

@@ -32,10 +32,11 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
-@pytest.fixture(params=["twopass", "fused", "stream"])
+@pytest.fixture(params=["twopass", "words", "fused", "stream"])
 def decoder(request):
     """Runs a decode test under each mid-unit decoder (capnp_packed_set_decoder): the two-pass
-    decoder (the shipped one), and the fused / streaming single-read decoders, which exist in
+    decoder, the single-read words decoder (round 5), and the fused / streaming
+    single-read decoders, which exist in
     dev builds only (CPK_DEV_DECODERS=1, capnp-zig_amd/lib_exp/dev_decoders.so via CPK_LIB;
     DESIGN.md §2.3a / §2.3b) and are skipped otherwise."""
     import capnp_packed as cp

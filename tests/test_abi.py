@@ -42,7 +42,7 @@ def test_exports_are_c_symbols():
 
 
 def test_version_and_status_names():
-    assert cp.lib().capnp_packed_abi_version() == 1
+    assert cp.lib().capnp_packed_abi_version() == 2
     names = [cp.lib().capnp_packed_status_name(i).decode() for i in range(8)]
     assert names == ["Ok", "InvalidMessageSize", "UnexpectedEof", "Overflow", "OutOfSpace",
                      "InvalidArgument", "DeviceError", "NoDevice"]

@@ -529,3 +529,21 @@ def test_framer_session_steady_stream_reuses_regions():
     total = sum(len(s) for s in streams)
     assert stats["uploaded_bytes"] == total and stats["moved_bytes"] < total // 4, stats
     sess.close()
+
+
+def test_framer_sessions_release_their_stream_context():
+    """a framer session's decode passes run on the session's own stream, so the
+    library keeps a context (side stream, events, class queue) for that stream. Destroying the
+    session must drop it: 24 sessions created, read (each decodes whole messages) and closed
+    leave the library's context count where it was."""
+    rng = np.random.default_rng(0x5E55)
+    msgs, packed = make_stream(rng, 6)
+    stream = b"".join(packed)
+    torch.cuda.synchronize()
+    before = cp.stream_contexts()
+    for _ in range(24):
+        sess = cp.FramerSession(2)
+        fr, st = sess.read({0: stream, 1: stream[:len(stream) // 2]})
+        assert [bytes(x) for x in fr[0]] == msgs
+        sess.close()
+    assert cp.stream_contexts() == before
