@@ -269,7 +269,7 @@ def c1_leg(reps_cpu=300, reps_gpu=100):
 
 
 def copy_ceiling(dev, nbytes, reps=5):
-    """Device-copy ceiling: a torch copy of nbytes (read + write), GB/s."""
+    """Device-copy ceiling: a torch copy of nbytes (read + write), GB/s (the round-1..4 figure)."""
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
     b.copy_(a)
@@ -284,6 +284,48 @@ def copy_ceiling(dev, nbytes, reps=5):
     ms = ev[0].elapsed_time(ev[1]) / reps
     del a, b
     return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
+def ceilings(dev, nbytes, reps=5):
+    """HBM ceilings on this box (verdict r4 item 1a), GB/s, from capnp-zig_amd/lib/libcpk_ceiling.so
+    (csrc/bench_ceiling.hip: 16 B per lane, UNR loads in flight, persistent grids, non-temporal):
+    the best tuned copy, read-only and write-only streams over a small grid x UNR sweep, and a
+    decode-shaped stream (reads 5, writes 8 4-KiB slabs per step: the p = 0.5 decode's P : U).
+    `torch_copy` is the plain torch copy the bench reported until round 4."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(HERE, "capnp-zig_amd", "lib", "libcpk_ceiling.so"))
+    L.cpk_ceiling_stream.restype = ctypes.c_float
+    L.cpk_ceiling_stream.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    L.cpk_ceiling_shaped.restype = ctypes.c_float
+    L.cpk_ceiling_shaped.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    s = torch.cuda.current_stream().cuda_stream
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    out, cfg = {}, {}
+    for kind, name, mult in ((0, "copy", 2), (1, "read", 1), (2, "write", 1)):
+        best = (0.0, None)
+        for grid in (1024, 2048, 4096, 16384):
+            for unr in (2, 4, 8):
+                ms = L.cpk_ceiling_stream(kind, a.data_ptr(), b.data_ptr(), nbytes, grid, unr, s, reps)
+                if ms > 0 and mult * nbytes / (ms * 1e-3) / 1e9 > best[0]:
+                    best = (mult * nbytes / (ms * 1e-3) / 1e9, f"grid {grid} x 256, {unr} x 16 B in flight")
+        out[name], cfg[name] = round(best[0], 1), best[1]
+    nsteps = nbytes // (8 * 4096)
+    best = (0.0, None)
+    for grid in (1024, 2048, 4096, 16384):
+        ms = L.cpk_ceiling_shaped(a.data_ptr(), b.data_ptr(), nsteps, 5, 8, grid, s, reps)
+        if ms > 0 and 13 * 4096 * nsteps / (ms * 1e-3) / 1e9 > best[0]:
+            best = (13 * 4096 * nsteps / (ms * 1e-3) / 1e9, f"grid {grid} x 256")
+    out["decode_shaped"], cfg["decode_shaped"] = round(best[0], 1), best[1]
+    torch.cuda.synchronize()
+    del a, b
+    torch.cuda.empty_cache()
+    out["torch_copy"] = copy_ceiling(dev, nbytes)
+    out["config"] = cfg
+    return out
 
 
 def dense_leg(args, dev, reps=10):
@@ -939,7 +981,7 @@ def main():
                 extra["sweep"][name] = sweep_entry(measure(wl, args, k, 2, world, dev), thr, k)
         del wl
         torch.cuda.empty_cache()
-        extra["roofline_copy_ceiling_GBps"] = copy_ceiling(dev, n * ub)
+        extra["roofline_ceilings_GBps"] = ceilings(dev, n * ub)
         if not args.no_dense:
             torch.cuda.empty_cache()
             extra["dense_stream"] = dense_leg(args, dev)
@@ -997,7 +1039,7 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                          "encode_frac": round(head["encode_frac"], 4), "decode_frac": round(head["decode_frac"], 4),
-                         "copy_ceiling_GBps": extra.pop("roofline_copy_ceiling_GBps", None)},
+                         "ceilings_GBps": extra.pop("roofline_ceilings_GBps", None)},
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
             "encode_GiB_s": round(n * ub / (enc_ms * 1e-3) / 2 ** 30, 2),
@@ -1007,6 +1049,11 @@ def main():
             "bit_exact_roundtrip": bool(ok_t.item()),
         }
         line.update(extra)
+        ceil = line["roofline"].get("ceilings_GBps")
+        if ceil:  # the dominant kernel against what this box's HBM delivers for its traffic shape
+            shaped = ceil.get("decode_shaped") if role == "decode" else ceil.get("copy")
+            if shaped:
+                line["roofline"]["frac_of_box_ceiling"] = round(achieved / shaped, 4)
         if args.same_gpu and world > 1:
             line["same_gpu_rehearsal"] = {"ranks": world, "devices": 1, "collectives": "gloo",
                                           "note": "all ranks share cuda:0: checks the N-rank step, not a scaling number"}

@@ -2617,27 +2617,35 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // ---------------------------------------------------------------------------
 // unpackPacked (message.zig:88-145) with the size pass's truncation checks (152-191) made on
 // the way. A wave owns 64 units. Their packed bytes stream through the index pass's ring
-// (quad-coalesced 16-B loads issued a round ahead: every packed byte is fetched from HBM
-// once); round k's window holds the unit's bytes [64k - 16, 64k + 64), and its lane emits
-// every output word whose source lies in [64k - 16, 64k + 48), ONE word per step:
-//   r == 0          a record at pos: tag t, then (00) a zero word and a zero run of b1 more,
-//                   (FF) the word at pos+1 and a literal run of c9 more, (mixed) the word
-//                   scattered from the popc(t) bytes after the tag (message.zig:101-141);
-//   r > 0, kind 0   one more zero word of a zero run (no bytes, any round);
-//   r > 0, kind 1   one more literal word, the 8 bytes at pos.
-// The step is the same code for all three (a literal word reads as the payload of an FF tag
-// one byte earlier; a zero word as the payload of tag 00), so no lane branches. Steps run
-// in sub-rounds of kLwS: each lane keeps its words in registers, then writes them and its
-// store address to a staging row, and quad q of the wave stores unit 16m + q's words as one
-// 64-B run per store instruction (16 units per instruction), the way decode_index_kernel
-// stores its records. A record that runs past the input is UNEXPECTED_EOF: the unit's
+// (quad-coalesced 16-B loads issued a round ahead: every packed byte is fetched from HBM once);
+// round k's window holds the unit's bytes [64k - 16, 64k + 64), and its lane emits every output
+// word whose source lies in [64k - 16, 64k + 48), ONE word per step:
+//   run == 0        a record at pos, tag t: (00) a zero word, then a zero run of b1 more;
+//                   (FF) the 8 bytes after the tag, then a literal run of c9 more words;
+//                   (other) the popc(t) bytes after the tag scattered by t (message.zig:101-141);
+//   run > 0         one more word of the run: zero (rsel 00, no bytes, any round) or literal
+//                   (rsel FF, the 8 bytes at pos).
+// Steps run in sub-rounds of kLwS, in two phases:
+//   A, the chain: per step three byte reads at pos (tag, +1, +9) give the record's length and
+//      the next pos; the step only records the word's payload offset in the ring and its
+//      selector tag (a literal word: tag FF one byte earlier; a zero word: tag 00), so the
+//      dependency pos -> tag -> length -> pos carries a few instructions and one LDS read;
+//   B, the words: each recorded word's 8 payload bytes and its v_perm selector, independent
+//      of each other, then into the unit's 128-B output line in LDS.
+// A line that fills is flushed whole: eight lanes store it as one 128-B line, eight lines per
+// store instruction (MI355X: whole lines from eight units write at ~4.3 TB/s, 64-B runs at 8-B
+// offsets at ~1.6 TB/s). A sub-round's words past the line's end wait in
+// registers until the flush and then start the next line. The unit's first and last lines are
+// flushed in part (only its own words; a slot need not be line aligned).
+// Errors (message.zig:152-191): a record that runs past the input leaves pos past the end, and
+// a literal run cut short leaves run > 0: the unit is UNEXPECTED_EOF, found at its end, so its
 // earlier words may already be in its slot (the two-pass decoder writes nothing for a failed
-// unit; capnp_packed_set_all_or_nothing routes mid units to it). Words past out_cap are
-// never stored; the unit reports OUT_OF_SPACE with the size it needs.
+// unit; capnp_packed_set_all_or_nothing routes mid units to it). Words past out_cap are never
+// stored; the unit reports OUT_OF_SPACE with the size it needs.
 constexpr uint32_t kLwWaves = 2;   // waves per block (a block shares one selector table)
 constexpr uint32_t kLwRing = 80;   // ring bytes per lane, as decode_index_kernel
-constexpr uint32_t kLwS = 8;       // words per sub-round
-constexpr uint32_t kLwStg = 80;    // staging bytes per lane: kLwS words + {address, count}
+constexpr uint32_t kLwS = 8;       // steps (words) per sub-round
+constexpr uint32_t kLwLine = 16;   // words per output line (128 B)
 
 __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
@@ -2645,14 +2653,16 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
     const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kLwWaves * kWave * kLwRing];
-    __shared__ __attribute__((aligned(16))) uint8_t stg_blk[kLwWaves * kWave * kLwStg];
+    __shared__ __attribute__((aligned(16))) uint64_t line_blk[kLwWaves * kLwLine * kWave];  // [slot][lane]
+    __shared__ __attribute__((aligned(16))) u32x4 ftab_blk[kLwWaves * kWave];                // flush table
     __shared__ uint64_t lut[256];  // tag -> v_perm selector (00: zero word, FF: the 8 bytes)
     for (uint32_t i = threadIdx.x; i < 256; i += kLwWaves * kWave) lut[i] = expand_selector(i);
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wave = threadIdx.x >> 6;
     uint8_t* const ring_all = ring_blk + wave * (kWave * kLwRing);
-    uint8_t* const stg_all = stg_blk + wave * (kWave * kLwStg);
+    uint64_t* const lines = line_blk + wave * (kLwLine * kWave);
+    u32x4* const ftab = ftab_blk + wave * kWave;
     const uint32_t wv = blockIdx.x * kLwWaves + wave;
     const uint32_t count = list ? *list_count : n;
     if (wv * kWave >= count) return;  // wave-uniform
@@ -2681,7 +2691,10 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
     maxr = __builtin_amdgcn_readfirstlane(maxr);
-    const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0xFFFFFFFFu);
+    const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0x7FFFFFFFu);
+    // output lines: word 0 of the unit sits in slot s0 of the 128-B line at line0
+    const uint32_t s0 = take ? (uint32_t)((reinterpret_cast<uintptr_t>(dstb) >> 3) & 15) : 0u;
+    const uint64_t line0 = reinterpret_cast<uint64_t>(dstb) - 8ull * s0;
 
     // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block ----------
     const uint4* qsrc[4];
@@ -2704,13 +2717,51 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     };
     uint8_t* const wq = ring_all + (lane / 4) * kLwRing + 16 + 16 * qp;
     uint8_t* const ring = ring_all + lane * kLwRing;
-    uint8_t* const stg = stg_all + lane * kLwStg;
+
+    // ---- flush: every lane with `want` stores words [lo, hi) of its current line (slot
+    // range) to the line at address A; eight lanes per line, eight lines per instruction ----
+    uint32_t younger = 0;  // store instructions issued after the ring loads in flight
+    auto flush = [&](bool want, uint64_t A, uint32_t lo, uint32_t hi) {
+        const uint64_t F = __builtin_amdgcn_ballot_w64(want);
+        if (F == 0) return;
+        const uint32_t cnt = (uint32_t)__popcll(F);
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u));
+        wave_lds_sync();  // the previous flush's table reads are done
+        if (want) ftab[rk] = u32x4{(uint32_t)A, (uint32_t)(A >> 32), lo | (hi << 8), lane};
+        wave_lds_sync();
+        const uint32_t j = lane & 7;
+        for (uint32_t g = 0; g < cnt; g += 8) {  // wave-uniform
+            const uint32_t rr = g + lane / 8;
+            const u32x4 ent = ftab[min(rr, cnt - 1)];
+            const uint32_t flo = ent.z & 0xFFu, fhi = ent.z >> 8, fu = ent.w;
+            const uint64_t x0 = lines[(2 * j) * kWave + fu], x1 = lines[(2 * j + 1) * kWave + fu];
+            uint8_t* const p = reinterpret_cast<uint8_t*>((uint64_t)ent.x | ((uint64_t)ent.y << 32)) + 16 * j;
+            const bool in_r = rr < cnt;
+            const bool a0 = in_r && 2 * j >= flo && 2 * j < fhi, a1 = in_r && 2 * j + 1 >= flo && 2 * j + 1 < fhi;
+            const bool both = a0 && a1, first = a0 && !a1, second = a1 && !a0;
+            if (__builtin_amdgcn_ballot_w64(both) != 0) {
+                ++younger;
+                const u32x4 v = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
+                if (both) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+            }
+            if (__builtin_amdgcn_ballot_w64(first | second) != 0) {
+                ++younger;
+                uint8_t* const q = second ? p + 8 : p;
+                const uint64_t x = second ? x1 : x0;
+                if (first | second) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(q), "v"(x) : "memory");
+            }
+        }
+    };
+    // the slots of line L a flush may store: the unit's own words (from s0 in line 0) below capw
+    auto line_hi_cap = [&](uint32_t L, uint32_t hi) {
+        const int64_t c = (int64_t)capw + s0 - 16ll * L;  // slots of line L below word capw
+        return (uint32_t)max<int64_t>(0, min<int64_t>(hi, c));
+    };
 
     uint32_t pos = take ? s : kIxDead;  // next source (aligned space)
-    uint32_t zrem = 0, lrem = 0;        // zero / literal words left in the current run
+    uint32_t run = 0, rsel = 0;         // words left in the current run; its selector tag (00 / FF)
     uint32_t apos = pos;                // pos, or 0 during a zero run (its words need no bytes)
     uint32_t W = 0;                     // words emitted
-    uint32_t younger = 0;               // store instructions issued after the ring loads in flight
     if (maxr > 0) load(0);
     for (uint32_t k = 0; k <= maxr; ++k) {
         if (k < maxr) {
@@ -2734,83 +2785,71 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         const uint32_t base = 64 * k - 16;          // aligned-space position of ring offset 0
         const uint32_t lim = min(64 * k + 48, end);  // sources of this round: < lim
         for (;;) {  // sub-rounds
-            // step j leaves the word's 8 payload bytes in pw[j] and its selector's tag in byte
-            // j % 4 of ts[j / 4]; the selectors are looked up and applied when the words are
-            // staged, off the chain pos -> tag -> length -> pos
-            uint64_t pw[kLwS];
-            uint32_t ts[kLwS / 4] = {0u, 0u};
+            // ---- A: the chain. Step j leaves (payload ring offset | selector tag << 8) in
+            // half j % 2 of rec[j / 2] ----
+            uint32_t rec[kLwS / 2];
+#pragma unroll
+            for (uint32_t j = 0; j < kLwS / 2; ++j) rec[j] = 0u;
             uint32_t e = 0;
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) {
                 const bool act = apos < lim;
                 if (__builtin_amdgcn_ballot_w64(act) == 0) break;
                 if (act) {
-                    // 16 bytes from the dword at or below the source (a zero word reads anywhere)
-                    const uint32_t o = min(pos - base, 64u);
-                    const uint32_t* const rw = reinterpret_cast<const uint32_t*>(ring + (o & ~3u));
-                    const uint32_t D0 = rw[0], D1 = rw[1], D2 = rw[2], D3 = rw[3];
-                    const uint32_t sh = o & 3u;
-                    const uint32_t X0 = __builtin_amdgcn_alignbyte(D1, D0, sh);  // bytes o .. o+3
-                    const uint32_t X1 = __builtin_amdgcn_alignbyte(D2, D1, sh);  // o+4 .. o+7
-                    const uint32_t X2 = __builtin_amdgcn_alignbyte(D3, D2, sh);  // o+8 .. o+11
-                    const bool inrec = (zrem | lrem) == 0u;
-                    const uint32_t lit = min(lrem, 1u), zw = min(zrem, 1u);
-                    const uint32_t t = X0 & 0xFFu, b1 = (X0 >> 8) & 0xFFu, c9 = (X2 >> 8) & 0xFFu;
-                    const uint32_t sh1 = 1u - lit;  // payload: o+1 .. o+8 (record), o .. o+7 (literal)
-                    pw[j] = (uint64_t)__builtin_amdgcn_alignbyte(X1, X0, sh1) |
-                            ((uint64_t)__builtin_amdgcn_alignbyte(X2, X1, sh1) << 32);
-                    const uint32_t tsel = inrec ? t : lit * 0xFFu;  // zero word: tag 00
-                    ts[j / 4] |= tsel << (8 * (j % 4));
+                    // ring offset of pos, kept inside the ring (a zero run's pos may have left it)
+                    const uint32_t o = (uint32_t)min(max((int32_t)(pos - base), 0), 64);
+                    const uint8_t* const a = ring + o;
+                    uint32_t t = a[0], b1 = a[1], c9 = a[9];
+                    asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per step
+                    const bool inrec = run == 0u;
                     const bool tz = t == 0u, tf = t == 0xFFu;
                     const uint32_t len = (uint32_t)__popc(t) + 1u + (uint32_t)(tz | tf);
-                    const uint32_t need = tf ? len + 8u * c9 : len;
-                    // message.zig:152-191: a record that runs past the input
-                    const bool eof = inrec && pos + need > end;
-                    st = eof ? ST_EOF : st;
-                    pos = eof ? kIxDead : pos + (inrec ? len : 8u * lit);
-                    zrem = (eof || !inrec) ? zrem - zw : (tz ? b1 : 0u);
-                    lrem = (eof || !inrec) ? lrem - lit : (tf ? c9 : 0u);
-                    apos = zrem ? 0u : pos;
-                    e += eof ? 0u : 1u;
+                    const uint32_t cnt = tz ? b1 : (tf ? c9 : 0u);
+                    const uint32_t tsel = inrec ? t : rsel;
+                    rec[j / 2] |= ((o + (uint32_t)inrec) | (tsel << 8)) << (16 * (j % 2));
+                    pos += inrec ? len : (rsel & 8u);
+                    run = inrec ? cnt : run - 1u;
+                    rsel = inrec ? (tf ? 0xFFu : 0u) : rsel;
+                    apos = (run != 0u && rsel == 0u) ? 0u : pos;
+                    e = j + 1;
                 }
             }
-            // ---- store the sub-round: lane u's words go out as one run, by its unit's quad ----
-            if (__builtin_amdgcn_ballot_w64(e != 0) != 0) {
-                const uint32_t room = W < capw ? capw - W : 0u;
-                const uint32_t nst = min(e, room);
-                const uint64_t a = reinterpret_cast<uint64_t>(dstb) + 8ull * W;
-                uint64_t w[kLwS];
+            // ---- B: the words (selectors looked up and applied off the chain) ----
+            uint64_t w[kLwS];
 #pragma unroll
-                for (uint32_t j = 0; j < kLwS; ++j) w[j] = perm64(pw[j], lut[(ts[j / 4] >> (8 * (j % 4))) & 0xFFu]);
-                wave_lds_sync();  // the previous sub-round's staging reads are done
-                u32x4* const sv = reinterpret_cast<u32x4*>(stg);
-#pragma unroll
-                for (uint32_t j = 0; j < kLwS; j += 2)
-                    sv[j / 2] = u32x4{(uint32_t)w[j], (uint32_t)(w[j] >> 32), (uint32_t)w[j + 1],
-                                      (uint32_t)(w[j + 1] >> 32)};
-                sv[kLwS / 2] = u32x4{(uint32_t)a, (uint32_t)(a >> 32), nst, 0u};
-                wave_lds_sync();
-#pragma unroll
-                for (uint32_t m = 0; m < 4; ++m) {
-                    const uint8_t* const row = stg_all + (16 * m + lane / 4) * kLwStg;
-                    const u32x4 mt = *reinterpret_cast<const u32x4*>(row + 64);
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(row + 16 * qp);
-                    uint8_t* const p = reinterpret_cast<uint8_t*>((uint64_t)mt.x | ((uint64_t)mt.y << 32)) + 16 * qp;
-                    const bool two = 2 * qp + 1 < mt.z, one = 2 * qp + 1 == mt.z;
-                    if (__builtin_amdgcn_ballot_w64(two) != 0) {
-                        ++younger;
-                        if (two) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-                    }
-                    if (__builtin_amdgcn_ballot_w64(one) != 0) {
-                        ++younger;
-                        const uint64_t x = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                        if (one) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(x) : "memory");
-                    }
-                }
-                W += e;
+            for (uint32_t j = 0; j < kLwS; ++j) {
+                const uint32_t r16 = (rec[j / 2] >> (16 * (j % 2))) & 0xFFFFu;
+                const uint32_t o = r16 & 0xFFu, sh = o & 3u;
+                const uint32_t* const rw = reinterpret_cast<const uint32_t*>(ring + (o & ~3u));
+                const uint32_t D0 = rw[0], D1 = rw[1], D2 = rw[2];
+                const uint64_t pay = (uint64_t)__builtin_amdgcn_alignbyte(D1, D0, sh) |
+                                     ((uint64_t)__builtin_amdgcn_alignbyte(D2, D1, sh) << 32);
+                w[j] = perm64(pay, lut[r16 >> 8]);
             }
+            // ---- into the unit's line; a line that fills is flushed, the rest follows ----
+            const uint32_t sl = (s0 + W) & 15u;  // first slot of this sub-round's words
+            const uint32_t f = kLwLine - sl;     // free slots of the current line
+#pragma unroll
+            for (uint32_t j = 0; j < kLwS; ++j)
+                if (j < e && j < f) lines[((sl + j) & 15u) * kWave + lane] = w[j];
+            const bool full = e >= f && e != 0u;
+            if (__builtin_amdgcn_ballot_w64(full) != 0) {
+                const uint32_t L = (s0 + W) >> 4;
+                flush(full, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, 16u));
+                wave_lds_sync();  // the flush's line reads come before the next line's words
+#pragma unroll
+                for (uint32_t j = 0; j < kLwS; ++j)
+                    if (j < e && j >= f) lines[((sl + j) & 15u) * kWave + lane] = w[j];
+            }
+            W += e;
             if (__builtin_amdgcn_ballot_w64(apos < lim) == 0) break;
         }
+    }
+    // the unit's last line, in part (a full last line went out when it filled)
+    {
+        const uint32_t L = (s0 + W) >> 4, hi = (s0 + W) & 15u;
+        const bool part = take && hi != 0u;
+        flush(part, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, hi));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!valid) return;
@@ -2818,6 +2857,8 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         status[unit] = st;
         return;
     }
+    // message.zig:152-191: the walk ends exactly at the input's end with no literal word owed
+    if (take && (pos != end || run != 0u)) st = ST_EOF;
     if (st != ST_OK) {
         out_len[unit] = 0;
         status[unit] = st;
@@ -5817,8 +5858,9 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     // mid units: the indexed two-pass decoder (index pass + fill pass), the single-read words
     // decoder, or in a dev build the fused single-pass decoder (capnp_packed_set_decoder)
     if (decoder_variant() == CAPNP_PACKED_DECODER_WORDS && small_variant() != 0) {
-        decode_words_kernel<<<(n + kLwWaves * kWave - 1) / (kLwWaves * kWave), kLwWaves * kWave, 0, ms>>>(
-            in, in_off, in_len, n, out, out_off, out_cap, out_len, status, mid, q + 4);
+        const uint32_t lw_blocks = (n + kLwWaves * kWave - 1) / (kLwWaves * kWave);
+        decode_words_kernel<<<lw_blocks, kLwWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                   out_len, status, mid, q + 4);
     } else
 #if CPK_DEV_DECODERS
     if (dv == CAPNP_PACKED_DECODER_FUSED) {
