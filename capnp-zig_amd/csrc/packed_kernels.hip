@@ -2643,9 +2643,15 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // unit; capnp_packed_set_all_or_nothing routes mid units to it). Words past out_cap are never
 // stored; the unit reports OUT_OF_SPACE with the size it needs.
 constexpr uint32_t kLwWaves = 2;   // waves per block (a block shares one selector table)
-constexpr uint32_t kLwRing = 80;   // ring bytes per lane, as decode_index_kernel
+constexpr uint32_t kLwCarry = 12;  // ring bytes kept from the previous round's block
+constexpr uint32_t kLwRing = kLwCarry + 64;  // 76 B per lane (an odd dword stride: fewer bank conflicts)
 constexpr uint32_t kLwS = 8;       // steps (words) per sub-round
 constexpr uint32_t kLwLine = 16;   // words per output line (128 B)
+// LDS per 2-wave block: rings 9728 + lines 16384 + flush tables 256 + selector table 128 = 26496 B,
+// so six blocks (12 waves) fit a CU: the CU admits at most ~159.7 KB of them (census,
+// scripts/dev/lds_census.hip: 6 x 26624 B blocks resident, 6 x 27136 B not; 5 x 32768 B neither).
+constexpr uint32_t kLwLds = kLwWaves * kWave * (kLwRing + 128 + 2) + 128;
+static_assert(kLwLds <= 26624, "six blocks per CU");
 
 __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
@@ -2653,16 +2659,27 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
     const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kLwWaves * kWave * kLwRing];
-    __shared__ __attribute__((aligned(16))) uint64_t line_blk[kLwWaves * kLwLine * kWave];  // [slot][lane]
-    __shared__ __attribute__((aligned(16))) u32x4 ftab_blk[kLwWaves * kWave];                // flush table
-    __shared__ uint64_t lut[256];  // tag -> v_perm selector (00: zero word, FF: the 8 bytes)
-    for (uint32_t i = threadIdx.x; i < 256; i += kLwWaves * kWave) lut[i] = expand_selector(i);
+    __shared__ __attribute__((aligned(16))) uint8_t line_blk[kLwWaves * kWave * 128];  // [lane][slot]
+    __shared__ uint16_t ftab_blk[kLwWaves * kWave];  // flush table: lane | lo << 6 | hi << 10, by rank
+    // The v_perm selector of tag t (message.zig:134-141: bit k set -> output byte k takes the next
+    // packed byte) from two reads of a 16-entry table: nibble n -> its 4 selector bytes (bit k set:
+    // packed byte popc(n & (2^k - 1)), else 0x0C = a zero byte) | a mask of its set bytes << 32. The
+    // high nibble's bytes then add popc(low nibble). At most 16 distinct addresses per read: no bank
+    // conflicts (the 256-entry table had 3-4-way conflicts and 2 KB of LDS).
+    __shared__ uint64_t nib[16];
+    if (threadIdx.x < 16) {
+        const uint64_t e = expand_selector(threadIdx.x);
+        uint32_t m = 0;
+        for (uint32_t k = 0; k < 4; ++k) m |= ((threadIdx.x >> k) & 1u) ? 0xFFu << (8 * k) : 0u;
+        nib[threadIdx.x] = (e & 0xFFFFFFFFull) | ((uint64_t)m << 32);
+    }
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wave = threadIdx.x >> 6;
     uint8_t* const ring_all = ring_blk + wave * (kWave * kLwRing);
-    uint64_t* const lines = line_blk + wave * (kLwLine * kWave);
-    u32x4* const ftab = ftab_blk + wave * kWave;
+    uint8_t* const lines = line_blk + wave * (kWave * 128);
+    uint8_t* const myline = lines + lane * 128;
+    uint16_t* const ftab = ftab_blk + wave * kWave;
     const uint32_t wv = blockIdx.x * kLwWaves + wave;
     const uint32_t count = list ? *list_count : n;
     if (wv * kWave >= count) return;  // wave-uniform
@@ -2715,7 +2732,16 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         ds_gload16(d2, qsrc[2] + min(4 * k + qp, qlast[2]));
         ds_gload16(d3, qsrc[3] + min(4 * k + qp, qlast[3]));
     };
-    uint8_t* const wq = ring_all + (lane / 4) * kLwRing + 16 + 16 * qp;
+    // a quad lane's 16 B of unit 16m + l/4's block go to ring offset 12 + 16 qp (4-B aligned only:
+    // dword writes, as an unaligned ds_write_b128 is correct but ~3.4x slower)
+    uint8_t* const wq = ring_all + (lane / 4) * kLwRing + kLwCarry + 16 * qp;
+    auto put16 = [&](uint8_t* p, const u32x4& v) {
+        uint32_t* const d = reinterpret_cast<uint32_t*>(p);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+    };
     uint8_t* const ring = ring_all + lane * kLwRing;
 
     // ---- flush: every lane with `want` stores words [lo, hi) of its current line (slot
@@ -2727,29 +2753,40 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         const uint32_t cnt = (uint32_t)__popcll(F);
         const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u));
         wave_lds_sync();  // the previous flush's table reads are done
-        if (want) ftab[rk] = u32x4{(uint32_t)A, (uint32_t)(A >> 32), lo | (hi << 8), lane};
+        if (want) ftab[rk] = (uint16_t)(lane | (lo << 6) | (hi << 10));
         wave_lds_sync();
+        const uint32_t Alo = (uint32_t)A, Ahi = (uint32_t)(A >> 32);
         const uint32_t j = lane & 7;
-        for (uint32_t g = 0; g < cnt; g += 8) {  // wave-uniform
-            const uint32_t rr = g + lane / 8;
-            const u32x4 ent = ftab[min(rr, cnt - 1)];
-            const uint32_t flo = ent.z & 0xFFu, fhi = ent.z >> 8, fu = ent.w;
-            const uint64_t x0 = lines[(2 * j) * kWave + fu], x1 = lines[(2 * j + 1) * kWave + fu];
-            uint8_t* const p = reinterpret_cast<uint8_t*>((uint64_t)ent.x | ((uint64_t)ent.y << 32)) + 16 * j;
-            const bool in_r = rr < cnt;
+        // one pass stores two groups of eight lines; both groups' table, address and line reads
+        // go out before either group's stores (the stores carry no memory clobber)
+        auto store16 = [&](uint32_t ent, uint64_t a, const u32x4& v, bool in_r) {
+            const uint32_t flo = (ent >> 6) & 15u, fhi = ent >> 10;
+            uint8_t* const p = reinterpret_cast<uint8_t*>(a) + 16 * j;
             const bool a0 = in_r && 2 * j >= flo && 2 * j < fhi, a1 = in_r && 2 * j + 1 >= flo && 2 * j + 1 < fhi;
             const bool both = a0 && a1, first = a0 && !a1, second = a1 && !a0;
             if (__builtin_amdgcn_ballot_w64(both) != 0) {
                 ++younger;
-                const u32x4 v = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
-                if (both) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+                if (both) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v));
             }
             if (__builtin_amdgcn_ballot_w64(first | second) != 0) {
                 ++younger;
                 uint8_t* const q = second ? p + 8 : p;
-                const uint64_t x = second ? x1 : x0;
-                if (first | second) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(q), "v"(x) : "memory");
+                const uint64_t x = second ? ((uint64_t)v.z | ((uint64_t)v.w << 32)) : ((uint64_t)v.x | ((uint64_t)v.y << 32));
+                if (first | second) asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(q), "v"(x));
             }
+        };
+        for (uint32_t g = 0; g < cnt; g += 16) {  // wave-uniform
+            const uint32_t ra = g + lane / 8, rb = ra + 8;
+            const uint32_t ea = ftab[min(ra, cnt - 1)], eb = ftab[min(rb, cnt - 1)];
+            const uint32_t ua = ea & 63u, ub = eb & 63u;
+            const uint64_t aa = (uint64_t)(uint32_t)__shfl((int)Alo, (int)ua, kWave) |
+                                ((uint64_t)(uint32_t)__shfl((int)Ahi, (int)ua, kWave) << 32);
+            const uint64_t ab = (uint64_t)(uint32_t)__shfl((int)Alo, (int)ub, kWave) |
+                                ((uint64_t)(uint32_t)__shfl((int)Ahi, (int)ub, kWave) << 32);
+            const u32x4 va = *reinterpret_cast<const u32x4*>(lines + ua * 128 + 16 * j);
+            const u32x4 vb = *reinterpret_cast<const u32x4*>(lines + ub * 128 + 16 * j);
+            store16(ea, aa, va, ra < cnt);
+            if (g + 8 < cnt) store16(eb, ab, vb, rb < cnt);
         }
     };
     // the slots of line L a flush may store: the unit's own words (from s0 in line 0) below capw
@@ -2758,46 +2795,67 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         return (uint32_t)max<int64_t>(0, min<int64_t>(hi, c));
     };
 
-    uint32_t pos = take ? s : kIxDead;  // next source (aligned space)
-    uint32_t run = 0, rsel = 0;         // words left in the current run; its selector tag (00 / FF)
-    uint32_t apos = pos;                // pos, or 0 during a zero run (its words need no bytes)
-    uint32_t W = 0;                     // words emitted
+    // Round k's ring holds aligned-space positions [64k - 12, 64k + 64): the 12 carried bytes, then
+    // block k at offset 12. A source needs at most its 10 bytes (tag, count/payload), so round k walks
+    // the sources below position 64k + 52 (ring offset 64). Positions are kept as ring offsets: the
+    // next source's (po) and the unit end's (end_o), both moved back by 64 at every new round.
+    constexpr int32_t kFar = 0x3FFFFFFF;                   // a lane with nothing to walk
+    int32_t po = take ? (int32_t)(s + kLwCarry) : kFar;    // round 0: ring offset 0 is position -12
+    int32_t end_o = take ? (int32_t)(end + kLwCarry) : 0;
+    uint32_t run = 0, rsel = 0;  // words left in the current run; its selector tag (00 / FF)
+    int32_t apos = po;           // po, or INT_MIN during a zero run (its words need no bytes)
+    uint32_t W = 0;              // words emitted
+#ifdef CPK_FILL_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    FL_T(tk0);
+#endif
     if (maxr > 0) load(0);
     for (uint32_t k = 0; k <= maxr; ++k) {
+        FL_T(ta);
         if (k < maxr) {
             vmcnt_at_most63(younger);  // round k's loads are in
             asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
         }
+        FL_T(tb);
+        FL_ACC(0, tb - ta);
         younger = 0;
         if (k > 0) {
             wave_lds_sync();
-            *reinterpret_cast<uint4*>(ring) = *reinterpret_cast<const uint4*>(ring + 64);
+            uint32_t* const rd = reinterpret_cast<uint32_t*>(ring);
+            const uint32_t c0 = rd[16], c1 = rd[17], c2 = rd[18];  // ring[64, 76) -> ring[0, 12)
+            rd[0] = c0;
+            rd[1] = c1;
+            rd[2] = c2;
             wave_lds_sync();
+            po -= 64;
+            end_o -= 64;
+            apos = apos == INT32_MIN ? apos : po;
         }
         if (k < maxr) {
-            *reinterpret_cast<u32x4*>(wq) = d0;
-            *reinterpret_cast<u32x4*>(wq + 16 * kLwRing) = d1;
-            *reinterpret_cast<u32x4*>(wq + 32 * kLwRing) = d2;
-            *reinterpret_cast<u32x4*>(wq + 48 * kLwRing) = d3;
+            put16(wq, d0);
+            put16(wq + 16 * kLwRing, d1);
+            put16(wq + 32 * kLwRing, d2);
+            put16(wq + 48 * kLwRing, d3);
             if (k + 1 < maxr) load(k + 1);
             wave_lds_sync();
         }
-        const uint32_t base = 64 * k - 16;          // aligned-space position of ring offset 0
-        const uint32_t lim = min(64 * k + 48, end);  // sources of this round: < lim
+        const int32_t lim = min(64, end_o);  // sources of this round: ring offsets < lim
+        FL_T(tc);
+        FL_ACC(1, tc - tb);
         for (;;) {  // sub-rounds
-            // ---- A: the chain. Step j leaves (payload ring offset | selector tag << 8) in
-            // half j % 2 of rec[j / 2] ----
-            uint32_t rec[kLwS / 2];
+            FL_T(td);
+            // ---- A: the chain. Step j leaves (payload ring offset | selector tag << 8) in rec[j] ----
+            uint32_t rec[kLwS];
 #pragma unroll
-            for (uint32_t j = 0; j < kLwS / 2; ++j) rec[j] = 0u;
+            for (uint32_t j = 0; j < kLwS; ++j) rec[j] = 0u;  // steps not taken: ring offset 0, tag 00
             uint32_t e = 0;
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) {
                 const bool act = apos < lim;
                 if (__builtin_amdgcn_ballot_w64(act) == 0) break;
                 if (act) {
-                    // ring offset of pos, kept inside the ring (a zero run's pos may have left it)
-                    const uint32_t o = (uint32_t)min(max((int32_t)(pos - base), 0), 64);
+                    // the source's ring offset, kept inside the ring (a zero run's may have left it)
+                    const uint32_t o = (uint32_t)min(max(po, 0), 64);
                     const uint8_t* const a = ring + o;
                     uint32_t t = a[0], b1 = a[1], c9 = a[9];
                     asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per step
@@ -2806,42 +2864,53 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                     const uint32_t len = (uint32_t)__popc(t) + 1u + (uint32_t)(tz | tf);
                     const uint32_t cnt = tz ? b1 : (tf ? c9 : 0u);
                     const uint32_t tsel = inrec ? t : rsel;
-                    rec[j / 2] |= ((o + (uint32_t)inrec) | (tsel << 8)) << (16 * (j % 2));
-                    pos += inrec ? len : (rsel & 8u);
+                    rec[j] = (o + (uint32_t)inrec) | (tsel << 8);
+                    po += (int32_t)(inrec ? len : (rsel & 8u));
                     run = inrec ? cnt : run - 1u;
                     rsel = inrec ? (tf ? 0xFFu : 0u) : rsel;
-                    apos = (run != 0u && rsel == 0u) ? 0u : pos;
+                    apos = (run != 0u && rsel == 0u) ? INT32_MIN : po;
                     e = j + 1;
                 }
+                FL_ACC(5, 1);
             }
+            FL_T(te);
+            FL_ACC(2, te - td);
+            FL_ACC(6, 1);
             // ---- B: the words (selectors looked up and applied off the chain) ----
             uint64_t w[kLwS];
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) {
-                const uint32_t r16 = (rec[j / 2] >> (16 * (j % 2))) & 0xFFFFu;
+                const uint32_t r16 = rec[j];
                 const uint32_t o = r16 & 0xFFu, sh = o & 3u;
                 const uint32_t* const rw = reinterpret_cast<const uint32_t*>(ring + (o & ~3u));
                 const uint32_t D0 = rw[0], D1 = rw[1], D2 = rw[2];
                 const uint64_t pay = (uint64_t)__builtin_amdgcn_alignbyte(D1, D0, sh) |
                                      ((uint64_t)__builtin_amdgcn_alignbyte(D2, D1, sh) << 32);
-                w[j] = perm64(pay, lut[r16 >> 8]);
+                const uint32_t tg = r16 >> 8;
+                const uint64_t elo = nib[tg & 15u], ehi = nib[tg >> 4];
+                const uint32_t shi = (uint32_t)ehi + (((uint32_t)__popc(tg & 15u) * 0x01010101u) & (uint32_t)(ehi >> 32));
+                w[j] = perm64(pay, (uint64_t)(uint32_t)elo | ((uint64_t)shi << 32));
             }
             // ---- into the unit's line; a line that fills is flushed, the rest follows ----
             const uint32_t sl = (s0 + W) & 15u;  // first slot of this sub-round's words
             const uint32_t f = kLwLine - sl;     // free slots of the current line
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j)
-                if (j < e && j < f) lines[((sl + j) & 15u) * kWave + lane] = w[j];
+                if (j < e && j < f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & 15u)) = w[j];
             const bool full = e >= f && e != 0u;
+            FL_T(tf0);
+            FL_ACC(3, tf0 - te);
             if (__builtin_amdgcn_ballot_w64(full) != 0) {
                 const uint32_t L = (s0 + W) >> 4;
                 flush(full, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, 16u));
                 wave_lds_sync();  // the flush's line reads come before the next line's words
 #pragma unroll
                 for (uint32_t j = 0; j < kLwS; ++j)
-                    if (j < e && j >= f) lines[((sl + j) & 15u) * kWave + lane] = w[j];
+                    if (j < e && j >= f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & 15u)) = w[j];
             }
             W += e;
+            FL_T(tf1);
+            FL_ACC(4, tf1 - tf0);
             if (__builtin_amdgcn_ballot_w64(apos < lim) == 0) break;
         }
     }
@@ -2852,13 +2921,19 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         flush(part, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, hi));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef CPK_FILL_PROF
+    FL_T(tk1);
+    FL_ACC(7, tk1 - tk0);
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
+#endif
     if (!valid) return;
     if (st == kStNeedFull) {  // the long-unit decoders' (launch_decode never lists these here)
         status[unit] = st;
         return;
     }
     // message.zig:152-191: the walk ends exactly at the input's end with no literal word owed
-    if (take && (pos != end || run != 0u)) st = ST_EOF;
+    if (take && (po != end_o || run != 0u)) st = ST_EOF;
     if (st != ST_OK) {
         out_len[unit] = 0;
         status[unit] = st;

@@ -2,8 +2,8 @@
 the oracle (message.zig:88-191 restated in oracle/packed_oracle.c).
 
 Per unit (one lane): aligned-space positions pos in [s, s + P), rounds k = 0 .. maxr with the ring
-window [64k - 16, 64k + 64) (bytes outside the unit read as whatever the clamped loads left:
-modelled as random garbage), sources of round k below lim = min(64k + 48, end), one word per step:
+window [64k - 12, 64k + 64) (bytes outside the unit read as whatever the clamped loads left:
+modelled as random garbage), sources of round k below lim = min(64k + 52, end), one word per step:
 record (r == 0), zero word (zrem > 0), literal word (lrem > 0). Checks the words, the EOF status
 and out_len on random units of every density, truncations and the adversarial corpus.
 Usage: python3 scripts/dev/sim_words.py [n]
@@ -37,11 +37,12 @@ def sim_unit(p: bytes, s: int, rng):
     pos, run, rsel, apos = (s if P else DEAD), 0, 0, (s if P else DEAD)
     words = []
     for k in range(maxr + 1):
-        base = 64 * k - 16
-        lim = min(64 * k + 48, end)
+        base = 64 * k - 12
+        lim = min(64 * k + 52, end)
         while apos < lim:
             o = min(max(pos - base, 0), 64)
             q = base + o  # the ring's byte o
+            assert 0 <= o <= 64 and (o & ~3) + 12 <= 76  # every read inside the 76-B ring
             t, b1, c9 = byte_at(q), byte_at(q + 1), byte_at(q + 9)
             inrec = run == 0
             tz, tf = t == 0, t == 0xFF

@@ -44,7 +44,7 @@ for thr in [int(x) for x in (sys.argv[1:] or ["128", "26", "230"])]:
         torch.cuda.synchronize()
         f(buf)
     waves = reps * n // 64
-    names = ["wait_loads", "ring", "steps", "stores", "total", "steps_n", "subrounds_n", "stores_perm_part"]
+    names = ["wait_loads", "ring", "chain", "words", "flush", "steps_n", "subrounds_n", "total"]
     out = {nm: round(buf[i] / waves, 1) for i, nm in enumerate(names)}
     print(json.dumps({"thr": thr, "ms": round(ev0.elapsed_time(ev1) / reps, 4), "per_wave": out,
                       "roundtrip": bool(torch.equal(d_out, d_in))}), flush=True)
