@@ -802,9 +802,9 @@ class PackedConnections:
 # ---------------------------------------------------------------------------
 
 def set_decoder(name: str) -> str:
-    """Select the mid-unit batch decoder ("auto", "twopass"; "fused" and "stream" in dev builds,
-    decoder_available) for batches enqueued from now on; returns the previous setting's name.
-    Every one is bit-exact."""
+    """Select the mid-unit batch decoder ("auto", "twopass", "words"; "fused" and "stream" were
+    removed in round 5 and raise) for batches enqueued from now on; returns the previous
+    setting's name. Every one is bit-exact."""
     prev = lib().capnp_packed_set_decoder(DECODERS[name])
     if prev < 0 or prev not in DECODERS.values():
         _raise(prev, "set_decoder")
@@ -812,8 +812,8 @@ def set_decoder(name: str) -> str:
 
 
 def decoder_available(name: str) -> bool:
-    """Whether this build has the decoder: "auto" and "twopass" always; "fused" and "stream"
-    in dev builds only (CPK_DEV_DECODERS=1)."""
+    """Whether this build has the decoder: "auto", "twopass" and "words"; not "fused" and
+    "stream" (removed in round 5)."""
     L = lib()
     prev = L.capnp_packed_set_decoder(DECODERS[name])
     if prev not in DECODERS.values():
@@ -850,7 +850,7 @@ class launch_flags:
 
 
 class decoder:
-    """Context manager: `with decoder("fused"): ...` restores the previous decoder after."""
+    """Context manager: `with decoder("words"): ...` restores the previous decoder after."""
 
     def __init__(self, name: str):
         self.name, self.prev = name, None

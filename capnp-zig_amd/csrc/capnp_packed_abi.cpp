@@ -9,7 +9,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -353,7 +352,7 @@ int capnp_packed_set_decoder(int decoder) {
     if (decoder < CAPNP_PACKED_DECODER_AUTO || decoder > CAPNP_PACKED_DECODER_WORDS)
         return fail(CAPNP_PACKED_INVALID_ARGUMENT, "unknown decoder");
     if (!cpk::decoder_built(decoder))
-        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "decoder not in this build (dev builds: CPK_DEV_DECODERS=1)");
+        return fail(CAPNP_PACKED_INVALID_ARGUMENT, "decoder removed from the library (round 5; DESIGN.md §2.3a, §2.3b)");
     return cpk::set_decoder(decoder);
 }
 
@@ -943,24 +942,6 @@ int capnp_packed_framer_stats(capnp_packed_framer* f, uint64_t* uploaded, uint64
 
 namespace {
 
-#if CPK_FRAMER_PROF  // dev builds: wall-time marks of a framer read on stderr
-struct FrProf {
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
-    std::string line;
-    void mark(const char* what) {
-        const auto t = std::chrono::steady_clock::now();
-        char b[64];
-        std::snprintf(b, sizeof b, " %s %.2f", what, std::chrono::duration<double, std::milli>(t - last).count());
-        line += b;
-        last = t;
-    }
-    ~FrProf() { std::fprintf(stderr, "[framer_read]%s\n", line.c_str()); }
-};
-#define FR_MARK(p, w) (p).mark(w)
-#else
-struct FrProf {};
-#define FR_MARK(p, w) ((void)(p))
-#endif
 
 // The gather of capnp_packed_framer_readv: bytes [r0, r1) of the connections' reads, laid end
 // to end at their prefix offsets, into the session's page-locked staging, by byte range over up
@@ -1008,7 +989,6 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
                        uint32_t* n_frames, bool staged = false) {
     const uint32_t n = f->n;
     const hipStream_t s = f->s;
-    FrProf prof;
     hipError_t e = hipSuccess;
     int st = CAPNP_PACKED_OK;
     for (uint32_t c = 0; c < n; ++c) status[c] = CAPNP_PACKED_END_OF_STREAM;
@@ -1092,7 +1072,6 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         f->commit(L);  // every copy of this read is enqueued: the regions describe the arena now
         f->uploaded += in_bytes;
     }
-    FR_MARK(prof, "upload");
 
     // ---- 2. passes: a walk over every connection's held messages, then one decode of them ----
     // state scratch: base, avail, need, X, W (u64 x n), status (i32 x n), then the copy jobs
@@ -1200,7 +1179,6 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         if (e == hipSuccess) e = hipMemcpyAsync(f->pin_tab.p, r_cnt, 4ull * (k + tab_words), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "framer walk pass");
-        FR_MARK(prof, "walk");
         f->jobs_inflight = false;
         // whole messages, in order per connection, while the frames buffer and table hold them:
         // decoded from the arena into frame slots, then to the caller's buffer
@@ -1254,7 +1232,6 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
             if (e == hipSuccess) e = hipMemcpyAsync(hm + 4ull * U, u + 4ull * U, 2ull * U * 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) return hip_fail(e, "framer decode pass");
-            FR_MARK(prof, "decode");
             const int32_t* const us = reinterpret_cast<const int32_t*>(hm + 5ull * U);
             for (uint32_t q = 0; q < U; ++q) {
                 if (us[q] != CAPNP_PACKED_OK || hm[4ull * U + q] != hm[3ull * U + q])  // the walk verified the bytes
@@ -1276,7 +1253,6 @@ int framer_read_locked(capnp_packed_framer* f, const uint8_t* in, uint64_t in_by
         }
     }
     *n_frames = nf;
-    FR_MARK(prof, "host");
     if ((st = f->settle())) return st;  // no pass ran after the upload: the caller's bytes are consumed
     return full ? fail(CAPNP_PACKED_OUT_OF_SPACE, "frames buffer or frame table full: call again to pop the rest")
                 : CAPNP_PACKED_OK;
@@ -1335,9 +1311,6 @@ int capnp_packed_framer_readv(capnp_packed_framer* f, const uint8_t* const* in_p
         // gather and upload in 32-MiB pieces: piece i's H2D runs while piece i + 1 is gathered
         if ((st = f->settle())) return st;  // the previous read's copies are done with d_stage
         if ((st = capnp_packed_framer::grow(&f->d_stage, &f->stage_cap, total + 32))) return st;
-#if CPK_FRAMER_PROF  // dev builds: the gather's wall time per call on stderr
-        const auto g0 = std::chrono::steady_clock::now();
-#endif
         constexpr uint64_t kPiece = 32ull << 20;
         for (uint64_t r0 = 0; r0 < total; r0 += kPiece) {
             const uint64_t r1 = std::min(total, r0 + kPiece);
@@ -1345,11 +1318,6 @@ int capnp_packed_framer_readv(capnp_packed_framer* f, const uint8_t* const* in_p
             const hipError_t e = hipMemcpyAsync(f->d_stage + r0, f->h_stage + r0, r1 - r0, hipMemcpyHostToDevice, f->s);
             if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(framer H2D)");
         }
-#if CPK_FRAMER_PROF
-        std::fprintf(stderr, "[framer_readv] gather + upload enqueue %.3f ms for %llu bytes\n",
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count(),
-                     (unsigned long long)total);
-#endif
     }
     return framer_read_locked(f, total ? f->h_stage : nullptr, total, total ? off.data() : nullptr,
                               total ? in_len : nullptr, frames, frames_cap, frame_off, frame_len, frame_conn,

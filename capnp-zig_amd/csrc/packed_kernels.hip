@@ -9,7 +9,7 @@
 // class_scatter): small units (lane per unit), mid units (wave per unit)
 // and long units (> one 512-word tile / > 5 KiB packed), which run on a side stream of
 // the caller's stream, beside the main grid.
-//   encode  small: encode_small_kernel, lane per unit. Mid: one 64-lane wave per unit of
+//   encode  small: encode_stream_kernel, lane per unit. Mid: one 64-lane wave per unit of
 //           <= 512 words (encode_kernel): the unit is staged in the wave's LDS slice
 //           with coalesced 16-B loads; lane j owns words [8j, 8j+8); zero-byte tags come
 //           from SWAR + a multiply gather; greedy 256-capped zero / literal runs are
@@ -20,13 +20,15 @@
 //           carries it reads back from the input, sizes then writes); units the tile
 //           table cannot hold go to encode_tiled_kernel (tile by tile, one wave).
 //   decode  the record chain (tag -> record length -> next tag) is serial. Small:
-//           decode_small_kernel, lane per unit. Mid: pass 1 (decode_index_kernel) walks
-//           every unit's chain once, lane per unit, with quad-coalesced loads into an LDS
-//           ring, and leaves one u16 record per 16-B piece; pass 2 (decode_fill_kernel,
-//           wave per unit) starts every lane at its own pieces' first tag, lists the
-//           source of each output word (runs' later words filled by a wave scan) and
-//           expands with coalesced stores. Opt-in alternative for mid units: the fused
-//           single-pass decoder (decode_fused_kernel). Long: window-parallel
+//           decode_small_kernel, lane per unit. Mid, in large batches: the words decoder
+//           (decode_words_kernel): lane per unit, quad-coalesced loads into an
+//           LDS ring, one output word per step, staged in 128-B LDS lines and stored by
+//           eight lanes per line. Otherwise two passes: pass 1 (decode_index_kernel) walks
+//           every unit's chain once, lane per unit, with the same ring loads, and leaves
+//           one u16 record per 16-B piece; pass 2 (decode_fill_kernel, wave per unit)
+//           starts every lane at its own pieces' first tag, lists the source of each
+//           output word (runs' later words filled by a wave scan) and expands with
+//           coalesced stores. Long: window-parallel
 //           (long_windows / window_spec / window_resolve / window_fill: 4608-B windows
 //           speculated from every entry state, resolved in order per unit, expanded in
 //           parallel); units the window table cannot hold go to decode_wave_kernel
@@ -110,7 +112,7 @@ __device__ __forceinline__ uint4 load_nt(const void* p) {
     return make_uint4(t.x, t.y, t.z, t.w);
 }
 
-// Ring loads (and the dev-build streaming decoder's output stores) of the lane-per-unit
+// Ring loads of the lane-per-unit
 // decoders in inline asm, so hipcc neither turns them into FLAT instructions
 // (pointers that went through __shfl / LDS lose their address space, and FLAT counts on
 // lgkmcnt too: every LDS wait of the walk would wait for the prefetch) nor waits for them
@@ -119,9 +121,6 @@ __device__ __forceinline__ uint4 load_nt(const void* p) {
 // the wait (cdna_hip_programming.md §5.7 item 1, form ii).
 __device__ __forceinline__ void ds_gload16(u32x4& d, const void* p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-__device__ __forceinline__ void ds_gload16_nt(u32x4& d, const void* p) {
-    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(d) : "v"(p) : "memory");
 }
 
 // Order LDS traffic between lanes of ONE wave (the wave owns its LDS slice).
@@ -133,16 +132,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-#ifdef CPK_EM_PROF
-// Diagnostic build: cycles per phase of the one-tile encoders (s_memtime), summed over waves:
-// [0..3] encode_unit (prologue, stage, tile, total), [4..7] encode_message_one (same).
-__device__ unsigned long long cpk_em_prof[8];
-#define EM_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define EM_ADD(i, d) do { if (lane == 0) atomicAdd(&cpk_em_prof[i], (unsigned long long)(d)); } while (0)
-#else
-#define EM_T(v) do { } while (0)
-#define EM_ADD(i, d) do { } while (0)
-#endif
 
 // Wave scans on DPP: row_shr:1/2/4/8 inside each 16-lane row, then row_bcast:15 and
 // row_bcast:31 across rows (gfx9). A lane a step does not reach keeps `ident`. No LDS
@@ -707,7 +696,6 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
                                                       uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                       uint32_t unit, uint8_t* lds, const uint64_t* lut,
                                                       uint32_t lane) {
-    EM_T(e0);
     const uint64_t b0 = in_off[unit];
     const uint64_t nbytes = in_len[unit];
     uint64_t ob = 0, cap = 0;
@@ -739,17 +727,10 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
     const uint32_t words = (uint32_t)(nbytes >> 3);
     if (words <= kEncMaxWords) {  // one tile (the headline 4-KiB units)
         wave_lds_sync();          // the previous unit's write-back read the slice
-        EM_T(e1);
         encode_stage(lds, src, words, lane);
         wave_lds_sync();
-        EM_T(e2);
         uint32_t cz = 0, cf = 0;
         const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
-        EM_T(e3);
-        EM_ADD(0, e1 - e0);
-        EM_ADD(1, e2 - e1);
-        EM_ADD(2, e3 - e2);
-        EM_ADD(3, e3 - e0);
         if (lane == 0) {
             out_len[unit] = P;
             status[unit] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
@@ -1134,7 +1115,6 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
                                                           uint64_t ob, uint64_t cap, uint8_t* __restrict__ out,
                                                           uint64_t* __restrict__ out_len,
                                                           int32_t* __restrict__ status) {
-    EM_T(e0);
     const uint32_t count = c_in == 0 ? 1u : c_in;  // toBytes 2128-2130: at least one (empty) segment
     // segments are whole words at 8-B aligned addresses (a MessageBuilder's always are); any
     // segment of more than a tile sends the message to the tiled pass before the u32 sum
@@ -1160,17 +1140,10 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
     if (lane == 63) *reinterpret_cast<uint32_t*>(msg_pad(lds, count)) = payload;  // woff[count]
     wave_lds_sync();
     const MsgView<1> m{reinterpret_cast<const uint32_t*>(lds), nullptr, count, hw};
-    EM_T(e1);
     msg_stage_pairs_map(m, words, lane, lds, incl - wl, lane < count && wl != 0);
     wave_lds_sync();
-    EM_T(e2);
     uint32_t cz = 0, cf = 0;
     const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
-    EM_T(e3);
-    EM_ADD(4, e1 - e0);
-    EM_ADD(5, e2 - e1);
-    EM_ADD(6, e3 - e2);
-    EM_ADD(7, e3 - e0);
     if (lane == 0) {
         out_len[msg] = P;
         status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
@@ -2013,21 +1986,13 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 // A unit's status on entry says which pass owns it, so no pass redoes another's work.
 constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2, kRdOne = 3;
 
-#ifndef CPK_IX_BW  // waves per block of the index pass (dev A/B; each wave owns 64 units)
-#define CPK_IX_BW 1
-#endif
-constexpr uint32_t kIxBw = CPK_IX_BW;
+constexpr uint32_t kIxBw = 1;  // waves per block of the index pass (each wave owns 64 units)
 // blocks of the index pass for a batch of n units
 __host__ __device__ constexpr uint32_t ix_blocks_for(uint32_t n) {
     return (uint32_t)((((uint64_t)n + kWave - 1) / kWave + kIxBw - 1) / kIxBw);
 }
-#ifdef CPK_IX_WAVES  // dev A/B: pin the index pass's occupancy (waves per SIMD)
-#define CPK_IX_ATTR __attribute__((amdgpu_waves_per_eu(CPK_IX_WAVES, CPK_IX_WAVES)))
-#else
-#define CPK_IX_ATTR
-#endif
 template <bool SIZE_ONLY, int RD = kRdNone>
-__global__ __launch_bounds__(kWave * kIxBw) CPK_IX_ATTR void decode_index_kernel(
+__global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
@@ -2279,15 +2244,6 @@ __global__ __launch_bounds__(kWave * kIxBw) CPK_IX_ATTR void decode_index_kernel
     status[unit] = (!SIZE_ONLY && 8 * words > cap) ? ST_SPACE : ST_OK;
 }
 
-#ifdef CPK_FILL_PROF
-// Diagnostic build: cycles per fill-kernel phase, summed over waves (s_memtime).
-__device__ unsigned long long cpk_fill_prof[8];
-#define FL_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define FL_ACC(i, d) prof[i] += (d)
-#else
-#define FL_T(v) do { } while (0)
-#define FL_ACC(i, d) do { } while (0)
-#endif
 
 constexpr uint32_t kFlWaves = 4;
 constexpr uint32_t kFlPk = kFlPieces * 16 + 8;    // staged pieces + room for the 16-B read at the last tag
@@ -2469,15 +2425,9 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
     FillMeta cur = meta(0);
     load_unit(cur);
     uint32_t younger = 0;  // vector-memory ops issued after cur's loads (its predecessor's stores)
-#ifdef CPK_FILL_PROF
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
     for (uint32_t k = 0; (uint64_t)u0 + (uint64_t)k * G < n; ++k) {
         const bool go = cur.st == ST_OK && cur.P > 0;
-        FL_T(t0);
         vmcnt_at_most(younger);  // cur's pieces and records are in registers
-        FL_T(t1);
-        FL_ACC(0, t1 - t0);
         younger = 0;
         uint32_t np = 0, end = 0, pos = 0, words = 0, jend = 0;
         if (go) {
@@ -2513,11 +2463,7 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
             load_batch(k1);
         }
         const FillMeta nxt = meta(k1 & 63);  // st = -1 past the batch end
-        FL_T(t2);
-        FL_ACC(1, t2 - t1);
         load_unit(nxt);
-        FL_T(t3);
-        FL_ACC(2, t3 - t2);
         if (go) {
             const uint32_t incl = wave_incl_sum(words, lane);
             const uint32_t wbase = incl - words;
@@ -2556,8 +2502,6 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                     w = act ? w + 1u + (z ? b1 : 0u) + c : w;
                     p = act ? p + 1u + __popc(t) + (uint32_t)(z | f) + 8u * c : p;
                 }
-                FL_T(t4);
-                FL_ACC(3, t4 - t3);
                 wave_lds_sync();
                 if (__builtin_amdgcn_ballot_w64(runs) != 0) {
                     fl_bodies(pk, code, W1 - W0, lane);
@@ -2583,14 +2527,8 @@ __global__ __launch_bounds__(kFlWaves * kWave) void decode_fill_kernel(const uin
                 }
             }
         }
-        FL_T(t5);
-        FL_ACC(4, t5 - t0);
         cur = nxt;
     }
-#ifdef CPK_FILL_PROF
-    if (lane == 0)
-        for (int i = 0; i < 5; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -2657,7 +2595,8 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count,
+    const uint32_t* __restrict__ list_lo) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kLwWaves * kWave * kLwRing];
     __shared__ __attribute__((aligned(16))) uint8_t line_blk[kLwWaves * kWave * 128];  // [lane][slot]
     __shared__ uint16_t ftab_blk[kLwWaves * kWave];  // flush table: lane | lo << 6 | hi << 10, by rank
@@ -2681,11 +2620,12 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     uint8_t* const myline = lines + lane * 128;
     uint16_t* const ftab = ftab_blk + wave * kWave;
     const uint32_t wv = blockIdx.x * kLwWaves + wave;
-    const uint32_t count = list ? *list_count : n;
+    const uint32_t lo = list_lo ? *list_lo : 0u;  // the list's entries [lo, *list_count)
+    const uint32_t count = (list ? *list_count : n) - lo;
     if (wv * kWave >= count) return;  // wave-uniform
     const uint32_t slot = wv * kWave + lane;
     const bool valid = slot < count;
-    const uint32_t unit = valid ? ((list && count != n) ? list[slot] : slot) : 0u;
+    const uint32_t unit = valid ? ((list && (lo != 0 || count != n)) ? list[lo + slot] : slot) : 0u;
 
     // ---- per-lane unit ---------------------------------------------------------------
     const uint8_t* src = cpk_dummy16;
@@ -2805,19 +2745,12 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     uint32_t run = 0, rsel = 0;  // words left in the current run; its selector tag (00 / FF)
     int32_t apos = po;           // po, or INT_MIN during a zero run (its words need no bytes)
     uint32_t W = 0;              // words emitted
-#ifdef CPK_FILL_PROF
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    FL_T(tk0);
-#endif
     if (maxr > 0) load(0);
     for (uint32_t k = 0; k <= maxr; ++k) {
-        FL_T(ta);
         if (k < maxr) {
             vmcnt_at_most63(younger);  // round k's loads are in
             asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
         }
-        FL_T(tb);
-        FL_ACC(0, tb - ta);
         younger = 0;
         if (k > 0) {
             wave_lds_sync();
@@ -2840,10 +2773,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
             wave_lds_sync();
         }
         const int32_t lim = min(64, end_o);  // sources of this round: ring offsets < lim
-        FL_T(tc);
-        FL_ACC(1, tc - tb);
         for (;;) {  // sub-rounds
-            FL_T(td);
             // ---- A: the chain. Step j leaves (payload ring offset | selector tag << 8) in rec[j] ----
             uint32_t rec[kLwS];
 #pragma unroll
@@ -2871,11 +2801,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                     apos = (run != 0u && rsel == 0u) ? INT32_MIN : po;
                     e = j + 1;
                 }
-                FL_ACC(5, 1);
             }
-            FL_T(te);
-            FL_ACC(2, te - td);
-            FL_ACC(6, 1);
             // ---- B: the words (selectors looked up and applied off the chain) ----
             uint64_t w[kLwS];
 #pragma unroll
@@ -2898,8 +2824,6 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
             for (uint32_t j = 0; j < kLwS; ++j)
                 if (j < e && j < f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & 15u)) = w[j];
             const bool full = e >= f && e != 0u;
-            FL_T(tf0);
-            FL_ACC(3, tf0 - te);
             if (__builtin_amdgcn_ballot_w64(full) != 0) {
                 const uint32_t L = (s0 + W) >> 4;
                 flush(full, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, 16u));
@@ -2909,8 +2833,6 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                     if (j < e && j >= f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & 15u)) = w[j];
             }
             W += e;
-            FL_T(tf1);
-            FL_ACC(4, tf1 - tf0);
             if (__builtin_amdgcn_ballot_w64(apos < lim) == 0) break;
         }
     }
@@ -2921,12 +2843,6 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         flush(part, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, hi));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef CPK_FILL_PROF
-    FL_T(tk1);
-    FL_ACC(7, tk1 - tk0);
-    if (lane == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
-#endif
     if (!valid) return;
     if (st == kStNeedFull) {  // the long-unit decoders' (launch_decode never lists these here)
         status[unit] = st;
@@ -2943,22 +2859,18 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     status[unit] = 8ull * W > cap ? ST_SPACE : ST_OK;
 }
 
-// The single-read mid-unit decoders (fused, round 3; streaming, round 4) measured slower than
-// the two-pass decoder and live in a dev build only.
-#ifndef CPK_DEV_DECODERS
-#define CPK_DEV_DECODERS 0
-#endif
-#if CPK_DEV_DECODERS
-#include "dev_decoders.inc"
-#endif
+// The earlier single-read mid-unit decoders (fused, round 3; streaming, round 4) measured slower
+// than the two-pass decoder and were removed in round 5; their source is at 869fccf
+// (csrc/dev_decoders.inc).
 
 // ---- size classes ------------------------------------------------
 // A batch's units are split by size before the coding kernels run, so each kernel gets
 // units of the shape it is built for:
-//   small: lane per unit (encode_small_kernel / decode_small_kernel): units so short that
+//   small: lane per unit (encode_stream_kernel / decode_small_kernel): units so short that
 //          a wave per unit would leave most of its 64 lanes idle (config C5: median 15 words);
-//   mid:   a wave per unit (encode_kernel) / the indexed decoder (decode_index_kernel,
-//          64 units per wave, then decode_fill_kernel, a wave per unit);
+//   mid:   a wave per unit (encode_kernel) / the words decoder (decode_words_kernel, a lane
+//          per unit) or the indexed decoder (decode_index_kernel, 64 units per wave, then
+//          decode_fill_kernel, a wave per unit);
 //   long, huge: a wave per unit walking it tile by tile / window by window
 //          (encode_tiled_kernel / decode_wave_kernel<kWvLong>), on the side stream.
 // Workspace q (queue_bytes(n)): q[0] long, q[2] huge, q[3] small and q[4] mid counts, q[5]
@@ -2967,21 +2879,21 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
 // q[kQHead + 2n ..], kClassK counts per class block, the serial list (serial_off), then the
 // tile table (encode) or the window table (decode). Count, scan, scatter: each list keeps
 // batch order, and no atomic is contended.
-// decode mid units are binned by packed length (CL_MID + 0..3: <= 1280, <= 2048, <= 3072,
-// more bytes), so the lanes of an index-pass wave walk units of similar length in lockstep;
-// the mid list is the bins in order (batch order within a bin). The streaming decoder
-// (KIND 3) takes small and mid units together: 8 bins (<= 64, 128, 256, 512, 1280, 2048,
-// 3072, more packed bytes), so a wave's 64 lanes walk units of about as many 64-B rounds.
+// decode mid units are binned by packed length (CL_MID + 0..7: <= 768, 1024, 1280, 1536, 2048,
+// 2560, 3072, more bytes), so the lanes of an index-pass or words-decoder wave walk units of
+// similar length in lockstep; the mid list is the bins in order (batch order within a bin), and
+// q[20] is the two-pass decoder's share of it (class_scan_kernel).
 enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3, CL_MID_BINS = 8 };
 constexpr uint64_t kSmEncWords = 64;  // encode: units of at most 64 words are small
 constexpr uint64_t kSmDecP = 512;     // decode: small = at most 512 packed bytes ...
 constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
+constexpr uint64_t kMidSplitP = 1280; // decode: mid units of at most this many packed bytes (bins 0 .. 2)
 
 __device__ __forceinline__ uint32_t* q_blocks(uint32_t* q, uint32_t n) { return q + kQHead + 3ull * n; }
 
-// KIND 0: encode, 1: decode (small lane kernel + indexed / fused mid decoders), 2: decoded size
-// (no output: long by packed length alone), 3: decode by the streaming decoder (no small class),
-// 4: encode with the streaming small-unit encoder (mid units bin 0, small units bins 4 .. 7)
+// KIND 1: decode (small lane kernel + words / indexed mid decoders), 2: decoded size (no output:
+// long by packed length alone), 4: encode with the streaming small-unit encoder (mid units bin
+// 0, small units bins 4 .. 7)
 template <int KIND>
 __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
@@ -2992,29 +2904,18 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
         if (len > 0 && ((s + len + 15) >> 4) > kFlPieces) return len > kQHuge ? CL_HUGE : CL_LONG;
         return CL_MID;
     }
-    if (KIND == 0 || KIND == 4) {
+    if (KIND == 4) {
         if (encode_tiled_unit(in, off, len)) return len > kQHuge ? CL_HUGE : CL_LONG;
         const bool valid = !(reinterpret_cast<uintptr_t>(in + off) & 7) && !(len & 7);
         const bool small = !valid || (len >> 3) <= kSmEncWords;
-        if (KIND == 0) return small ? CL_SMALL : CL_MID;
         const uint64_t w = len >> 3;
         return !small ? CL_MID : CL_MID + 4 + (valid && w > 8) + (valid && w > 16) + (valid && w > 32);
     }
     const uint64_t cap = out_cap[u];
-    if (KIND == 5) {  // dev (CPK_DS_SMALL): small units binned for the streaming decoder, mid units bin 0
-        if (len <= kSmDecP && cap <= kSmDecCap)
-            return CL_MID + 4 + (len > 64) + (len > 128) + (len > 256);
-        if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
-        return CL_MID;
-    }
-    if (KIND == 3) {
-        if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
-        return CL_MID + (len > 64) + (len > 128) + (len > 256) + (len > 512) + (len > 1280) + (len > 2048) +
-               (len > 3072);
-    }
     if (len <= kSmDecP && cap <= kSmDecCap) return CL_SMALL;
     if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
-    return CL_MID + (len > 1280) + (len > 2048) + (len > 3072);
+    return CL_MID + (len > 768) + (len > 1024) + (len > kMidSplitP) + (len > 1536) + (len > 2048) + (len > 2560) +
+           (len > 3072);
 }
 
 // Pass 1: units per class in each block of kClassBlock units; long units get the
@@ -3044,7 +2945,7 @@ __global__ __launch_bounds__(kClassBlock) void class_count_kernel(const uint8_t*
 }
 
 // Pass 2 (one block): exclusive scan of the block counts per class, and the totals.
-__global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t n, uint32_t nb) {
+__global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t n, uint32_t nb, uint32_t words_min) {
     __shared__ uint32_t wsum[16][kClassK];
     __shared__ uint32_t carry[kClassK];
     uint32_t* const bl = q_blocks(q, n);
@@ -3085,6 +2986,13 @@ __global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t 
             mid += carry[CL_MID + b];
         }
         q[4] = mid;
+        // decode: the mid list's share for the two-pass decoder, [0, q[20]); the words decoder
+        // takes [q[20], mid). words_min 0: all to the words decoder; else the units over
+        // kMidSplitP packed bytes (bins 3 .. 7) when there are at least words_min of them
+        // (the words decoder is a throughput design, and a wave's walk of
+        // ~600 steps is long: under a resident grid of units, or at p ~ 0.9, two-pass wins)
+        const uint32_t over = mid - q[11 + 3];
+        q[20] = words_min == 0 ? 0u : (over >= words_min ? q[11 + 3] : mid);
     }
 }
 
@@ -3627,10 +3535,6 @@ __global__ __launch_bounds__(kWvBlock) void window_fill_kernel(const uint8_t* __
 // completed in one round sits next to its neighbours of the previous one, so lines fill up in
 // L2 within a round or two. The small units come binned by length (<= 8, 16, 32, 64 words:
 // 1, 2, 4 or 8 rounds; unit_class<4>), so a wave's units take about as many rounds.
-#ifndef CPK_ES_STREAM  // 1: small units by encode_stream_kernel; 0 (dev build): encode_small_kernel
-#define CPK_ES_STREAM 1
-#endif
-#if CPK_ES_STREAM
 constexpr uint32_t kEsWaves = 4;
 constexpr uint32_t kEsBins = 4;   // small-unit bins of unit_class<4>: mid list bins 4 .. 7
 constexpr uint32_t kEsRing = 80;  // ring row per unit: 64 B + 16 B pad (spreads the lanes' banks)
@@ -3860,11 +3764,10 @@ __global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
     status[unit] = st != ST_OK ? st : ((WRITE && op > cap) ? ST_SPACE : ST_OK);
 }
 
-#endif  // CPK_ES_STREAM
 
 // ---- small units, lane per unit ----------------------------------------------------------
-// (encode_small_kernel is the dev build's, CPK_ES_STREAM=0: C5 encode 0.630 ms against the
-// streaming encoder's 0.588-0.603, same box; decode_small_kernel ships.)
+// (a lane-per-unit encode_small_kernel, removed in round 5 (at 869fccf), measured C5 encode
+// 0.630 ms against the streaming encoder's 0.588-0.603, same box)
 // A persistent grid: each wave owns a contiguous range of the small list and its lanes
 // take the range's next unit as they finish (a wave-uniform cursor, as in
 // validate_kernel), so one longer unit does not idle the rest of its wave. Every turn
@@ -3874,226 +3777,6 @@ __global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
 constexpr uint32_t kSmBlock = 256;
 enum : uint32_t { SM_IDLE, SM_EXIT, SM_META, SM_FIRST, SM_RUN };
 
-#if !CPK_ES_STREAM
-// Zig encoder rules (message.zig:200-271) as a word-at-a-time state machine, one word per
-// step on every lane with a predicated body (no per-word branches): a zero run (00 n-1) is
-// emitted when it ends; a literal run's count byte (FF w0 n-1 w1..) is patched when it ends
-// (in the 16-B chunk being assembled in registers, or with a byte store once that chunk has
-// been written). A turn codes the 4 words read a turn earlier while the next 32 B are read.
-template <bool WRITE>
-__global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* __restrict__ in,
-                                                                const uint64_t* __restrict__ in_off,
-                                                                const uint64_t* __restrict__ in_len, uint32_t n,
-                                                                uint8_t* __restrict__ out,
-                                                                const uint64_t* __restrict__ out_off,
-                                                                const uint64_t* __restrict__ out_cap,
-                                                                uint64_t* __restrict__ out_len,
-                                                                int32_t* __restrict__ status, const uint32_t* q) {
-    __shared__ uint64_t lut[256];
-    if (WRITE) {
-        lut[threadIdx.x] = compact_selector(threadIdx.x);
-        __syncthreads();
-    }
-    // (Round 3 measured a variant staging each lane's output by 64-B windows in LDS for quad
-    // stores: 235 -> 159 MB written per C5 launch, but 96 VGPRs and C5 encode 0.630-0.637 ->
-    // 0.638-0.642 ms; removed in round 4)
-    const uint32_t count = q[3];
-    const uint32_t* const list = q + kQHead + n;
-    const uint32_t lane = lane_id();
-    const uint32_t gw = blockIdx.x * (kSmBlock / kWave) + (threadIdx.x >> 6);
-    const uint32_t GW = gridDim.x * (kSmBlock / kWave);
-    const uint32_t per = (count + GW - 1) / GW;
-    const uint64_t first = (uint64_t)gw * per;
-    const uint64_t last = min((uint64_t)count, first + per);
-    uint64_t cursor = first;  // wave-uniform
-
-    uint32_t kind = SM_IDLE, unit = 0;
-    const uint8_t* cb = in;     // 32-B aligned base of the unit's input
-    uint32_t s8 = 0, nw = 0;    // word index space: the unit's words are [s8, nw)
-    uint32_t cj = 0, nch = 0;   // current 32-B chunk; chunks of the unit
-    uint4 c0, c1, n0, n1;       // the chunk being coded, the next one (in flight)
-    uint8_t* db = out;          // 16-B aligned base of the output slot
-    uint32_t da = 0;            // slot start & 15
-    uint64_t cap = 0, op = 0;   // slot capacity; packed bytes so far
-    uint64_t b0 = 0, b1 = 0;    // the output chunk being assembled: chunk (da + op) >> 4
-    uint32_t mode = 0, run = 0; // 0: none, 1: zero run, 2: literal run; its length
-    uint64_t cpos = 0;          // literal run: output offset of its count byte
-
-    auto finish = [&](int32_t st, uint64_t len) {
-        out_len[unit] = len;
-        status[unit] = st;
-        kind = SM_IDLE;
-    };
-    // write bytes [lo, hi) of output chunk `ch` = (x0, x1) (slot-relative, clipped to the slot)
-    auto flush = [&](uint64_t ch, uint64_t x0, uint64_t x1, uint32_t lo, uint32_t hi) {
-        const uint64_t cs = 16 * ch;
-        const uint64_t lim = cap > ~0ull - 16 ? ~0ull : da + cap;  // slot end (saturated)
-        const uint64_t a = max(cs + lo, (uint64_t)da), e = min(cs + hi, lim);
-        if (a >= e) return;
-        if (a == cs && e == cs + 16) {
-            // plain store: a later count-byte patch of this chunk must land after it
-            *reinterpret_cast<u32x4*>(db + cs) = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
-                                                      (uint32_t)(x1 >> 32)};
-        } else {
-            // a unit's first / last chunk
-            store_partial16(db + cs, (uint32_t)(a - cs), (uint32_t)(e - cs), x0, x1);
-        }
-    };
-    // a step appends <= 12 bytes, so it completes at most one chunk: kept here, written
-    // once at the end of the step
-    uint64_t f0 = 0, f1 = 0, fch = 0;
-    bool fpend = false;
-    // append nb <= 8 bytes of v (higher bytes zero) when p
-    auto app = [&](bool p, uint64_t v, uint32_t nb) {
-        if (WRITE) {
-            const uint32_t k = (uint32_t)((da + op) & 15);
-            const uint32_t sh = 8 * (k & 7);
-            const uint64_t lo = v << sh, hi = (v >> 1) >> (63 - sh);  // v's bytes at chunk bytes k ..
-            const bool low = k < 8;
-            if (p) {
-                b0 |= low ? lo : 0ull;
-                b1 |= low ? hi : lo;
-            }
-            if (p && k + nb >= 16) {  // the chunk is complete (k >= 8): keep it, continue with the spill
-                f0 = b0;
-                f1 = b1;
-                fch = (da + op) >> 4;
-                fpend = true;
-                b0 = hi;
-                b1 = 0;
-            }
-        }
-        op += p ? nb : 0u;
-    };
-    // the open literal run's count byte = c (in the chunk being assembled, the completed
-    // one not yet written, or the slot)
-    auto patch = [&](bool p, uint32_t c) {
-        if (!WRITE || !p) return;
-        const uint64_t x = da + cpos;
-        const uint32_t k = (uint32_t)(x & 15);
-        const uint64_t m0 = k < 8 ? (uint64_t)c << (8 * k) : 0ull, m1 = k < 8 ? 0ull : (uint64_t)c << (8 * (k - 8));
-        if ((x >> 4) == ((da + op) >> 4)) {
-            b0 |= m0;
-            b1 |= m1;
-        } else if (fpend && (x >> 4) == fch) {
-            f0 |= m0;
-            f1 |= m1;
-        } else if (cpos < cap) {
-            db[x] = (uint8_t)c;
-        }
-    };
-    auto step = [&](uint64_t w, bool valid) {  // message.zig:206-266, one word
-        const uint32_t tg = nonzero_tag(w);
-        const bool isz = tg == 0u, isf = tg == 0xFFu;
-        const bool cz = valid && mode == 1 && isz && run < 256;  // continues the zero run
-        const bool cf = valid && mode == 2 && isf && run < 256;  // continues the literal run
-        const bool cl = valid && mode != 0 && !cz && !cf;        // the open run ends here
-        app(cl && mode == 1, (uint64_t)(run - 1) << 8, 2);       // 00 <count>
-        patch(cl && mode == 2, run - 1);
-        const bool nz = valid && !cz && !cf && isz;  // a new zero run
-        const bool nf = valid && !cz && !cf && isf;  // a new literal run
-        const bool mx = valid && !isz && !isf;       // tag + nonzero bytes
-        const uint64_t v = cf ? w : (nf ? (0xFFull | (w << 8)) : ((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) << 8 : 0ull)));
-        app(cf || nf || mx, v, (cf || nf) ? 8u : 1u + __popc(tg));
-        app(nf, w >> 56, 2);  // w7, then the count byte (0 until patched)
-        cpos = nf ? op - 1 : cpos;
-        mode = (cz || nz) ? 1u : ((cf || nf) ? 2u : (valid ? 0u : mode));
-        run = (cz || cf) ? run + 1 : ((nz || nf) ? 1u : run);
-        if (WRITE && fpend) {
-            flush(fch, f0, f1, 0, 16);
-            fpend = false;
-        }
-    };
-    for (;;) {
-        const uint64_t idle = __ballot(kind == SM_IDLE);
-        if (idle) {
-            if (cursor < last) {
-                if (kind == SM_IDLE) {
-                    const uint64_t id = cursor + __popcll(idle & ((1ull << lane) - 1ull));
-                    if (id < last) {
-                        unit = list[id];
-                        kind = SM_META;
-                    } else {
-                        kind = SM_EXIT;
-                    }
-                }
-                cursor += __popcll(idle);
-            } else if (kind == SM_IDLE) {
-                kind = SM_EXIT;
-            }
-        }
-        if (__ballot(kind != SM_EXIT) == 0) break;
-        // ---- this turn's reads -----------------------------------------------------------
-        uint64_t m_off = 0, m_len = 0, m_oo = 0, m_cap = 0;
-        if (kind == SM_META) {
-            m_off = in_off[unit];
-            m_len = in_len[unit];
-            if (WRITE) {
-                m_oo = out_off[unit];
-                m_cap = out_cap[unit];
-            }
-        } else if (kind == SM_FIRST) {
-            c0 = *reinterpret_cast<const uint4*>(cb);
-            c1 = *reinterpret_cast<const uint4*>(cb + 16 * (uint32_t)(nw > 2));
-        } else if (kind == SM_RUN && cj + 1 < nch) {
-            const uint8_t* const g = cb + 32ull * (cj + 1);
-            n0 = *reinterpret_cast<const uint4*>(g);
-            n1 = *reinterpret_cast<const uint4*>(g + 16 * (uint32_t)(4 * (cj + 1) + 2 < nw));
-        }
-        // ---- code what the previous turn read -----------------------------------------------
-        const bool run_now = kind == SM_RUN;
-        if (kind == SM_META) {
-            const uint8_t* const src = in + m_off;
-            if (reinterpret_cast<uintptr_t>(src) & 7) finish(ST_ARG, 0);
-            else if (m_len & 7) finish(ST_SIZE, 0);  // message.zig:201
-            else if (m_len == 0) finish(ST_OK, 0);
-            else {
-                const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 31);  // 0, 8, 16, 24
-                s8 = s >> 3;
-                cb = src - s;
-                nw = s8 + (uint32_t)(m_len >> 3);
-                nch = (nw + 3) >> 2;
-                uint8_t* const dst = out + m_oo;
-                da = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
-                db = dst - da;
-                cap = m_cap;
-                op = 0;
-                b0 = b1 = 0;
-                mode = 0;
-                cj = 0;
-                kind = SM_FIRST;
-            }
-        } else if (kind == SM_FIRST) {
-            kind = SM_RUN;  // chunk 0 is coded next turn
-        }
-        if (__ballot(run_now) != 0) {
-            const uint32_t w0 = 4 * cj;
-#pragma nounroll
-            for (uint32_t t = 0; t < 4; ++t) {  // one word after another (unrolled: 116 VGPRs)
-                const uint4 c = t < 2 ? c0 : c1;
-                const uint64_t w = (t & 1) ? ((uint64_t)c.z | ((uint64_t)c.w << 32)) : ((uint64_t)c.x | ((uint64_t)c.y << 32));
-                step(w, run_now && w0 + t >= s8 && w0 + t < nw);
-            }
-            if (run_now) {
-                if (cj + 1 < nch) {
-                    c0 = n0;
-                    c1 = n1;
-                    ++cj;
-                } else {
-                    app(mode == 1, (uint64_t)(run - 1) << 8, 2);  // the unit ends inside a run
-                    patch(mode == 2, run - 1);
-                    if (WRITE && fpend) {
-                        flush(fch, f0, f1, 0, 16);
-                        fpend = false;
-                    }
-                    if (WRITE && ((da + op) & 15)) flush((da + op) >> 4, b0, b1, 0, (uint32_t)((da + op) & 15));
-                    finish((WRITE && op > cap) ? ST_SPACE : ST_OK, op);
-                }
-            }
-        }
-    }
-}
-#endif  // !CPK_ES_STREAM
 
 
 // unpackPacked (message.zig:88-145) for one unit per lane. Each lane keeps a 64-B ring of
@@ -4110,10 +3793,7 @@ __global__ __launch_bounds__(kSmBlock) void encode_small_kernel(const uint8_t* _
 // lanes per chunk (16 chunks of 64 contiguous bytes per store instruction). A unit's partial
 // first and last chunks, and chunks a zero run completes, are stored by their lane.
 constexpr uint32_t kSdRing = 80;  // LDS bytes per lane: the 64-B ring + 16 B (fewer bank conflicts)
-#ifndef CPK_SD_CHUNK
-#define CPK_SD_CHUNK 8
-#endif
-constexpr uint32_t kSdChunk = CPK_SD_CHUNK;         // output words per staged chunk (64 B)
+constexpr uint32_t kSdChunk = 8;         // output words per staged chunk (64 B)
 constexpr uint32_t kSdGroup = 2 * kWave / kSdChunk; // chunks per cooperative store instruction
 __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* __restrict__ in,
                                                                 const uint64_t* __restrict__ in_off,
@@ -4406,11 +4086,7 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
     const uint32_t per = (count + GW - 1) / GW;
     uint64_t cursor = (uint64_t)gw * per;
     const uint64_t last = min((uint64_t)count, cursor + per);
-#ifdef CPK_FILL_PROF
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
     while (cursor < last) {  // wave-uniform
-        FL_T(t0);
         // ---- 1. meta of the next (up to) 64 entries -----------------------------------------
         const bool valid = cursor + lane < last;
         uint32_t unit = 0, P = 0, s = 0, np = 0, capw = 0;
@@ -4436,8 +4112,6 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
         wave_lds_sync();  // the previous group's LDS reads are done
         ppf[lane] = mine ? pb : 0xFFFFFFFFu;
         wave_lds_sync();
-        FL_T(t1);
-        FL_ACC(0, t1 - t0);
         // ---- 2. load the group's pieces, flattened ------------------------------------------
         // piece j of the group: its unit k (binary search of the piece prefix), then 16 B from
         // the unit's aligned base (all lanes take part in the bpermutes; past NP they re-load
@@ -4457,8 +4131,6 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
             if (jb < NP) *reinterpret_cast<uint4*>(pin + 16 * jb) = vb;
         }
         wave_lds_sync();
-        FL_T(t2);
-        FL_ACC(1, t2 - t1);
         // ---- 3. decode: lane i walks unit i -------------------------------------------------
         const uint8_t* const b = pin + (mine ? 16 * pb : 0u);
         uint64_t* const o = pout + (mine ? wb : 0u);
@@ -4504,8 +4176,6 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
             }
         }
         if (mine && st == ST_OK && wo > capw) st = ST_SPACE;
-        FL_T(t3);
-        FL_ACC(2, t3 - t2);
         // ---- 4. store the OK units' words, flattened by 16-B pairs -----------------------------
         const uint32_t npair = (mine && st == ST_OK) ? (wo + 1) >> 1 : 0u;
         const uint32_t ipr = wave_incl_sum(npair, lane);
@@ -4538,15 +4208,7 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
             status[unit] = st;
         }
         cursor += g;
-        FL_T(t4);
-        FL_ACC(3, t4 - t3);
-        FL_ACC(4, g);
-        FL_ACC(5, 1);
     }
-#ifdef CPK_FILL_PROF
-    if (lane == 0)
-        for (int i = 0; i < 6; ++i) atomicAdd(&cpk_fill_prof[i], (unsigned long long)prof[i]);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -4583,10 +4245,7 @@ constexpr uint32_t kVdDepth = 64;  // frames per lane in LDS + private scratch (
 // levels, far past the depth at which the reference's recursive validatePointer exhausts
 // its thread stack. It bounds the DEEP kernel's frame stack and every far-pointer chain.
 constexpr uint32_t kVdMaxNest = 1u << 18;
-#ifndef CPK_VD_LDS
-#define CPK_VD_LDS 8
-#endif
-constexpr uint32_t kVdLds = CPK_VD_LDS;  // stack frames per lane held in LDS
+constexpr uint32_t kVdLds = 8;  // stack frames per lane held in LDS
 constexpr uint32_t kVdSegs = 4;          // segments per lane whose offsets are held in LDS
 
 enum : uint32_t {
@@ -4632,12 +4291,8 @@ struct VdDeep {
 template <bool DEEP>
 // Occupancy: the compiler's choice (129 VGPRs) gives 3 waves/SIMD; pinned at 4 (127 VGPRs, 4
 // spilled) the trees leg runs 1.87 instead of 1.95-1.96 ms; at 5 (78 spilled) 3.42 ms (same box,
-// scripts/dev/vd_ab.sh; CPK_VD_WAVES overrides for A/B).
-#ifndef CPK_VD_WAVES
-#define CPK_VD_WAVES 4
-#endif
-#define CPK_VD_ATTR __attribute__((amdgpu_waves_per_eu(CPK_VD_WAVES, CPK_VD_WAVES)))
-__global__ __launch_bounds__(kWave) CPK_VD_ATTR void validate_kernel(const uint8_t* __restrict__ in,
+// scripts/dev/vd_ab.sh against the round-4 source).
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 4))) void validate_kernel(const uint8_t* __restrict__ in,
                                                          const uint64_t* __restrict__ in_off,
                                                          const uint64_t* __restrict__ in_len, uint32_t n,
                                                          uint32_t per_wave, uint64_t seg_limit, uint64_t trav_limit,
@@ -5486,10 +5141,10 @@ static uint32_t resident_blocks(K kernel, int block, uint32_t fallback_per_cu) {
 template <int KIND>
 static void launch_classes(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                            uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint32_t* q,
-                           int32_t* status, hipStream_t stream) {
+                           int32_t* status, hipStream_t stream, uint32_t words_min = ~0u) {
     const uint32_t nb = (n + kClassBlock - 1) / kClassBlock;
     class_count_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q, status);
-    class_scan_kernel<<<1, 1024, 0, stream>>>(q, n, nb);
+    class_scan_kernel<<<1, 1024, 0, stream>>>(q, n, nb, words_min);
     class_scatter_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q);
 }
 
@@ -5682,10 +5337,6 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     // classes (caller's stream), then the long units on the side stream (encode_tiled_kernel
     // over a grid taking units from the queue) beside the small units (a lane each) and the
     // mid units (a wave each) on the caller's stream
-#if !CPK_ES_STREAM
-    static const uint32_t sm_res = resident_blocks(encode_small_kernel<true>, kSmBlock, 8);
-    const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_res);
-#endif
     // long-unit workers: up to one wave per unit, at most the resident grid (a batch of a
     // few long units must not get a grid sized by its unit count / 256)
     static const uint32_t tiled_res = resident_blocks(encode_tiled_kernel<true>, kBlock, 3);
@@ -5694,14 +5345,9 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-#if CPK_ES_STREAM  // small units: the streaming encoder (mid-list bins 4 .. 7)
     launch_classes<4>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
     const uint32_t* const mid_count = q + 12;  // bin 0: the units before bin 1
     const uint32_t es_blocks = (n + kEsWaves * kWave - 1) / (kEsWaves * kWave);  // waves past the count exit
-#else
-    launch_classes<0>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
-    const uint32_t* const mid_count = q + 4;
-#endif
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
     const hipStream_t ss = side.stream();
@@ -5720,13 +5366,8 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
         if (ms != stream)  // LAUNCH_MID_SIDE_STREAM: the mid units beside the small ones
             encode_kernel<true><<<mid_blocks, kBlock, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap, out_len,
                                                                 status, mid, mid_count);
-#if CPK_ES_STREAM
         encode_stream_kernel<true><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                                out_cap, out_len, status, q);
-#else
-        encode_small_kernel<true><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                       out_cap, out_len, status, q);
-#endif
         if (ms == stream)
             encode_kernel<true><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                     out_len, status, mid, mid_count);
@@ -5740,13 +5381,8 @@ hipError_t launch_encode(const uint8_t* in, const uint64_t* in_off, const uint64
         if (ms != stream)
             encode_kernel<false><<<mid_blocks, kBlock, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                  out_len, status, mid, mid_count);
-#if CPK_ES_STREAM
         encode_stream_kernel<false><<<es_blocks, kEsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
                                                                                 out_cap, out_len, status, q);
-#else
-        encode_small_kernel<false><<<sm_blocks, kSmBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                        out_cap, out_len, status, q);
-#endif
         if (ms == stream)
             encode_kernel<false><<<mid_blocks, kBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                      out_len, status, mid, mid_count);
@@ -5798,14 +5434,10 @@ static std::atomic<int> g_decoder{CAPNP_PACKED_DECODER_AUTO};
 static std::atomic<int> g_small{1};
 static int small_variant() { return g_small.load(std::memory_order_relaxed); }
 int set_all_or_nothing(int on) { return g_small.exchange(on ? 0 : 1) == 0 ? 1 : 0; }
-static int decoder_variant() {
-    const int v = g_decoder.load(std::memory_order_relaxed);
-    return v == CAPNP_PACKED_DECODER_AUTO ? (int)CAPNP_PACKED_DECODER_TWO_PASS : v;
-}
+static int decoder_variant() { return g_decoder.load(std::memory_order_relaxed); }
 int set_decoder(int v) { return g_decoder.exchange(v); }
 bool decoder_built(int v) {
-    return v == CAPNP_PACKED_DECODER_AUTO || v == CAPNP_PACKED_DECODER_TWO_PASS || v == CAPNP_PACKED_DECODER_WORDS ||
-           CPK_DEV_DECODERS;
+    return v == CAPNP_PACKED_DECODER_AUTO || v == CAPNP_PACKED_DECODER_TWO_PASS || v == CAPNP_PACKED_DECODER_WORDS;
 }
 
 hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
@@ -5853,26 +5485,17 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     const double sm_frac = mid_stream ? 0.85 : 1.0;  // share of the resident grid
     const uint32_t sm_cap = std::max(1u, (uint32_t)(sm_res * sm_frac));
     const uint32_t sm_blocks = min((n + kSmBlock - 1) / kSmBlock, sm_cap);
-#if CPK_DEV_DECODERS
-    // the streaming decoder may leave a failed unit's prefix: all-or-nothing takes the two-pass one
-    const int dv = (decoder_variant() == CAPNP_PACKED_DECODER_STREAM && small_variant() == 0)
-                       ? (int)CAPNP_PACKED_DECODER_TWO_PASS : decoder_variant();
-    const bool streaming = dv == CAPNP_PACKED_DECODER_STREAM;
-#else
-    constexpr bool streaming = false;
-#endif
+    // mid units: the words decoder where it pays (AUTO: class_scan_kernel's rule, from a grid of
+    // its resident units) or for all of them (WORDS); the rest two-pass. The words decoder may
+    // leave a failed unit's prefix, so all-or-nothing decodes take the two-pass decoder only.
+    const bool words = (decoder_variant() == CAPNP_PACKED_DECODER_AUTO ||
+                        decoder_variant() == CAPNP_PACKED_DECODER_WORDS) && small_variant() != 0;
+    static const uint32_t words_min = resident_blocks(decode_words_kernel, kLwWaves * kWave, 6) * kLwWaves * kWave;
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
-#ifndef CPK_DS_SMALL  // dev: 1 = the streaming decoder takes the small units only, mid units two-pass
-#define CPK_DS_SMALL 0
-#endif
-    if (streaming && CPK_DS_SMALL)
-        launch_classes<5>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
-    else if (streaming)  // small and mid units in one list, binned by packed length
-        launch_classes<3>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
-    else
-        launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream);
+    launch_classes<1>(in, in_off, in_len, n, out, out_off, out_cap, q, status, stream,
+                      !words ? ~0u : (decoder_variant() == CAPNP_PACKED_DECODER_WORDS ? 0u : words_min));
     hipError_t e = side.fork();
     if (e != hipSuccess) return e;
     // long units, window-parallel (window table) or, if the table is full, serial
@@ -5893,30 +5516,6 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     decode_wave_kernel<kWvLong><<<long_blocks, kWvBlock, 0, ss>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                    out_len, status, q);
     const uint32_t* const mid = q + kQHead + 2ull * n;
-#if CPK_DEV_DECODERS
-    if (streaming && CPK_DS_SMALL) {  // small units by the streaming decoder, mid units two-pass
-        const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);
-        decode_stream_kernel<true><<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                out_cap, out_len, status, q, nullptr);
-        uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);
-        decode_index_kernel<false><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(
-            in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 12, rec);
-        decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                              out_len, out_cap, status, mid, q + 12,
-                                                                              rec);
-        e = hipGetLastError();
-        const hipError_t j = side.join();
-        return e != hipSuccess ? e : j;
-    }
-    if (streaming) {  // small and mid units, 64 per wave
-        const uint32_t sd_blocks = (n + kDsWaves * kWave - 1) / (kDsWaves * kWave);  // waves past the count exit
-        decode_stream_kernel<false><<<sd_blocks, kDsWaves * kWave, 0, stream>>>(in, in_off, in_len, n, out, out_off,
-                                                                                 out_cap, out_len, status, mid, q + 4);
-        e = hipGetLastError();
-        const hipError_t j = side.join();
-        return e != hipSuccess ? e : j;
-    }
-#endif
     // the mid units' passes on a second side stream, before the small kernel (mid_side_stream)
     const hipStream_t ms = mid_stream ? side.stream2() : stream;
     if (!mid_stream) {
@@ -5932,19 +5531,16 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     }
     // mid units: the indexed two-pass decoder (index pass + fill pass), the single-read words
     // decoder, or in a dev build the fused single-pass decoder (capnp_packed_set_decoder)
-    if (decoder_variant() == CAPNP_PACKED_DECODER_WORDS && small_variant() != 0) {
+    if (words) {  // [0, q[20]) two-pass, [q[20], q[4]) words (either may be empty)
         const uint32_t lw_blocks = (n + kLwWaves * kWave - 1) / (kLwWaves * kWave);
+        uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);
+        decode_index_kernel<false><<<ix_blocks_for(n), kWave * kIxBw, 0, ms>>>(
+            in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 20, rec);
+        decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off,
+                                                                           out_len, out_cap, status, mid, q + 20, rec);
         decode_words_kernel<<<lw_blocks, kLwWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                   out_len, status, mid, q + 4);
+                                                                   out_len, status, mid, q + 4, q + 20);
     } else
-#if CPK_DEV_DECODERS
-    if (dv == CAPNP_PACKED_DECODER_FUSED) {
-        static const uint32_t fu_res = resident_blocks(decode_fused_kernel, kFuWaves * kWave, 5);
-        const uint32_t fu_blocks = std::min((n + kFuWaves - 1) / kFuWaves, fu_res);
-        decode_fused_kernel<<<fu_blocks, kFuWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                        out_len, status, mid, q + 4);
-    } else
-#endif
     {
         uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
         decode_index_kernel<false><<<ix_blocks_for(n), kWave * kIxBw, 0, ms>>>(
@@ -6183,17 +5779,3 @@ hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t*
 }  // namespace cpk
 
 // Diagnostic builds only: read and clear the phase cycle sums.
-#ifdef CPK_EM_PROF
-extern "C" int capnp_packed_debug_em_prof(unsigned long long* out8) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_em_prof), sizeof(z)) != hipSuccess) return 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(cpk::cpk_em_prof), z, sizeof(z)) != hipSuccess;
-}
-#endif
-#ifdef CPK_FILL_PROF
-extern "C" int capnp_packed_debug_fill_prof(unsigned long long* out8) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cpk::cpk_fill_prof), sizeof(z)) != hipSuccess) return 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(cpk::cpk_fill_prof), z, sizeof(z)) != hipSuccess;
-}
-#endif

@@ -369,7 +369,11 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
  *   CAPNP_PACKED_DECODER_WORDS     single read: lane per unit, one output word per step
  *                                  (round 5; a failed unit may hold a prefix
  *                                  of its output unless capnp_packed_set_all_or_nothing(1));
- *   CAPNP_PACKED_DECODER_AUTO      the library's default (the two-pass decoder).
+ *   CAPNP_PACKED_DECODER_AUTO      the library's default: the words decoder for the mid units of
+ *                                  more than 1280 packed bytes when a batch has at least a
+ *                                  resident grid of them (~196K units on MI355X), the two-pass
+ *                                  decoder for the rest; all two-pass under
+ *                                  capnp_packed_set_all_or_nothing(1).
  * Dev builds only (built with CPK_DEV_DECODERS=1; the shipped library returns
  * CAPNP_PACKED_INVALID_ARGUMENT for them): the single-read decoders, both measured slower
  * than the two-pass decoder on every density:
@@ -387,12 +391,14 @@ enum {
 int capnp_packed_set_decoder(int decoder);
 
 /* All-or-nothing for small decode units too (process-wide, for batches enqueued from
- * now on; returns the previous setting, 0 or 1). Mid and long units always leave a failed
- * unit's slot untouched (message.zig:90 raises before any output). Small units (<= 512
- * packed bytes into <= 8-KiB slots) are by default decoded a lane each in one streaming
- * pass, and a failed one may keep a prefix of its output (never a byte past out_cap);
- * with on != 0 they are decoded through LDS and stored only when OK, at a cost (C5 decode
- * 0.69 -> 0.79 ms). */
+ * now on; returns the previous setting, 0 or 1). Long units, and mid units the two-pass
+ * decoder takes, always leave a failed unit's slot untouched (message.zig:90 raises before any
+ * output). Small units (<= 512 packed bytes into <= 8-KiB slots) are by default decoded a lane
+ * each in one streaming pass, and mid units the words decoder takes (see
+ * capnp_packed_set_decoder) stream their output out as they go: a failed one may keep a prefix
+ * of its output (never a byte past out_cap). With on != 0, small units are decoded through LDS
+ * and stored only when OK, and every mid unit goes to the two-pass decoder, at a cost (C5
+ * decode 0.69 -> 0.79 ms; the headline decode 2.0 -> 2.5 ms). */
 int capnp_packed_set_all_or_nothing(int on);
 
 /* Launch policy (process-wide, for batches enqueued from now on; returns the previous flags;

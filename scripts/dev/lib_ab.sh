@@ -9,7 +9,7 @@ mkdir -p "$(dirname "$OUT")"
 for r in $(seq 1 "$R"); do
   for L in $LIBS; do
     echo "== $L round $r" >> "$OUT"
-    CPK_LIB=capnp-zig_amd/$L timeout -k 10 240 python3 scripts/dev/dec_ab.py --decoders words --reps 5 "$@" 2>/dev/null | tail -1 >> "$OUT" || exit 1
+    CPK_LIB=capnp-zig_amd/$L timeout -k 10 240 python3 scripts/dev/dec_ab.py --decoders ${DECS:-words} --reps 5 "$@" 2>/dev/null | tail -1 >> "$OUT" || exit 1
   done
 done
 cat "$OUT"

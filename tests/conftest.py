@@ -32,15 +32,13 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
-@pytest.fixture(params=["twopass", "words", "fused", "stream"])
+@pytest.fixture(params=["twopass", "words"])
 def decoder(request):
     """Runs a decode test under each mid-unit decoder (capnp_packed_set_decoder): the two-pass
-    decoder, the single-read words decoder (round 5), and the fused / streaming
-    single-read decoders, which exist in
-    dev builds only (CPK_DEV_DECODERS=1, capnp-zig_amd/lib_exp/dev_decoders.so via CPK_LIB;
-    DESIGN.md §2.3a / §2.3b) and are skipped otherwise."""
+    decoder and the single-read words decoder (round 5), each forced for every
+    mid unit of the batch (the default, "auto", picks between them by batch, class_scan_kernel)."""
     import capnp_packed as cp
     if not cp.decoder_available(request.param):
-        pytest.skip(f"the {request.param} decoder is in dev builds only")
+        pytest.skip(f"the {request.param} decoder is not in this build")
     with cp.decoder(request.param):
         yield request.param

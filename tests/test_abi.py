@@ -107,20 +107,16 @@ def test_status_tables_agree():
 
 def test_decoder_selection_round_trips():
     # capnp_packed_set_decoder is a process-wide knob (no device needed to set it)
-    # the fused / streaming decoders exist in dev builds only (CPK_DEV_DECODERS=1)
-    for dev in ("fused", "stream"):
-        if cp.decoder_available(dev):
-            prev = cp.set_decoder(dev)
-            assert cp.set_decoder("twopass") == dev
-            with cp.decoder(dev):
-                assert cp.set_decoder(dev) == dev
-            assert cp.set_decoder(prev) == "twopass"
-        else:
-            assert cp.lib().capnp_packed_set_decoder(cp.DECODERS[dev]) == cp.INVALID_ARGUMENT
-    prev = cp.set_decoder("twopass")
+    prev = cp.set_decoder("words")
+    assert cp.set_decoder("twopass") == "words"
+    with cp.decoder("words"):
+        assert cp.set_decoder("words") == "words"
     assert cp.set_decoder(prev) == "twopass"
-    if not os.environ.get("CPK_LIB"):  # the shipped build has the two-pass decoder only
-        assert not cp.decoder_available("fused") and not cp.decoder_available("stream")
+    assert cp.decoder_available("auto") and cp.decoder_available("words")
+    # the fused / streaming decoders were removed in round 5
+    for gone in ("fused", "stream"):
+        assert not cp.decoder_available(gone)
+        assert cp.lib().capnp_packed_set_decoder(cp.DECODERS[gone]) == cp.INVALID_ARGUMENT
     assert cp.lib().capnp_packed_set_decoder(7) == cp.INVALID_ARGUMENT
     assert cp.set_all_or_nothing(True) is False
     assert cp.set_all_or_nothing(False) is True

@@ -43,15 +43,15 @@ def words(rng, n_words, thr):
 
 @pytest.mark.parametrize("cls,n_words,thr", CLASSES, ids=[c[0] for c in CLASSES])
 def test_failed_units_leave_their_slot_untouched(cls, n_words, thr, decoder):
-    check_class(cls, n_words, thr, strict=False, prefix_mid=decoder in ("stream", "words"))
+    check_class(cls, n_words, thr, strict=False, prefix_mid=decoder == "words")
 
 
-@pytest.mark.parametrize("dec", ["words", "stream"])
+@pytest.mark.parametrize("dec", ["words", "auto"])
 @pytest.mark.parametrize("cls,n_words,thr", CLASSES[1:], ids=[c[0] for c in CLASSES[1:]])
 def test_mid_units_all_or_nothing_when_asked_under_stream(cls, n_words, thr, dec):
-    """capnp_packed_set_all_or_nothing(1) routes mid units past the single-read streaming
-    decoders (which may leave a failed unit's prefix) to the two-pass decoder: every failed
-    slot untouched."""
+    """capnp_packed_set_all_or_nothing(1) routes mid units past the single-read words decoder
+    (which may leave a failed unit's prefix), forced or by the default's rule, to the two-pass
+    decoder: every failed slot untouched."""
     if not cp.decoder_available(dec):
         pytest.skip(f"the {dec} decoder is not in this build")
     prev = cp.set_all_or_nothing(True)

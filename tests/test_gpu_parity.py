@@ -411,3 +411,36 @@ def test_config3_full_size_density_sweep(thr, decoder):
     check_sample_vs_oracle(d_in, d_pk, plen, slot, 4096, 1024)
     ratio = int(plen.sum().item()) / (1 << 32)
     assert (0.98 < ratio < 1.08) if thr == 26 else (0.18 < ratio < 0.30)  # ~1.033 / ~0.232
+
+
+def test_auto_decoder_splits_mixed_densities():
+    """AUTO on a batch past the words decoder's routing threshold with units on both sides of the
+    split (launch_decode / class_scan_kernel: units of <= 1280 packed bytes two-pass, longer ones
+    by the words decoder): 512K x 4 KiB units alternating p = 0.9 and p = 0.5, plus a tail of
+    p = 0.1 units, decode(encode(x)) == x with every length and status, a strided sample against
+    the oracle."""
+    n2, ub = 1 << 18, 4096
+    a = cp.generate(n2, ub, seed=0xC0DE0031, zero_thresh=230, device=DEV).view(n2, ub)
+    b = cp.generate(n2, ub, seed=0xC0DE0032, zero_thresh=128, device=DEV).view(n2, ub)
+    c = cp.generate(4096, ub, seed=0xC0DE0033, zero_thresh=26, device=DEV).view(4096, ub)
+    d_in = torch.cat([torch.stack([a, b], dim=1).reshape(2 * n2, ub), c]).reshape(-1)
+    del a, b, c
+    n = d_in.numel() // ub
+    in_off, in_len = cp.uniform_layout(n, ub)
+    slot = cp.encode_bound(ub)
+    pk_off, pk_cap = cp.uniform_layout(n, slot)
+    d_pk = torch.empty(n * slot, dtype=torch.uint8, device=DEV)
+    plen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    pst = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_batch(d_in, in_off, in_len, d_pk, pk_off, pk_cap, plen, pst)
+    lens = plen.cpu().numpy()
+    assert (lens[0:2 * n2:2] <= 1280).mean() > 0.99 and (lens[1:2 * n2:2] > 1280).all()
+    d_out = torch.empty(n * ub, dtype=torch.uint8, device=DEV)
+    ulen = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ust = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    with cp.decoder("auto"):
+        cp.decode_batch(d_pk, pk_off, plen, d_out, in_off, in_len, ulen, ust)
+    torch.cuda.synchronize()
+    assert (pst == 0).all().item() and (ust == 0).all().item() and (ulen == ub).all().item()
+    assert torch.equal(d_out, d_in)
+    check_sample_vs_oracle(d_in, d_pk, plen, slot, ub, 512)

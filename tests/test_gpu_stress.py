@@ -107,7 +107,7 @@ def check(packed, caps, ooff, out, out_len, st, sz_len, sz_st, poff, strict_smal
             if want == oracle.OUT_OF_SPACE:
                 assert int(out_len[i]) == len(ref), i
             small = len(p) <= 512 and caps[i] <= 8192
-            # the streaming mid decoder may leave a prefix too; long units
+            # the streaming and words mid decoders may leave a prefix too; long units
             # (> 320 packed 16-B pieces from the unit's 16-B aligned base) never do
             mid = not small and (poff[i] % 16 + len(p) + 15) // 16 <= 320
             if strict_small or not (small or (prefix_mid and mid)):
@@ -117,14 +117,14 @@ def check(packed, caps, ooff, out, out_len, st, sz_len, sz_st, poff, strict_smal
 
 @pytest.mark.parametrize("strict", [False, True])
 def test_mixed_class_stress(decoder, strict):
-    seed = 0xC0DE5000 + {"twopass": 0, "fused": 2, "stream": 4}[decoder] + strict
+    seed = 0xC0DE5000 + {"twopass": 0, "words": 6}[decoder] + strict
     rng, data, packed, caps, _ = build(seed, 1500)
     prev = cp.set_all_or_nothing(strict)
     try:
         res = run_decode(rng, packed, caps)
     finally:
         cp.set_all_or_nothing(prev)
-    check(packed, caps, *res, strict_small=strict, prefix_mid=decoder == "stream" and not strict)
+    check(packed, caps, *res, strict_small=strict, prefix_mid=decoder == "words" and not strict)
 
 
 def test_encode_batch_stress():
