@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--no-read-message", action="store_true", help="skip the Reader.readPackedMessage leg")
     ap.add_argument("--no-skewed", action="store_true", help="skip the skewed-size config C5 leg")
     ap.add_argument("--no-validate", action="store_true", help="skip the Message.validate leg")
+    ap.add_argument("--no-ceilings", action="store_true", help="skip the HBM ceiling sweep (headline-only traces)")
     ap.add_argument("--only", default="", help=argparse.SUPPRESS)  # dev: run one side leg (validate, c5, ...)
     ap.add_argument("--decoder", default="", help=argparse.SUPPRESS)  # dev: capnp_packed_set_decoder name
     return ap.parse_args()
@@ -307,15 +308,15 @@ def ceilings(dev, nbytes, reps=5):
     out, cfg = {}, {}
     for kind, name, mult in ((0, "copy", 2), (1, "read", 1), (2, "write", 1)):
         best = (0.0, None)
-        for grid in (1024, 2048, 4096, 16384):
-            for unr in (2, 4, 8):
+        for grid in (1024, 2048, 4096, 16384, 65536, 262144):
+            for unr in (1, 2, 4, 8):
                 ms = L.cpk_ceiling_stream(kind, a.data_ptr(), b.data_ptr(), nbytes, grid, unr, s, reps)
                 if ms > 0 and mult * nbytes / (ms * 1e-3) / 1e9 > best[0]:
                     best = (mult * nbytes / (ms * 1e-3) / 1e9, f"grid {grid} x 256, {unr} x 16 B in flight")
         out[name], cfg[name] = round(best[0], 1), best[1]
     nsteps = nbytes // (8 * 4096)
     best = (0.0, None)
-    for grid in (1024, 2048, 4096, 16384):
+    for grid in (1024, 2048, 4096, 16384, 65536):
         ms = L.cpk_ceiling_shaped(a.data_ptr(), b.data_ptr(), nsteps, 5, 8, grid, s, reps)
         if ms > 0 and 13 * 4096 * nsteps / (ms * 1e-3) / 1e9 > best[0]:
             best = (13 * 4096 * nsteps / (ms * 1e-3) / 1e9, f"grid {grid} x 256")
@@ -981,7 +982,8 @@ def main():
                 extra["sweep"][name] = sweep_entry(measure(wl, args, k, 2, world, dev), thr, k)
         del wl
         torch.cuda.empty_cache()
-        extra["roofline_ceilings_GBps"] = ceilings(dev, n * ub)
+        if not args.no_ceilings:
+            extra["roofline_ceilings_GBps"] = ceilings(dev, n * ub)
         if not args.no_dense:
             torch.cuda.empty_cache()
             extra["dense_stream"] = dense_leg(args, dev)
