@@ -544,6 +544,25 @@ int oracle_read_packed_message(const uint8_t* in, size_t n, uint8_t* out, size_t
     return 0;
 }
 
+/* One connection's buffered bytes through readPackedMessage until no whole message is left, as
+ * Connection.handleRead's loop does (level2/connection.zig:153-203 over reader.zig:84-156): the
+ * CPU side of scripts/framer_crossover.py. Frames are written back to back into out; returns the
+ * frames read, *used = bytes consumed, *out_total = frame bytes written. */
+size_t oracle_read_stream(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* used,
+                          size_t* out_total) {
+    size_t pos = 0, o = 0, frames = 0;
+    for (;;) {
+        size_t len = 0, cons = 0;
+        if (oracle_read_packed_message(in + pos, n - pos, out + o, cap - o, &len, &cons) != 0) break;
+        pos += cons;
+        o += len;
+        ++frames;
+    }
+    *used = pos;
+    *out_total = o;
+    return frames;
+}
+
 void oracle_pack_batch(const uint8_t* in, const uint64_t* in_off, uint32_t n,
                        uint8_t* out, const uint64_t* out_off, uint64_t* out_len,
                        int32_t* status, int threads) {

@@ -51,6 +51,10 @@ int oracle_message_init(const uint8_t* data, size_t n, uint32_t max_segs,
  * -6 MessageTooLarge, -7 InvalidPackedMessage, -8 OutOfSpace. */
 int oracle_read_packed_message(const uint8_t* in, size_t n, uint8_t* out, size_t cap,
                                size_t* out_len, size_t* consumed);
+/* Connection.handleRead's loop over one connection's bytes (readPackedMessage until no whole
+ * message is left); returns the frames read. */
+size_t oracle_read_stream(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* used,
+                          size_t* out_total);
 
 /* message.zig:699-969 Message.validate over a framed message (Message.init first,
  * message.zig:341-394). Returns a capnp_packed_status code (include/capnp_packed.h):

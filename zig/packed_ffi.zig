@@ -162,6 +162,23 @@ pub extern "capnp_packed" fn capnp_packed_lengths_to_offsets(
 pub const gpu_pack_min_bytes: usize = 64 * 1024;
 pub const gpu_unpack_min_bytes: usize = 64 * 1024;
 
+/// Framer dispatch (INTEGRATION.md §1.8; scripts/framer_crossover.py,
+/// profiles/r05_framer_crossover.json, MI355X + EPYC 9575F host, p = 0.5): one read call of the
+/// device framer session (capnp_packed_framer_readv: gather, H2D, walk, decode, D2H) against
+/// the Zig Framer + readPackedMessage loop on one core, host buffers both sides.
+///   N connections x 16 messages of 4 KiB framed per call: the device is faster from 4
+///     connections (164 KB packed: 587 vs 611 us; 4096 connections: 13.5 vs 655 ms); one
+///     connection (41 KB): 518 vs 142 us, so small batches stay on the CPU.
+///   one connection, a message arriving in 64 KiB reads: faster from 256 KiB framed (503 vs
+///     1342 us; 16 MiB: 17.9 vs 3361 ms), since the device walk resumes across reads while the
+///     CPU framer re-decodes the buffered prefix on every read.
+/// A read batch goes to the device session when its new bytes reach gpu_framer_min_read_bytes,
+/// or when a connection's message in progress (capnp_packed_framer_expected) is at least
+/// gpu_framer_min_message_bytes; a connection moves between the two framers only while it holds
+/// no partial message, so no framer state ever has to be handed over.
+pub const gpu_framer_min_read_bytes: usize = 160 * 1024;
+pub const gpu_framer_min_message_bytes: usize = 256 * 1024;
+
 /// The reference's error names, plus the two the device can add. `NoDevice`
 /// lets the patched message.zig fall back to its own Zig body.
 pub const Error = error{
