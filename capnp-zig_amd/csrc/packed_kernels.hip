@@ -132,6 +132,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// a 64-bit value from lane `src` (two 32-bit shuffles, zero-extended halves: an int | u64 would
+// sign-extend the low half)
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, 64);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 
 // Wave scans on DPP: row_shr:1/2/4/8 inside each 16-lane row, then row_bcast:15 and
 // row_bcast:31 across rows (gfx9). A lane a step does not reach keeps `ident`. No LDS
@@ -478,6 +486,31 @@ __device__ __forceinline__ void encode_put(uint8_t* lds, const uint4 (&v)[5], ui
                 }
                 uint32_t w = 2 * c;
                 if (w < words) *reinterpret_cast<uint64_t*>(lds + (w >> 3) * kEncRow + (w & 7) * 8) = hi;
+            }
+        }
+    }
+}
+// encode_put for a payload that starts at framed word w0 (after a message's segment table): the
+// 16-B chunks land as two 8-B words each (w0 + word may be odd)
+__device__ __forceinline__ void encode_put_at(uint8_t* lds, const uint4 (&v)[5], uint32_t s, uint32_t words,
+                                              uint32_t lane, uint32_t w0) {
+    const uint32_t nch = (s + 8 * words + 15) >> 4;
+    auto put8 = [&](uint32_t w, uint64_t x) {
+        const uint32_t f = w0 + w;
+        *reinterpret_cast<uint64_t*>(lds + (f >> 3) * kEncRow + (f & 7) * 8) = x;
+    };
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = lane + 64 * k;
+        if ((uint32_t)(64 * k) < nch && c < nch) {
+            const uint64_t lo = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+            const uint64_t hi = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+            if (s == 0) {
+                put8(2 * c, lo);
+                if (2 * c + 1 < words) put8(2 * c + 1, hi);
+            } else {
+                if (c > 0) put8(2 * c - 1, lo);
+                if (2 * c < words) put8(2 * c, hi);
             }
         }
     }
@@ -1131,6 +1164,32 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
     const uint32_t words = hw + payload;
     if (words > kEncMaxWords) {
         if (lane == 0) status[msg] = kStNeedFull;
+        return;
+    }
+    // Segments laid end to end (each starts where the previous one ends, as a MessageBuilder's
+    // arena or a pool of one message's segments has them): the payload is one run, staged as
+    // encode_kernel stages a unit (coalesced 16-B loads), after the segment table's words, which
+    // lanes < hw compute from the segment lengths (toBytes 2147-2163). No map, no per-word search.
+    const uint64_t nptr = shfl_u64(ptr, min(lane + 1, 63u));
+    if (__builtin_amdgcn_ballot_w64(lane + 1 < count && ptr + len != nptr) == 0) {
+        const uint32_t ja = 2 * lane, jb = 2 * lane + 1;  // u32 entries of header word `lane`
+        const uint32_t sa = (uint32_t)__shfl((int)wl, (int)(ja == 0 ? 0u : min(ja - 1, 63u)), kWave);
+        const uint32_t sb = (uint32_t)__shfl((int)wl, (int)min(jb - 1, 63u), kWave);
+        const uint32_t ha = ja == 0 ? count - 1 : (ja <= count ? sa : 0u);
+        const uint32_t hb = jb <= count ? sb : 0u;
+        const uint8_t* const src = reinterpret_cast<const uint8_t*>(shfl_u64(ptr, 0));
+        uint4 v[5];
+        if (payload) encode_load(v, src, payload, lane);
+        if (lane < hw) *reinterpret_cast<uint64_t*>(lds + (lane >> 3) * kEncRow + (lane & 7) * 8) =
+            (uint64_t)ha | ((uint64_t)hb << 32);
+        if (payload) encode_put_at(lds, v, (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15), payload, lane, hw);
+        wave_lds_sync();
+        uint32_t cz = 0, cf = 0;
+        const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        if (lane == 0) {
+            out_len[msg] = P;
+            status[msg] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
+        }
         return;
     }
     if (lane < count) {
