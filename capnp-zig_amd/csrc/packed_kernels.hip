@@ -3842,8 +3842,9 @@ enum : uint32_t { SM_IDLE, SM_EXIT, SM_META, SM_FIRST, SM_RUN };
 // its unit's packed bytes in LDS (piece p at slot p % 4). A turn codes the records that
 // start in the lane's 32-B span [16k, 16k + 32) -- one record per loop pass on every lane,
 // predicated (no per-record branches: zero-run and literal-run records take the same path
-// as the others, a literal word as if it followed an FF tag) -- while pieces k + 4 and
-// k + 5 are in flight into registers; they enter the ring at the start of the next turn.
+// as the others, a literal word as if it followed an FF tag) -- while later pieces are in
+// flight into registers: every other turn the next four (64 B) are loaded at once, and they
+// enter the ring two at a time at the start of the next two turns.
 // A truncated record is UnexpectedEof with nothing more written.
 // Output (round 3): lanes write to different units, so a lane's own 16-B store is a memory
 // transaction of its own, and those scattered partial-line writes also slowed every kernel
@@ -3939,20 +3940,42 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
     };
     auto ld = [&](uint32_t i) { return *reinterpret_cast<const uint4*>(base + 16ull * min(i, np - 1)); };
 
+    // The metadata of the wave's next 64 list entries, one per lane (lane i: entry cb + i),
+    // loaded together when the cursor leaves the cached block: a lane taking a unit gets its
+    // offsets by shuffles in the same turn (no dependent load and no stall of the whole wave
+    // per new unit), and the four arrays' lines are read once, not once per taking lane.
+    uint64_t cb = first;  // wave-uniform
+    uint32_t c_unit = 0;
+    uint64_t c_off = 0, c_len = 0, c_oo = 0, c_cap = 0;
+    auto fill_cache = [&](uint64_t b) {
+        cb = b;
+        const uint64_t e = b + lane;
+        if (e < last) {
+            c_unit = list[e];
+            c_off = in_off[c_unit];
+            c_len = in_len[c_unit];
+            c_oo = out_off[c_unit];
+            c_cap = out_cap[c_unit];
+        }
+    };
+    if (first < last) fill_cache(first);
+    uint32_t cslot = 0;  // a SM_META lane's cache lane
     for (;;) {
         const uint64_t idle = __ballot(kind == SM_IDLE);
         if (idle) {
             if (cursor < last) {
+                if (cursor >= cb + kWave) fill_cache(cursor);  // wave-uniform
+                const uint64_t avail = min(last, cb + kWave) - cursor;  // cached entries from the cursor
+                const uint64_t rank = __popcll(idle & ((1ull << lane) - 1ull));
                 if (kind == SM_IDLE) {
-                    const uint64_t id = cursor + __popcll(idle & ((1ull << lane) - 1ull));
-                    if (id < last) {
-                        unit = list[id];
+                    if (rank < avail) {
+                        cslot = (uint32_t)(cursor - cb + rank);
                         kind = SM_META;
-                    } else {
+                    } else if (cursor + rank >= last) {
                         kind = SM_EXIT;
-                    }
+                    }  // else: a unit from the next block, next turn
                 }
-                cursor += __popcll(idle);
+                cursor += min((uint64_t)__popcll(idle), avail);
             } else if (kind == SM_IDLE) {
                 kind = SM_EXIT;
             }
@@ -3960,32 +3983,16 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
         if (__ballot(kind != SM_EXIT) == 0) break;
         // ---- this turn's reads (and last turn's pieces into the ring) -------------------
         uint64_t m_off = 0, m_len = 0, m_oo = 0, m_cap = 0;
-        if (kind == SM_META) {
-            m_off = in_off[unit];
-            m_len = in_len[unit];
-            m_oo = out_off[unit];
-            m_cap = out_cap[unit];
-        } else if (kind == SM_FIRST) {
-            d0 = ld(0);
-            d1 = ld(1);
-            d2 = ld(2);
-            d3 = ld(3);
-        } else if (kind == SM_RUN) {
-            uint4* const r4 = reinterpret_cast<uint4*>(ring);
-            if (k == 0) {
-                r4[0] = d0;
-                r4[1] = d1;
-                r4[2] = d2;
-                r4[3] = d3;
-            } else {
-                r4[(k + 2) & 3] = d0;
-                r4[(k + 3) & 3] = d1;
-            }
-            d0 = ld(k + 4);
-            d1 = ld(k + 5);
+        if (__ballot(kind == SM_META) != 0) {  // every lane shuffles (a taker reads its cache lane)
+            const uint32_t src_l = kind == SM_META ? cslot : lane;
+            const uint32_t u = (uint32_t)__shfl((int)c_unit, (int)src_l, kWave);
+            m_off = shfl_u64(c_off, src_l);
+            m_len = shfl_u64(c_len, src_l);
+            m_oo = shfl_u64(c_oo, src_l);
+            m_cap = shfl_u64(c_cap, src_l);
+            if (kind == SM_META) unit = u;
         }
-        // ---- decode -------------------------------------------------------------------------
-        bool act = kind == SM_RUN;  // the lanes that code this turn
+        // a new unit is set up from its metadata and issues its first loads in the same turn
         if (kind == SM_META) {
             const uint8_t* const src = in + m_off;
             const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
@@ -4004,7 +4011,39 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
             if (m_len == 0) finish(ST_OK);  // an empty unit writes nothing: any slot will do
             else if (reinterpret_cast<uintptr_t>(o) & 7) finish(ST_ARG);
             else kind = SM_FIRST;
-        } else if (kind == SM_FIRST) {
+        }
+        if (kind == SM_FIRST) {
+            d0 = ld(0);
+            d1 = ld(1);
+            d2 = ld(2);
+            d3 = ld(3);
+        } else if (kind == SM_RUN) {
+            // pieces k+2, k+3 enter the ring; every other turn (k = 0 mod 4) the next four
+            // pieces are loaded together (64 contiguous bytes: a line's half is fetched in one
+            // burst, not 16 B a turn while other lanes' traffic evicts it in between)
+            uint4* const r4 = reinterpret_cast<uint4*>(ring);
+            if (k == 0) {
+                r4[0] = d0;
+                r4[1] = d1;
+                r4[2] = d2;
+                r4[3] = d3;
+            } else if (k & 2) {
+                r4[(k + 2) & 3] = d0;
+                r4[(k + 3) & 3] = d1;
+            } else {
+                r4[(k + 2) & 3] = d2;
+                r4[(k + 3) & 3] = d3;
+            }
+            if ((k & 2) == 0) {
+                d0 = ld(k + 4);
+                d1 = ld(k + 5);
+                d2 = ld(k + 6);
+                d3 = ld(k + 7);
+            }
+        }
+        // ---- decode -------------------------------------------------------------------------
+        bool act = kind == SM_RUN;  // the lanes that code this turn
+        if (kind == SM_FIRST) {
             kind = SM_RUN;  // its first pieces enter the ring next turn
         }
         wave_lds_sync();  // the ring writes above are visible to the reads below
