@@ -1,19 +1,12 @@
 #!/usr/bin/env python3
-"""Dev: per-call kernel timeline of a rocprofv3 kernel trace (calls split at class_count_kernel)."""
+"""Dev-only: the last N cpk:: kernels of a rocprofv3 kernel trace as a timeline (start / end in
+us from the first of them, queue id, duration). Usage: timeline.py run_kernel_trace.csv [N]"""
 import csv, sys
-r = sorted(csv.DictReader(open(sys.argv[1])), key=lambda x: int(x['Start_Timestamp']))
-nm = lambda x: x['Kernel_Name'].split('(')[0].replace('void ', '')
-groups, cur = [], None
-for x in r:
-    if nm(x).startswith('cpk::class_count_kernel'):
-        cur = [x]; groups.append(cur)
-    elif cur is not None:
-        cur.append(x)
-for g in groups[-2:]:
-    t0 = int(g[0]['Start_Timestamp'])
-    print('----')
-    for x in g[:14]:
-        if not nm(x).startswith('cpk::'):
-            continue
-        s, e = int(x['Start_Timestamp']) - t0, int(x['End_Timestamp']) - t0
-        print(f"  {nm(x)[:44]:44s} {s/1e3:8.1f} .. {e/1e3:8.1f}  ({(e-s)/1e3:7.1f} us)")
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "cpk::" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+rows = rows[-int(sys.argv[2] if len(sys.argv) > 2 else 40):]
+t0 = int(rows[0]["Start_Timestamp"])
+for r in rows:
+    n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("cpk::", "")
+    s, e = (int(r["Start_Timestamp"]) - t0) / 1e3, (int(r["End_Timestamp"]) - t0) / 1e3
+    print(f"{n[:40]:40s} q{r['Queue_Id']:>3} {s:9.1f} {e:9.1f} {e - s:8.1f}")
