@@ -1372,10 +1372,43 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
     uint32_t* const woff = woff_all + wave * (kMsgMaxSegs + 1);
     uint64_t* const base = TILED ? base_all + wave * kMsgMaxSegs : nullptr;
     if (!TILED) {
+#ifdef CPK_X_EM2
+        // two messages per wave: both segment tables are loaded before the first is coded, so
+        // the second's dependent load level is hidden behind the first's coding
+        const uint32_t m0 = 2 * (blockIdx.x * kWavesPerBlock + wave), m1 = m0 + 1;
+        if (m0 >= n) return;
+        const bool two = m1 < n;
+        const uint32_t c0 = seg_count[m0], f0 = seg_first[m0];
+        const uint32_t c1 = two ? seg_count[m1] : 0u, f1 = two ? seg_first[m1] : 0u;
+        uint64_t len0 = 0, ptr0 = 0, len1 = 0, ptr1 = 0;
+        if (c0 && c0 <= kMsgOneSegs && lane < c0) {
+            len0 = seg_len[f0 + lane];
+            ptr0 = seg_ptr[f0 + lane];
+        }
+        if (two && c1 && c1 <= kMsgOneSegs && lane < c1) {
+            len1 = seg_len[f1 + lane];
+            ptr1 = seg_ptr[f1 + lane];
+        }
+        uint64_t ob0 = 0, cap0 = 0, ob1 = 0, cap1 = 0;
+        if (WRITE) {
+            ob0 = out_off[m0];
+            cap0 = out_cap[m0];
+            if (two) {
+                ob1 = out_off[m1];
+                cap1 = out_cap[m1];
+            }
+        }
+        encode_message_tile1_body<WRITE>(m0, lane, lut, lds, c0, len0, ptr0, ob0, cap0, out, out_len, status);
+        if (two) {
+            wave_lds_sync();  // m0's write-back read the slice
+            encode_message_tile1_body<WRITE>(m1, lane, lut, lds, c1, len1, ptr1, ob1, cap1, out, out_len, status);
+        }
+#else
         const uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
         if (msg < n)
             encode_message_tile1<WRITE>(msg, lane, lut, lds, seg_ptr, seg_len, seg_first, seg_count, out, out_off,
                                         out_cap, out_len, status);
+#endif
         return;
     }
     const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;
@@ -5165,6 +5198,11 @@ __global__ __launch_bounds__(256) void scan_apply_kernel(uint64_t* __restrict__ 
 namespace cpk {
 
 static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) / kWavesPerBlock; }
+#ifdef CPK_X_EM2
+#define EM_BLOCKS(n) blocks_for(((n) + 1) / 2)
+#else
+#define EM_BLOCKS(n) blocks_for(n)
+#endif
 // Grid of the long-list kernels (long_tiles_kernel, long_windows_kernel): at most 64 blocks
 // striding over the long list, so they start beside a persistent small-unit grid (a block per
 // 256 units of the batch waited ~0.2 ms for slots on config C5, delaying the long-unit chain).
@@ -5670,12 +5708,12 @@ hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_le
     // every message, then the marked multi-tile ones (a grid striding over the statuses)
     const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
     if (write) {
-        encode_message_kernel<true, false><<<blocks_for(n), kBlock, 0, stream>>>(
+        encode_message_kernel<true, false><<<EM_BLOCKS(n), kBlock, 0, stream>>>(
                 seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
         encode_message_kernel<true, true><<<tiled_blocks, kBlock, 0, stream>>>(
             seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
     } else {
-        encode_message_kernel<false, false><<<blocks_for(n), kBlock, 0, stream>>>(
+        encode_message_kernel<false, false><<<EM_BLOCKS(n), kBlock, 0, stream>>>(
                 seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
         encode_message_kernel<false, true><<<tiled_blocks, kBlock, 0, stream>>>(
             seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
