@@ -1209,31 +1209,6 @@ __device__ __forceinline__ void encode_message_tile1_body(uint32_t msg, uint32_t
     }
 }
 
-template <bool WRITE>
-__device__ __forceinline__ void encode_message_tile1(uint32_t msg, uint32_t lane, const uint64_t* lut, uint8_t* lds,
-                                                     const uint64_t* __restrict__ seg_ptr,
-                                                     const uint64_t* __restrict__ seg_len,
-                                                     const uint32_t* __restrict__ seg_first,
-                                                     const uint32_t* __restrict__ seg_count,
-                                                     uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
-                                                     const uint64_t* __restrict__ out_cap,
-                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
-    const uint32_t c_in = seg_count[msg];
-    const uint32_t first = seg_first[msg];
-    uint64_t len = 0, ptr = 0;
-    if (c_in && c_in <= kMsgOneSegs && lane < c_in) {
-        len = seg_len[first + lane];
-        ptr = seg_ptr[first + lane];
-    }
-    uint64_t ob = 0, cap = 0;
-    if (WRITE) {
-        ob = out_off[msg];
-        cap = out_cap[msg];
-    }
-    encode_message_tile1_body<WRITE>(msg, lane, lut, lds, c_in, len, ptr, ob, cap, out, out_len, status);
-}
-
-
 // One message (see encode_message_kernel); lds / woff / base are the wave's slices.
 template <bool WRITE, bool TILED>
 __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, const uint64_t* lut, uint8_t* lds,
@@ -1254,7 +1229,7 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
         if (lane == 0) { out_len[msg] = 0; status[msg] = ST_ARG; }
         return;
     }
-    static_assert(TILED, "one-tile messages: encode_message_tile1");
+    static_assert(TILED, "one-tile messages: encode_message_tile1_body");
     auto wput = [&](uint32_t s, uint32_t v) { woff[s] = v; };
     uint32_t wsum = 0;
     bool bad = false;
@@ -1343,8 +1318,9 @@ __device__ __forceinline__ void encode_message_one(uint32_t msg, uint32_t lane, 
     }
 }
 
-// TILED = false: every message; one framed tile (<= 512 words) of at most 64 segments is
-// encoded here (encode_message_tile1: offsets and addresses in the tile's row pads), other
+// TILED = false: every message, two per wave; one framed tile (<= 512 words) of at most 64
+// segments is encoded here (encode_message_tile1_body: segments end to end staged as one run,
+// else offsets and addresses in the tile's row pads and the pair gather), other
 // messages are marked for TILED = true, which keeps the offsets and addresses in LDS arrays,
 // applies the argument checks and walks the tiles.
 // The multi-tile pass strides over the batch with a small grid, 64 statuses per load.
@@ -1372,9 +1348,9 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
     uint32_t* const woff = woff_all + wave * (kMsgMaxSegs + 1);
     uint64_t* const base = TILED ? base_all + wave * kMsgMaxSegs : nullptr;
     if (!TILED) {
-#ifdef CPK_X_EM2
         // two messages per wave: both segment tables are loaded before the first is coded, so
-        // the second's dependent load level is hidden behind the first's coding
+        // the second's dependent load level (count / first -> lengths / addresses -> data) is
+        // hidden behind the first's coding
         const uint32_t m0 = 2 * (blockIdx.x * kWavesPerBlock + wave), m1 = m0 + 1;
         if (m0 >= n) return;
         const bool two = m1 < n;
@@ -1403,12 +1379,6 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
             wave_lds_sync();  // m0's write-back read the slice
             encode_message_tile1_body<WRITE>(m1, lane, lut, lds, c1, len1, ptr1, ob1, cap1, out, out_len, status);
         }
-#else
-        const uint32_t msg = blockIdx.x * kWavesPerBlock + wave;
-        if (msg < n)
-            encode_message_tile1<WRITE>(msg, lane, lut, lds, seg_ptr, seg_len, seg_first, seg_count, out, out_off,
-                                        out_cap, out_len, status);
-#endif
         return;
     }
     const uint32_t stride = gridDim.x * kWavesPerBlock * kWave;
@@ -2794,6 +2764,12 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         auto store16 = [&](uint32_t ent, uint64_t a, const u32x4& v, bool in_r) {
             const uint32_t flo = (ent >> 6) & 15u, fhi = ent >> 10;
             uint8_t* const p = reinterpret_cast<uint8_t*>(a) + 16 * j;
+            // every line of the group whole (all but a unit's first and last lines): one store
+            if (__builtin_amdgcn_ballot_w64(in_r && (flo | (fhi ^ 16u)) != 0u) == 0) {
+                ++younger;
+                if (in_r) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v));
+                return;
+            }
             const bool a0 = in_r && 2 * j >= flo && 2 * j < fhi, a1 = in_r && 2 * j + 1 >= flo && 2 * j + 1 < fhi;
             const bool both = a0 && a1, first = a0 && !a1, second = a1 && !a0;
             if (__builtin_amdgcn_ballot_w64(both) != 0) {
@@ -5198,11 +5174,7 @@ __global__ __launch_bounds__(256) void scan_apply_kernel(uint64_t* __restrict__ 
 namespace cpk {
 
 static inline uint32_t blocks_for(uint32_t n) { return (n + kWavesPerBlock - 1) / kWavesPerBlock; }
-#ifdef CPK_X_EM2
-#define EM_BLOCKS(n) blocks_for(((n) + 1) / 2)
-#else
-#define EM_BLOCKS(n) blocks_for(n)
-#endif
+
 // Grid of the long-list kernels (long_tiles_kernel, long_windows_kernel): at most 64 blocks
 // striding over the long list, so they start beside a persistent small-unit grid (a block per
 // 256 units of the batch waited ~0.2 ms for slots on config C5, delaying the long-unit chain).
@@ -5708,12 +5680,12 @@ hipError_t launch_encode_message(const uint64_t* seg_ptr, const uint64_t* seg_le
     // every message, then the marked multi-tile ones (a grid striding over the statuses)
     const uint32_t tiled_blocks = min(((n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock, 2048u);
     if (write) {
-        encode_message_kernel<true, false><<<EM_BLOCKS(n), kBlock, 0, stream>>>(
+        encode_message_kernel<true, false><<<blocks_for((n + 1) / 2), kBlock, 0, stream>>>(
                 seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
         encode_message_kernel<true, true><<<tiled_blocks, kBlock, 0, stream>>>(
             seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
     } else {
-        encode_message_kernel<false, false><<<EM_BLOCKS(n), kBlock, 0, stream>>>(
+        encode_message_kernel<false, false><<<blocks_for((n + 1) / 2), kBlock, 0, stream>>>(
                 seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
         encode_message_kernel<false, true><<<tiled_blocks, kBlock, 0, stream>>>(
             seg_ptr, seg_len, seg_first, seg_count, n, out, out_off, out_cap, out_len, status);
