@@ -2646,11 +2646,13 @@ constexpr uint32_t kLwWaves = 2;   // waves per block (a block shares one select
 constexpr uint32_t kLwCarry = 12;  // ring bytes kept from the previous round's block
 constexpr uint32_t kLwRing = kLwCarry + 64;  // 76 B per lane (an odd dword stride: fewer bank conflicts)
 constexpr uint32_t kLwS = 8;       // steps (words) per sub-round
-constexpr uint32_t kLwLine = 16;   // words per output line (128 B)
+constexpr uint32_t kLwLine = 16;             // words per output line (128 B; 64-B lines measured 2.57 ms vs 1.92)
+constexpr uint32_t kLwLB = 8 * kLwLine;      // line bytes
+constexpr uint32_t kLwLanes = kLwLB / 16;    // lanes per line in a flush store
 // LDS per 2-wave block: rings 9728 + lines 16384 + flush tables 256 + selector table 128 = 26496 B,
 // so six blocks (12 waves) fit a CU: the CU admits at most ~159.7 KB of them (census,
 // scripts/dev/lds_census.hip: 6 x 26624 B blocks resident, 6 x 27136 B not; 5 x 32768 B neither).
-constexpr uint32_t kLwLds = kLwWaves * kWave * (kLwRing + 128 + 2) + 128;
+constexpr uint32_t kLwLds = kLwWaves * kWave * (kLwRing + kLwLB + 2) + 128;
 static_assert(kLwLds <= 26624, "six blocks per CU");
 
 __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
@@ -2660,7 +2662,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count,
     const uint32_t* __restrict__ list_lo) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kLwWaves * kWave * kLwRing];
-    __shared__ __attribute__((aligned(16))) uint8_t line_blk[kLwWaves * kWave * 128];  // [lane][slot]
+    __shared__ __attribute__((aligned(16))) uint8_t line_blk[kLwWaves * kWave * kLwLB];  // [lane][slot]
     __shared__ uint16_t ftab_blk[kLwWaves * kWave];  // flush table: lane | lo << 6 | hi << 10, by rank
     // The v_perm selector of tag t (message.zig:134-141: bit k set -> output byte k takes the next
     // packed byte) from two reads of a 16-entry table: nibble n -> its 4 selector bytes (bit k set:
@@ -2678,8 +2680,8 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint32_t lane = lane_id();
     const uint32_t wave = threadIdx.x >> 6;
     uint8_t* const ring_all = ring_blk + wave * (kWave * kLwRing);
-    uint8_t* const lines = line_blk + wave * (kWave * 128);
-    uint8_t* const myline = lines + lane * 128;
+    uint8_t* const lines = line_blk + wave * (kWave * kLwLB);
+    uint8_t* const myline = lines + lane * kLwLB;
     uint16_t* const ftab = ftab_blk + wave * kWave;
     const uint32_t wv = blockIdx.x * kLwWaves + wave;
     const uint32_t lo = list_lo ? *list_lo : 0u;  // the list's entries [lo, *list_count)
@@ -2712,7 +2714,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     maxr = __builtin_amdgcn_readfirstlane(maxr);
     const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0x7FFFFFFFu);
     // output lines: word 0 of the unit sits in slot s0 of the 128-B line at line0
-    const uint32_t s0 = take ? (uint32_t)((reinterpret_cast<uintptr_t>(dstb) >> 3) & 15) : 0u;
+    const uint32_t s0 = take ? (uint32_t)((reinterpret_cast<uintptr_t>(dstb) >> 3) & (kLwLine - 1)) : 0u;
     const uint64_t line0 = reinterpret_cast<uint64_t>(dstb) - 8ull * s0;
 
     // ---- loads: instruction m, lane l moves piece l%4 of unit 16m + l/4's block ----------
@@ -2758,14 +2760,14 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         if (want) ftab[rk] = (uint16_t)(lane | (lo << 6) | (hi << 10));
         wave_lds_sync();
         const uint32_t Alo = (uint32_t)A, Ahi = (uint32_t)(A >> 32);
-        const uint32_t j = lane & 7;
+        const uint32_t j = lane & (kLwLanes - 1);
         // one pass stores two groups of eight lines; both groups' table, address and line reads
         // go out before either group's stores (the stores carry no memory clobber)
         auto store16 = [&](uint32_t ent, uint64_t a, const u32x4& v, bool in_r) {
             const uint32_t flo = (ent >> 6) & 15u, fhi = ent >> 10;
             uint8_t* const p = reinterpret_cast<uint8_t*>(a) + 16 * j;
             // every line of the group whole (all but a unit's first and last lines): one store
-            if (__builtin_amdgcn_ballot_w64(in_r && (flo | (fhi ^ 16u)) != 0u) == 0) {
+            if (__builtin_amdgcn_ballot_w64(in_r && (flo | (fhi ^ kLwLine)) != 0u) == 0) {
                 ++younger;
                 if (in_r) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v));
                 return;
@@ -2783,23 +2785,24 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                 if (first | second) asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(q), "v"(x));
             }
         };
-        for (uint32_t g = 0; g < cnt; g += 16) {  // wave-uniform
-            const uint32_t ra = g + lane / 8, rb = ra + 8;
+        constexpr uint32_t kGrp = kWave / kLwLanes;  // lines per store instruction
+        for (uint32_t g = 0; g < cnt; g += 2 * kGrp) {  // wave-uniform
+            const uint32_t ra = g + lane / kLwLanes, rb = ra + kGrp;
             const uint32_t ea = ftab[min(ra, cnt - 1)], eb = ftab[min(rb, cnt - 1)];
             const uint32_t ua = ea & 63u, ub = eb & 63u;
             const uint64_t aa = (uint64_t)(uint32_t)__shfl((int)Alo, (int)ua, kWave) |
                                 ((uint64_t)(uint32_t)__shfl((int)Ahi, (int)ua, kWave) << 32);
             const uint64_t ab = (uint64_t)(uint32_t)__shfl((int)Alo, (int)ub, kWave) |
                                 ((uint64_t)(uint32_t)__shfl((int)Ahi, (int)ub, kWave) << 32);
-            const u32x4 va = *reinterpret_cast<const u32x4*>(lines + ua * 128 + 16 * j);
-            const u32x4 vb = *reinterpret_cast<const u32x4*>(lines + ub * 128 + 16 * j);
+            const u32x4 va = *reinterpret_cast<const u32x4*>(lines + ua * kLwLB + 16 * j);
+            const u32x4 vb = *reinterpret_cast<const u32x4*>(lines + ub * kLwLB + 16 * j);
             store16(ea, aa, va, ra < cnt);
-            if (g + 8 < cnt) store16(eb, ab, vb, rb < cnt);
+            if (g + kGrp < cnt) store16(eb, ab, vb, rb < cnt);
         }
     };
     // the slots of line L a flush may store: the unit's own words (from s0 in line 0) below capw
     auto line_hi_cap = [&](uint32_t L, uint32_t hi) {
-        const int64_t c = (int64_t)capw + s0 - 16ll * L;  // slots of line L below word capw
+        const int64_t c = (int64_t)capw + s0 - (int64_t)kLwLine * L;  // slots of line L below word capw
         return (uint32_t)max<int64_t>(0, min<int64_t>(hi, c));
     };
 
@@ -2886,19 +2889,19 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                 w[j] = perm64(pay, (uint64_t)(uint32_t)elo | ((uint64_t)shi << 32));
             }
             // ---- into the unit's line; a line that fills is flushed, the rest follows ----
-            const uint32_t sl = (s0 + W) & 15u;  // first slot of this sub-round's words
+            const uint32_t sl = (s0 + W) & (kLwLine - 1);  // first slot of this sub-round's words
             const uint32_t f = kLwLine - sl;     // free slots of the current line
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j)
-                if (j < e && j < f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & 15u)) = w[j];
+                if (j < e && j < f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & (kLwLine - 1))) = w[j];
             const bool full = e >= f && e != 0u;
             if (__builtin_amdgcn_ballot_w64(full) != 0) {
-                const uint32_t L = (s0 + W) >> 4;
-                flush(full, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, 16u));
+                const uint32_t L = (s0 + W) / kLwLine;
+                flush(full, line0 + (uint64_t)kLwLB * L, L == 0 ? s0 : 0u, line_hi_cap(L, kLwLine));
                 wave_lds_sync();  // the flush's line reads come before the next line's words
 #pragma unroll
                 for (uint32_t j = 0; j < kLwS; ++j)
-                    if (j < e && j >= f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & 15u)) = w[j];
+                    if (j < e && j >= f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & (kLwLine - 1))) = w[j];
             }
             W += e;
             if (__builtin_amdgcn_ballot_w64(apos < lim) == 0) break;
@@ -2906,9 +2909,9 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     }
     // the unit's last line, in part (a full last line went out when it filled)
     {
-        const uint32_t L = (s0 + W) >> 4, hi = (s0 + W) & 15u;
+        const uint32_t L = (s0 + W) / kLwLine, hi = (s0 + W) & (kLwLine - 1);
         const bool part = take && hi != 0u;
-        flush(part, line0 + 128ull * L, L == 0 ? s0 : 0u, line_hi_cap(L, hi));
+        flush(part, line0 + (uint64_t)kLwLB * L, L == 0 ? s0 : 0u, line_hi_cap(L, hi));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!valid) return;
