@@ -2955,6 +2955,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
 // similar length in lockstep; the mid list is the bins in order (batch order within a bin), and
 // q[20] is the two-pass decoder's share of it (class_scan_kernel).
 enum : uint32_t { CL_LONG = 0, CL_HUGE = 1, CL_SMALL = 2, CL_MID = 3, CL_MID_BINS = 8 };
+constexpr uint32_t kEsBinsQ = 4;  // encode's small-unit bins (mid-list bins 4 .. 7, kEsBins)
 constexpr uint64_t kSmEncWords = 64;  // encode: units of at most 64 words are small
 constexpr uint64_t kSmDecP = 512;     // decode: small = at most 512 packed bytes ...
 constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
@@ -3090,6 +3091,24 @@ __global__ __launch_bounds__(kClassBlock) void class_scatter_kernel(const uint8_
     if (c >= kClassK) return;
     uint32_t idx = q_blocks(q, n)[blockIdx.x * kClassK + c] + rank;
     for (uint32_t j = 0; j < w; ++j) idx += wcnt[j][c];
+    if (KIND == 4 && c >= CL_MID + CL_MID_BINS - kEsBinsQ) {
+        // encode's small units ordered by (class block, length bin) instead of (bin, batch order):
+        // a unit's neighbours in memory (other bins) are then coded by waves of the same block,
+        // at about the same time, so the lines they share are read once
+        const uint32_t* const P = q_blocks(q, n);  // exclusive prefixes over blocks, per class
+        const uint32_t nb = gridDim.x;
+        uint32_t before = 0;  // small units of earlier blocks, and of lower bins in this block
+        for (uint32_t cc = CL_MID + CL_MID_BINS - kEsBinsQ; cc < CL_MID + CL_MID_BINS; ++cc) {
+            const uint32_t b = cc - CL_MID;
+            const uint32_t tot = (b + 1 < CL_MID_BINS ? q[12 + b] : q[4]) - q[11 + b];
+            const uint32_t pb = P[blockIdx.x * kClassK + cc];
+            const uint32_t pn = blockIdx.x + 1 < nb ? P[(blockIdx.x + 1) * kClassK + cc] : tot;
+            before += pb + (cc < c ? pn - pb : 0u);
+        }
+        idx = before + (idx - P[blockIdx.x * kClassK + c]);
+        q[kQHead + 2ull * n + q[11 + CL_MID_BINS - kEsBinsQ] + idx] = u;
+        return;
+    }
     if (c == CL_LONG) q[kQHead + idx] = u;
     else if (c == CL_HUGE) q[kQHead + n - 1 - idx] = u;
     else if (c == CL_SMALL) q[kQHead + 1ull * n + idx] = u;
