@@ -2354,14 +2354,14 @@ struct FillMeta {
 // Word of a code (see kFlLit): 16 bytes around its position from the staged
 // pieces, then the tag's v_perm selector (literal words: the identity).
 __device__ __forceinline__ uint64_t fill_word(const uint8_t* pk, const uint64_t* lut, uint32_t code) {
+    if (code == kFlZero) return 0ull;  // a zero word: its lanes issue no LDS reads (p = 0.9: -1%)
     const uint32_t q = code & kFlPos;
     const uint32_t a = q & ~7u, sh = 8u * (q & 7u);
     const uint64_t lo = *reinterpret_cast<const uint64_t*>(pk + a);
     const uint64_t hi = *reinterpret_cast<const uint64_t*>(pk + a + 8);
     const uint32_t t = (code & kFlLit) ? 0xFFu : (uint32_t)(lo >> sh) & 0xFFu;
     const uint64_t pay = ((lo >> sh) >> 8) | (hi << (56u - sh));  // bytes q+1 .. q+8
-    const uint64_t w = perm64(pay, lut[t]);
-    return code == kFlZero ? 0ull : w;
+    return perm64(pay, lut[t]);
 }
 
 // FF run bodies of a code pass (message.zig:112-128): the code walk writes only each
