@@ -547,16 +547,17 @@ __device__ __forceinline__ void encode_lookahead(const uint8_t* src, uint32_t nw
 // indices; tb = 0 for a single tile). SINGLE: the whole unit (no carries; run
 // crossings are tested per lane boundary). Returns the tile's packed size; writes
 // the packed bytes to dst when WRITE and they fit in `room`.
-template <bool WRITE, bool SINGLE>
+template <bool WRITE, bool SINGLE, bool FULL = false>
 __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lut, uint32_t lane, uint32_t words,
                                                 uint32_t tb, uint32_t& cz_c, uint32_t& cf_c, uint32_t nbz,
                                                 uint32_t nbf, uint8_t* dst, uint64_t room) {
     const uint32_t wend = tb + words;  // absolute end of the tile
     // ---- lane j owns words [tb + 8j, tb + 8j + 8) --------------------------------
     const uint32_t base = tb + lane * 8;
-    const uint32_t nw = lane * 8 < words ? min(8u, words - lane * 8) : 0u;
+    // FULL: a 512-word tile, every lane owns 8 words (the per-word range tests fold away)
+    const uint32_t nw = FULL ? 8u : (lane * 8 < words ? min(8u, words - lane * 8) : 0u);
     uint64_t w[8];
-    if (nw) {
+    if (FULL || nw) {
         const uint4* row = reinterpret_cast<const uint4*>(lds + lane * kEncRow);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -574,21 +575,22 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         tag[t] = nonzero_tag(w[t]);
-        if ((uint32_t)t < nw) {
-            if (tag[t] == 0) zmask |= 1u << t;
-            if (tag[t] == 0xFF) fmask |= 1u << t;
-        }
+        const bool in = FULL || (uint32_t)t < nw;  // selects, not branches: the per-word
+        zmask |= (in && tag[t] == 0) ? 1u << t : 0u;     // logic stays off the exec mask
+        fmask |= (in && tag[t] == 0xFF) ? 1u << t : 0u;
     }
     // break positions for the zero-run (Z) and literal-run (F) classes: last break + 1
     // (seeded with the carried run start) and first break (seeded with the lookahead)
     uint32_t lbz = cz_c, lbf = cf_c, fbz = nbz, fbf = nbf;
 #pragma unroll
     for (int t = 7; t >= 0; --t) {
-        uint32_t i = base + t;
-        if ((uint32_t)t < nw) {
-            if (!((zmask >> t) & 1u)) { lbz = max(lbz, i + 1); fbz = i; }
-            if (!((fmask >> t) & 1u)) { lbf = max(lbf, i + 1); fbf = i; }
-        }
+        const uint32_t i = base + t;
+        const bool in = FULL || (uint32_t)t < nw;
+        const bool bz = in && !((zmask >> t) & 1u), bf = in && !((fmask >> t) & 1u);
+        lbz = bz ? max(lbz, i + 1) : lbz;
+        fbz = bz ? i : fbz;
+        lbf = bf ? max(lbf, i + 1) : lbf;
+        fbf = bf ? i : fbf;
     }
     // run start carried into this lane = last break before it (+1); run end = first break after it.
     // In a single tile where no zero run and no literal run crosses a lane boundary (the
@@ -629,10 +631,9 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
     for (int t = 7; t >= 0; --t) {
         uint32_t i = base + t;
         re[t] = ((zmask >> t) & 1u) ? ez : ef;
-        if ((uint32_t)t < nw) {
-            if (!((zmask >> t) & 1u)) ez = i;
-            if (!((fmask >> t) & 1u)) ef = i;
-        }
+        const bool in = FULL || (uint32_t)t < nw;
+        ez = (in && !((zmask >> t) & 1u)) ? i : ez;
+        ef = (in && !((fmask >> t) & 1u)) ? i : ef;
     }
     uint32_t sz[8], cnt[8];
     uint32_t total = 0;
@@ -641,11 +642,9 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
         uint32_t i = base + t;
         uint32_t head = ((i - rs[t]) & 255u) == 0;
         cnt[t] = min(256u, re[t] - i) - 1;  // message.zig:214-223 / 236-245
-        uint32_t s;
-        if ((uint32_t)t >= nw) s = 0;
-        else if ((zmask >> t) & 1u) s = head ? 2 : 0;
-        else if ((fmask >> t) & 1u) s = head ? 10 : 8;
-        else s = 1 + __popc(tag[t]);
+        const uint32_t h2 = head ? 2u : 0u;
+        uint32_t s = ((zmask >> t) & 1u) ? h2 : (((fmask >> t) & 1u) ? 8u + h2 : 1u + __popc(tag[t]));
+        if (!FULL) s = (uint32_t)t < nw ? s : 0u;
         sz[t] = s;
         total += s;
     }
@@ -668,29 +667,36 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
     wave_lds_sync();
     {
         // Each record (<= 10 bytes) is OR-ed into the zeroed buffer as two (FF heads:
-        // three) aligned u64 pieces: no per-byte shifting state, no branches.
-        uint32_t x = so + o;
+        // three) aligned u64 pieces: no per-byte shifting state, no branches. A word with
+        // no bytes (a zero run's body, a word past the tile) ORs zeros; every address stays
+        // inside the slice (P <= 9 bytes per word: at most ~4.6 KB of the 5 KB).
+        const uint32_t x0 = so + o;
+        uint32_t x = x0, ex = 0;  // ex bit t: an FF head whose count byte opens a third u64
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            uint64_t lo, hi = 0;
-            if ((zmask >> t) & 1u) {
-                lo = (uint64_t)cnt[t] << 8;                                  // 00 <count>
-            } else if ((fmask >> t) & 1u) {
-                const bool head = sz[t] == 10;                               // FF w0..w7 <count>
-                lo = head ? (0xFFULL | (w[t] << 8)) : w[t];                  // or literal run body
-                hi = head ? ((w[t] >> 56) | ((uint64_t)cnt[t] << 8)) : 0;
-            } else {
-                lo = (uint64_t)tag[t] | (perm64(w[t], lut[tag[t]]) << 8);    // tag + nonzero bytes
-            }
-            if (sz[t]) {
-                const uint32_t a = x & ~7u, sh = (x & 7u) * 8u;
-                atomicOr(reinterpret_cast<unsigned long long*>(lds + a), (unsigned long long)(lo << sh));
-                atomicOr(reinterpret_cast<unsigned long long*>(lds + a + 8),
-                         (unsigned long long)(((lo >> 1) >> (63u - sh)) | (hi << sh)));
-                if (sh == 56 && (hi >> 8))
-                    atomicOr(reinterpret_cast<unsigned long long*>(lds + a + 16), (unsigned long long)(hi >> 8));
-            }
+            const bool head = sz[t] == 10u;                                     // FF w0..w7 <count>
+            const uint64_t mixed = (uint64_t)tag[t] | (perm64(w[t], lut[tag[t]]) << 8);  // tag + nonzero bytes
+            const uint64_t lit = head ? (0xFFULL | (w[t] << 8)) : w[t];          // or literal run body
+            uint64_t lo = ((zmask >> t) & 1u) ? ((uint64_t)cnt[t] << 8)         // 00 <count>
+                                              : (((fmask >> t) & 1u) ? lit : mixed);
+            lo = sz[t] ? lo : 0ull;
+            const uint64_t hi = head ? ((w[t] >> 56) | ((uint64_t)cnt[t] << 8)) : 0ull;
+            const uint32_t a = x & ~7u, sh = (x & 7u) * 8u;
+            atomicOr(reinterpret_cast<unsigned long long*>(lds + a), (unsigned long long)(lo << sh));
+            atomicOr(reinterpret_cast<unsigned long long*>(lds + a + 8),
+                     (unsigned long long)(((lo >> 1) >> (63u - sh)) | (hi << sh)));
+            ex |= (sh == 56 && (hi >> 8)) ? 1u << t : 0u;
             x += sz[t];
+        }
+        if (__builtin_amdgcn_ballot_w64(ex != 0) != 0) {  // rare (FF heads at byte 7 of a u64)
+            x = x0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                if ((ex >> t) & 1u)
+                    atomicOr(reinterpret_cast<unsigned long long*>(lds + (x & ~7u) + 16),
+                             (unsigned long long)(((w[t] >> 56) | ((uint64_t)cnt[t] << 8)) >> 8));
+                x += sz[t];
+            }
         }
     }
     wave_lds_sync();
@@ -763,7 +769,9 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
         encode_stage(lds, src, words, lane);
         wave_lds_sync();
         uint32_t cz = 0, cf = 0;
-        const uint32_t P = encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        const uint32_t P = words == kEncMaxWords
+                               ? encode_tile<WRITE, true, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap)
+                               : encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
         if (lane == 0) {
             out_len[unit] = P;
             status[unit] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
