@@ -206,14 +206,12 @@ __device__ __forceinline__ uint32_t fu_prev_lane(uint32_t v) {
     return r;
 }
 
-// inclusive min over lanes >= this lane
-__device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_down(v, d, kWave);
-        if (lane + d < (uint32_t)kWave) v = min(v, t);
-    }
-    return v;
+// v of the first lane above this one with `has` set, or `none` (encode_tile's run ends)
+__device__ __forceinline__ uint32_t next_break(bool has, uint32_t v, uint32_t lane, uint32_t none) {
+    const uint64_t above = (__builtin_amdgcn_ballot_w64(has) >> lane) >> 1;  // lanes > this one
+    const uint32_t src = above ? lane + 1u + (uint32_t)__builtin_ctzll(above) : lane;
+    const uint32_t r = (uint32_t)__shfl((int)v, (int)src, kWave);
+    return above ? r : none;
 }
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
@@ -227,7 +225,12 @@ __device__ __forceinline__ uint32_t nonzero_tag32(uint32_t x) {
     return ((y & 0x80808080u) * 0x00204081u) >> 28;        // gather the 4 high bits
 }
 __device__ __forceinline__ uint32_t nonzero_tag(uint64_t w) {
-    return nonzero_tag32((uint32_t)w) | (nonzero_tag32((uint32_t)(w >> 32)) << 4);
+    // byte k of c: bit 0 = byte k nonzero, bit 4 = byte k + 4 nonzero; the dot product with
+    // 2^k gathers them (one full-rate v_dot4 instead of two quarter-rate multiplies)
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t yl = ((lo & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | lo, yh = ((hi & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | hi;
+    const uint32_t c = ((yl >> 7) & 0x01010101u) | ((yh >> 3) & 0x10101010u);
+    return __builtin_amdgcn_udot4(c, 0x08040201u, 0u, false);
 }
 
 // v_perm_b32 over the 8 bytes of d: selector byte r in 0..7 picks byte r, 0x0C gives 0.
@@ -265,7 +268,9 @@ constexpr SelLut make_sel_lut(bool expand) {
 }
 __device__ constexpr SelLut kCompactLut = make_sel_lut(false);
 __device__ constexpr SelLut kExpandLut = make_sel_lut(true);
-__device__ __forceinline__ uint64_t compact_selector(uint32_t t) { return kCompactLut.v[t]; }
+// The compact selector moved up one byte (byte 0 selects a zero byte): perm64(w, it) is the
+// tag's record payload at bytes 1..popc, ready to OR with the tag (encode_tile).
+__device__ __forceinline__ uint64_t compact_selector(uint32_t t) { return (kCompactLut.v[t] << 8) | 0x0Cull; }
 __device__ __forceinline__ uint64_t expand_selector(uint32_t t) { return kExpandLut.v[t]; }
 
 // Unaligned 8-byte read from an LDS byte array (two aligned ds_read_b64 + funnel).
@@ -606,10 +611,12 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
     if (scan) {
         cz = wave_prev_lane(wave_incl_max(lbz, lane), 0u);
         cf = wave_prev_lane(wave_incl_max(lbf, lane), 0u);
-        ez = __shfl_down(wave_incl_suffix_min(fbz, lane), 1, kWave);
-        ef = __shfl_down(wave_incl_suffix_min(fbf, lane), 1, kWave);
+        // run end: the first break of the next lane that holds one (a lane's fb is its first
+        // break, or the lookahead, which lies past every break of the tile): a ballot and one
+        // shuffle instead of a six-step suffix-min scan
+        ez = next_break(fbz != nbz, fbz, lane, nbz);
+        ef = next_break(fbf != nbf, fbf, lane, nbf);
         if (lane == 0) { cz = cz_c; cf = cf_c; }
-        if (lane == 63) { ez = nbz; ef = nbf; }
     }
     // carries for the next tile: the run starts open at the tile end
     uint32_t lz_all = 0, lf_all = 0;
@@ -642,8 +649,9 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
         uint32_t i = base + t;
         uint32_t head = ((i - rs[t]) & 255u) == 0;
         cnt[t] = min(256u, re[t] - i) - 1;  // message.zig:214-223 / 236-245
-        const uint32_t h2 = head ? 2u : 0u;
-        uint32_t s = ((zmask >> t) & 1u) ? h2 : (((fmask >> t) & 1u) ? 8u + h2 : 1u + __popc(tag[t]));
+        // 00: 2 bytes at a head, else 0; FF: 10 / 8; other tags: 1 + popc (zero / FF words
+        // are exclusive, popc 0 / 8)
+        uint32_t s = __popc(tag[t]) + (((zmask | fmask) >> t) & 1u ? (head ? 2u : 0u) : 1u);
         if (!FULL) s = (uint32_t)t < nw ? s : 0u;
         sz[t] = s;
         total += s;
@@ -674,11 +682,14 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
         uint32_t x = x0, ex = 0;  // ex bit t: an FF head whose count byte opens a third u64
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            const bool head = sz[t] == 10u;                                     // FF w0..w7 <count>
-            const uint64_t mixed = (uint64_t)tag[t] | (perm64(w[t], lut[tag[t]]) << 8);  // tag + nonzero bytes
-            const uint64_t lit = head ? (0xFFULL | (w[t] << 8)) : w[t];          // or literal run body
-            uint64_t lo = ((zmask >> t) & 1u) ? ((uint64_t)cnt[t] << 8)         // 00 <count>
-                                              : (((fmask >> t) & 1u) ? lit : mixed);
+            // tag + nonzero bytes (00: just the tag; FF: the tag and bytes 0..6 of an FF head)
+            uint64_t sel = lut[tag[t]];
+            asm volatile("" : "+v"(sel));  // read for every word: the selects below stay branch-free
+            const uint64_t rec = (uint64_t)tag[t] | perm64(w[t], sel);
+            const bool zt = (zmask >> t) & 1u, head = sz[t] == 10u;  // head: FF w0..w7 <count>
+            const bool body = ((fmask >> t) & 1u) && !head;          // a literal run's body word
+            uint64_t lo = rec | ((uint64_t)(zt ? cnt[t] : 0u) << 8);    // 00 <count>
+            lo = body ? w[t] : lo;
             lo = sz[t] ? lo : 0ull;
             const uint64_t hi = head ? ((w[t] >> 56) | ((uint64_t)cnt[t] << 8)) : 0ull;
             const uint32_t a = x & ~7u, sh = (x & 7u) * 8u;
@@ -3802,7 +3813,7 @@ __global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
         const bool nzr = vw && !cz && !cf && isz;
         const bool nfr = vw && !cz && !cf && isf;
         const bool mx = vw && !isz && !isf;
-        const uint64_t v = cf ? w : (nfr ? (0xFFull | (w << 8)) : ((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) << 8 : 0ull)));
+        const uint64_t v = cf ? w : (nfr ? (0xFFull | (w << 8)) : ((uint64_t)tg | (WRITE ? perm64(w, lut[tg]) : 0ull)));
         app(cf || nfr || mx, v, (cf || nfr) ? 8u : 1u + __popc(tg));
         app(nfr, w >> 56, 2);  // w7, then the count byte (0 until patched)
         cpos = nfr ? op - 1 : cpos;
