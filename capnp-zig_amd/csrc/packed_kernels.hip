@@ -680,6 +680,9 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
         // inside the slice (P <= 9 bytes per word: at most ~4.6 KB of the 5 KB).
         const uint32_t x0 = so + o;
         uint32_t x = x0, ex = 0;  // ex bit t: an FF head whose count byte opens a third u64
+        // lanes past a short unit's words skip the ORs (one branch per lane, not per word:
+        // C5's mid units leave most lanes of a wave without words)
+        if (FULL || nw != 0)
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             // tag + nonzero bytes (00: just the tag; FF: the tag and bytes 0..6 of an FF head)
