@@ -555,14 +555,23 @@ __device__ __forceinline__ void encode_lookahead(const uint8_t* src, uint32_t nw
 template <bool WRITE, bool SINGLE, bool FULL = false>
 __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lut, uint32_t lane, uint32_t words,
                                                 uint32_t tb, uint32_t& cz_c, uint32_t& cf_c, uint32_t nbz,
-                                                uint32_t nbf, uint8_t* dst, uint64_t room) {
+                                                uint32_t nbf, uint8_t* dst, uint64_t room,
+                                                const uint8_t* direct = nullptr) {
     const uint32_t wend = tb + words;  // absolute end of the tile
     // ---- lane j owns words [tb + 8j, tb + 8j + 8) --------------------------------
     const uint32_t base = tb + lane * 8;
     // FULL: a 512-word tile, every lane owns 8 words (the per-word range tests fold away)
     const uint32_t nw = FULL ? 8u : (lane * 8 < words ? min(8u, words - lane * 8) : 0u);
     uint64_t w[8];
-    if (FULL || nw) {
+    if (FULL && direct) {  // a 16-B aligned full tile: the lane's 64 B straight from memory
+        const uint4* row = reinterpret_cast<const uint4*>(direct + 64 * lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 r = row[q];
+            w[2 * q] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+            w[2 * q + 1] = (uint64_t)r.z | ((uint64_t)r.w << 32);
+        }
+    } else if (FULL || nw) {
         const uint4* row = reinterpret_cast<const uint4*>(lds + lane * kEncRow);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -779,13 +788,14 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
     }
     const uint32_t words = (uint32_t)(nbytes >> 3);
     if (words <= kEncMaxWords) {  // one tile (the headline 4-KiB units)
+        const bool direct = words == kEncMaxWords && !(reinterpret_cast<uintptr_t>(src) & 15);
         wave_lds_sync();          // the previous unit's write-back read the slice
-        encode_stage(lds, src, words, lane);
+        if (!direct) encode_stage(lds, src, words, lane);
         wave_lds_sync();
         uint32_t cz = 0, cf = 0;
-        const uint32_t P = words == kEncMaxWords
-                               ? encode_tile<WRITE, true, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap)
-                               : encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
+        const uint32_t P = direct ? encode_tile<WRITE, true, true>(lds, lut, lane, words, 0, cz, cf, words, words,
+                                                                   out + ob, cap, src)
+                                  : encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
         if (lane == 0) {
             out_len[unit] = P;
             status[unit] = (WRITE && (uint64_t)P > cap) ? ST_SPACE : ST_OK;
