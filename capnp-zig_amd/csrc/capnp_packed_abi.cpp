@@ -743,14 +743,20 @@ struct capnp_packed_framer {
         }
     } pin_state, pin_tab, pin_units, pin_jobs;
     uint64_t uploaded = 0, moved = 0;  // bytes copied H2D (new reads) and moved between regions
+    int dev = -1;                      // the device the session was created on
     static constexpr uint32_t kWalkMessages = 64;  // messages a walk pass finds per connection
 
     ~capnp_packed_framer() {
+        // the session's device is current for the teardown, whatever device the caller has
+        // current now (the library's stream contexts are keyed by device and stream)
+        int cur = -1;
+        const bool switched = dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev &&
+                              hipSetDevice(dev) == hipSuccess;
         if (s) {
             (void)hipStreamSynchronize(s);
             // the decode passes ran on s: drop the library's context of it (side stream, events,
             // class queue), or every session ever created would keep one
-            (void)cpk::release_stream(s);
+            (void)cpk::release_stream(s, dev);
         }
         if (arena) (void)hipFree(arena);
         if (d_state) (void)hipFree(d_state);
@@ -761,6 +767,7 @@ struct capnp_packed_framer {
         if (d_units) (void)hipFree(d_units);
         if (h_stage) (void)hipHostFree(h_stage);
         if (s) (void)hipStreamDestroy(s);
+        if (switched) (void)hipSetDevice(cur);
     }
     static int grow(uint8_t** p, uint64_t* c, uint64_t need) {
         if (*p && need <= *c) return CAPNP_PACKED_OK;
@@ -886,6 +893,7 @@ int capnp_packed_framer_create(uint32_t n_conns, capnp_packed_framer** out) {
     capnp_packed_framer* f = new (std::nothrow) capnp_packed_framer();
     if (!f) return fail(CAPNP_PACKED_OUT_OF_SPACE, "framer allocation");
     f->n = n_conns;
+    if (hipGetDevice(&f->dev) != hipSuccess) f->dev = -1;
     for (auto* v : {&f->off, &f->cap, &f->m0, &f->len, &f->need, &f->X, &f->W}) v->assign(n_conns, 0);
     hipError_t e = hipStreamCreateWithFlags(&f->s, hipStreamNonBlocking);
     if (e != hipSuccess) {

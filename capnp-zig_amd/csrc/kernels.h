@@ -22,10 +22,10 @@ size_t queue_bytes(uint32_t n);
 
 // capnp_packed_set_decoder: returns the previous setting
 int set_decoder(int decoder);
-bool decoder_built(int decoder);  // the fused / streaming decoders exist in dev builds only
+bool decoder_built(int decoder);  // AUTO, TWO_PASS, WORDS (FUSED / STREAM removed in round 5)
 int set_all_or_nothing(int on);
 uint32_t set_launch_flags(uint32_t flags);
-hipError_t release_stream(hipStream_t stream);
+hipError_t release_stream(hipStream_t stream, int dev = -1);  // dev -1: the current device
 void stream_queue_info(hipStream_t stream, size_t* bytes, uint32_t* kept);
 uint32_t stream_context_count();  // caller streams with a library context (current device)
 

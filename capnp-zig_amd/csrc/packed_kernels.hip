@@ -96,6 +96,8 @@ enum : int32_t {
 constexpr int32_t kStNeedFull = 0x7FFF0001;
 constexpr int32_t kStNeedWalk = 0x7FFF0002;  // read-message: the one-pass walk could not take the unit
 constexpr int32_t kStNeedGate = 0x7FFF0003;  // read-message: walked (consumed known), records next
+constexpr int32_t kStWords = 0x7FFF0005;     // read-message: the words decoder's (read_header_kernel)
+constexpr uint64_t kRdWordsMax = 1024;       // read-message: framed words the words decoder takes
 // status of a long unit between its listing and its worker's result
 constexpr int32_t kStPending = CAPNP_PACKED_DEVICE_ERROR;
 
@@ -1892,7 +1894,8 @@ __device__ __forceinline__ void wv_expand(const uint8_t* pk, uint8_t* mk, const 
     }
 }
 
-// SEL: kWvMarked the units a first pass marked kStNeedFull (the read-message passes);
+// SEL: kWvMarked the units a first pass marked kStNeedFull (the read-message passes, the words
+// decoder's units stopped at their capacity; q, when given, counts them: 0 returns at once);
 // kWvLong the long units the window table could not hold (the serial list that
 // long_windows_kernel fills), one after another.
 constexpr int kWvMarked = 1, kWvLong = 2;
@@ -1910,6 +1913,7 @@ __global__ __launch_bounds__(kWvBlock) void decode_wave_kernel(const uint8_t* __
     __shared__ __attribute__((aligned(16))) uint8_t mk_all[kWvWaves * kWvWin];
     __shared__ uint64_t lut[256];  // tag -> v_perm selector that scatters the packed bytes (FF: identity, 00: zero)
     constexpr bool CK = SEL == kWvMarked;
+    if (CK && q && *q == 0) return;  // kWvMarked with a count of marked units: none
     const bool QD = SEL == kWvLong;
     if (QD && q[5] == 0) return;  // no serial units (block-uniform)
     lut[threadIdx.x] = expand_selector(threadIdx.x);
@@ -2068,17 +2072,15 @@ __device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 //
 // RD selects the Reader.readPackedMessage passes (reader.zig:84-156; launch_read_message):
 //   kRdNone  unpackPacked / estimateUnpackedSize as above;
-//   kRdOne   (round 3) the write pass of a whole read in one walk: records and the framed-length
-//            stop together (the bytes a message can take are bounded by 10 per word, so a
-//            stream of any length is walked only that far); a unit whose bound does not fit
-//            the fill pass is left kStNeedWalk for the two passes below;
 //   kRdWalk  size-only walk of the kStNeedWalk units that stops at the first record boundary
 //            where the decoded words reach out_len[unit] / 8 (the framed length
 //            read_header_kernel derived) and writes the bytes it took to consumed[unit]
 //            (status kStNeedGate when it reached the framed length exactly);
 //   kRdGate  the write pass over in_len = consumed of the kStNeedGate units.
+// These take the messages of more than kRdWordsMax framed words; the words decoder takes the
+// rest (round 6; round 3's one-walk write pass, kRdOne, was removed with it).
 // A unit's status on entry says which pass owns it, so no pass redoes another's work.
-constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2, kRdOne = 3;
+constexpr int kRdNone = 0, kRdWalk = 1, kRdGate = 2;
 
 constexpr uint32_t kIxBw = 1;  // waves per block of the index pass (each wave owns 64 units)
 // blocks of the index pass for a batch of n units
@@ -2094,8 +2096,7 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
     const uint32_t* __restrict__ list_count = nullptr, uint8_t* __restrict__ rec = nullptr) {
     static_assert(RD != kRdWalk || SIZE_ONLY, "the read walk writes no output");
     static_assert(RD != kRdGate || !SIZE_ONLY, "the gated pass is the write pass");
-    static_assert(RD != kRdOne || !SIZE_ONLY, "the one-pass read writes records");
-    constexpr bool kStop = RD == kRdWalk || RD == kRdOne;  // the walk stops at the framed length
+    constexpr bool kStop = RD == kRdWalk;  // the walk stops at the framed length
     constexpr uint32_t kRing = 80;  // [0, 16): block k-1's last piece, [16, 80): block k
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kIxBw * kWave * kRing];
     uint8_t* const ring_all = ring_blk + (threadIdx.x >> 6) * (kWave * kRing);  // this wave's
@@ -2125,10 +2126,6 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
             // a message of <= 8 Mi + 257 words takes < 2^31 packed bytes (<= 10 B per word),
             // so the walk always stops before this clamp
             if (P64 > kIxSizeMax - 1) P64 = kIxSizeMax - 1;
-            // kRdOne: the message's bytes are within 10 per framed word (FF record: 10 bytes for
-            // its first word, 8 per literal word; others fewer), so the stream past that is
-            // never walked
-            if (RD == kRdOne && P64 > 10 * lim_w) P64 = 10 * lim_w;
         }
         if (!SIZE_ONLY) {
             dstb = out + out_off[unit];
@@ -2144,7 +2141,7 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
         const bool fits = SIZE_ONLY ? P64 < kIxSizeMax : (np <= kFlPieces && (rec || cap >= 64 * ((nr + 8) / 8)));
         if (!fits) {
             take = false;
-            st = RD == kRdOne ? kStNeedWalk : kStNeedFull;
+            st = kStNeedFull;
         }
     }
     const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
@@ -2238,7 +2235,7 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
         // every lane stopped (at its framed length, the stream's end or an error)
         const bool stop = kStop && __builtin_amdgcn_ballot_w64(pos < end && wrun < lim_w) == 0;
         if (RD == kRdWalk && stop) break;
-        const bool last = k == maxr || stop;  // kRdOne: the record queue is flushed before the break
+        const bool last = k == maxr || stop;
         words += (cnt & 0xFFFFu) + ((cnt >> 16) & 0xFFFFu) + ((cnt >> 32) & 0xFFFFu) + (cnt >> 48);
         if (!SIZE_ONLY) {
             const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
@@ -2282,7 +2279,7 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
                                             ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(qa >> 32), (int)u, kWave) << 32);
                         const u32x4 v = *reinterpret_cast<const u32x4*>(ring_all + u * kRing + 16 * (lane & 3));
                         uint8_t* const qd = reinterpret_cast<uint8_t*>(ua) + 16 * (lane & 3);
-                        asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(qd), "v"(v) : "memory");
+                        asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(qd), "v"(v) : "memory");
                     }
                 }
             } else {
@@ -2293,16 +2290,6 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!valid || gated) return;  // gated: status and out_len of an earlier pass stand
-    if (RD == kRdOne && st == kStNeedWalk) {
-        status[unit] = kStNeedWalk;  // out_len (the framed length) stays for kRdWalk
-        return;
-    }
-    if (RD == kRdOne && st == ST_ARG) {  // a misaligned output slot: nothing consumed
-        out_len[unit] = 0;
-        consumed[unit] = 0;
-        status[unit] = ST_ARG;
-        return;
-    }
     if (kStop) {
         // reader.zig:91-93 / 146-153: the walk ended at the framed length (OK), past it
         // (InvalidPackedMessage), or the stream ended first (EndOfStream, also for a
@@ -2314,13 +2301,7 @@ __global__ __launch_bounds__(kWave * kIxBw) void decode_index_kernel(
             status[unit] = rs;
             return;
         }
-        if (RD == kRdWalk) {
-            status[unit] = kStNeedGate;
-            return;
-        }
-        // kRdOne: records written; the framed length is the decoded size
-        out_len[unit] = 8 * words;
-        status[unit] = 8 * words > cap ? ST_SPACE : ST_OK;
+        status[unit] = kStNeedGate;  // kRdWalk
         return;
     }
     if (st == kStNeedFull) {
@@ -2687,12 +2668,13 @@ constexpr uint32_t kLwLanes = kLwLB / 16;    // lanes per line in a flush store
 constexpr uint32_t kLwLds = kLwWaves * kWave * (kLwRing + kLwLB + 2) + 128;
 static_assert(kLwLds <= 26624, "six blocks per CU");
 
+template <bool RD>
 __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ in_len,
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
     const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count,
-    const uint32_t* __restrict__ list_lo) {
+    const uint32_t* __restrict__ list_lo, uint32_t* __restrict__ bail_count, uint64_t* __restrict__ consumed) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kLwWaves * kWave * kLwRing];
     __shared__ __attribute__((aligned(16))) uint8_t line_blk[kLwWaves * kWave * kLwLB];  // [lane][slot]
     __shared__ uint16_t ftab_blk[kLwWaves * kWave];  // flush table: lane | lo << 6 | hi << 10, by rank
@@ -2728,16 +2710,31 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     uint64_t P64 = 0, cap = 0;
     uint8_t* dstb = nullptr;
     int32_t st = ST_OK;
+    bool gated = false;  // RD: a unit the reader's other passes own (or that its header settled)
+    uint64_t fw = 0;     // RD: words of the framed message (read_header_kernel)
+    uint32_t past = 0;   // RD: stream bytes past the walked ones (capped; a cut literal run's test)
     if (valid) {
+        if (RD) gated = status[unit] != kStWords;
         src = in + in_off[unit];
         P64 = in_len[unit];
         dstb = out + out_off[unit];
         cap = out_cap[unit];
+        if (RD) {
+            // reader.zig:84-156 decodes records until the framed length is reached; a message
+            // takes at most 10 packed bytes per word (an FF record's first word), so the stream
+            // past that is never walked (read_header_kernel routes messages of more than
+            // kRdWordsMax words to the walk passes)
+            fw = out_len[unit] >> 3;
+            if (P64 > 10 * fw) {
+                past = P64 - 10 * fw > (1u << 20) ? (1u << 20) : (uint32_t)(P64 - 10 * fw);
+                P64 = 10 * fw;
+            }
+        }
         if (P64 > 0 && (reinterpret_cast<uintptr_t>(dstb) & 7)) st = ST_ARG;  // an empty unit writes nothing
         if (P64 >= kIxSizeMax) st = kStNeedFull;  // positions are u32 (the long-unit decoders own these)
     }
     const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-    const bool take = valid && st == ST_OK && P64 > 0;
+    const bool take = valid && !gated && st == ST_OK && P64 > 0;
     const uint32_t end = take ? s + (uint32_t)P64 : 0u;  // aligned-space end
     const uint32_t npieces = (end + 15) >> 4;
     uint32_t maxr = (end + 63) >> 6;  // rounds with data for this lane
@@ -2745,6 +2742,13 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     for (int d = 32; d >= 1; d >>= 1) maxr = max(maxr, (uint32_t)__shfl_xor((int)maxr, d, kWave));
     maxr = __builtin_amdgcn_readfirstlane(maxr);
     const uint32_t capw = (uint32_t)min(cap >> 3, (uint64_t)0x7FFFFFFFu);
+    // The walk stops after lim_w words: the framed length (RD), else the slot's capacity. A unit
+    // still owing input at capw is OUT_OF_SPACE (or UNEXPECTED_EOF further on): it is marked for
+    // decode_wave_kernel<kWvMarked>, whose window-parallel walk finds its status and size and
+    // writes nothing. A lane never steps more than capw words, and long zero runs go out as whole
+    // zero lines, so an expansion-heavy unit (00 FF chains: 256 words per 2 bytes) cannot hold its
+    // wave (launch_decode routes slots over kWordsCapMax to the two-pass decoder).
+    const uint32_t lim_w = RD ? (uint32_t)min(fw, (uint64_t)0x7FFFFFFFu) : capw;
     // output lines: word 0 of the unit sits in slot s0 of the 128-B line at line0
     const uint32_t s0 = take ? (uint32_t)((reinterpret_cast<uintptr_t>(dstb) >> 3) & (kLwLine - 1)) : 0u;
     const uint64_t line0 = reinterpret_cast<uint64_t>(dstb) - 8ull * s0;
@@ -2801,20 +2805,20 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
             // every line of the group whole (all but a unit's first and last lines): one store
             if (__builtin_amdgcn_ballot_w64(in_r && (flo | (fhi ^ kLwLine)) != 0u) == 0) {
                 ++younger;
-                if (in_r) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v));
+                if (in_r) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v));
                 return;
             }
             const bool a0 = in_r && 2 * j >= flo && 2 * j < fhi, a1 = in_r && 2 * j + 1 >= flo && 2 * j + 1 < fhi;
             const bool both = a0 && a1, first = a0 && !a1, second = a1 && !a0;
             if (__builtin_amdgcn_ballot_w64(both) != 0) {
                 ++younger;
-                if (both) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v));
+                if (both) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v));
             }
             if (__builtin_amdgcn_ballot_w64(first | second) != 0) {
                 ++younger;
                 uint8_t* const q = second ? p + 8 : p;
                 const uint64_t x = second ? ((uint64_t)v.z | ((uint64_t)v.w << 32)) : ((uint64_t)v.x | ((uint64_t)v.y << 32));
-                if (first | second) asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(q), "v"(x));
+                if (first | second) asm volatile("global_store_dwordx2 %0, %1, off nt\n\ts_nop 1" ::"v"(q), "v"(x));
             }
         };
         constexpr uint32_t kGrp = kWave / kLwLanes;  // lines per store instruction
@@ -2849,7 +2853,10 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
     int32_t apos = po;           // po, or INT_MIN during a zero run (its words need no bytes)
     uint32_t W = 0;              // words emitted
     if (maxr > 0) load(0);
+    uint32_t ksh = 0;  // rounds that moved the ring offsets back by 64
     for (uint32_t k = 0; k <= maxr; ++k) {
+        // every lane done (input walked, or lim_w words out): the rounds left would only move bytes
+        if (__builtin_amdgcn_ballot_w64(take && W < lim_w && (po < end_o || run != 0u)) == 0) break;
         if (k < maxr) {
             vmcnt_at_most63(younger);  // round k's loads are in
             asm volatile("" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
@@ -2865,6 +2872,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
             wave_lds_sync();
             po -= 64;
             end_o -= 64;
+            ++ksh;
             apos = apos == INT32_MIN ? apos : po;
         }
         if (k < maxr) {
@@ -2877,14 +2885,42 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         }
         const int32_t lim = min(64, end_o);  // sources of this round: ring offsets < lim
         for (;;) {  // sub-rounds
+            // ---- long zero runs: whole zero lines straight to the slot, not a step per word (an
+            // expansion-heavy unit, 00 FF: 256 words per 2 bytes, would hold its wave's round) ----
+            if (__builtin_amdgcn_ballot_w64(run >= kLwLine && rsel == 0u) != 0) {  // rare: one test per sub-round
+                const uint32_t wcap = min(lim_w, capw);  // whole lines below the slot's capacity
+                const bool bz = rsel == 0u && run >= kLwLine && ((s0 + W) & (kLwLine - 1)) == 0u &&
+                                W + kLwLine <= wcap;
+                if (__builtin_amdgcn_ballot_w64(bz) != 0) {
+                    const uint32_t nl = bz ? min(run, wcap - W) / kLwLine : 0u;
+                    const uint32_t nmax = wave_max_u32(nl);
+                    const u32x4 z = {0u, 0u, 0u, 0u};
+                    for (uint32_t i = 0; i < nmax; ++i) {  // wave-uniform
+                        if (i < nl) {
+                            uint8_t* const zl = reinterpret_cast<uint8_t*>(line0 + (uint64_t)kLwLB * ((s0 + W) / kLwLine + i));
+#pragma unroll
+                            for (uint32_t c = 0; c < kLwLB / 16; ++c)
+                                asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(zl + 16 * c), "v"(z));
+                        }
+                        younger += kLwLB / 16;
+                    }
+                    W += kLwLine * nl;
+                    run -= kLwLine * nl;
+                    apos = (run != 0u && rsel == 0u) ? INT32_MIN : po;
+                }
+            }
             // ---- A: the chain. Step j leaves (payload ring offset | selector tag << 8) in rec[j] ----
             uint32_t rec[kLwS];
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) rec[j] = 0u;  // steps not taken: ring offset 0, tag 00
             uint32_t e = 0;
+            // a decode stops a lane at the first sub-round that ends at or past its capacity (words
+            // past out_cap are never stored); a read stops at the framed length exactly
+            const uint32_t rem = W < lim_w ? lim_w - W : 0u;
+            const int32_t limx = rem != 0u ? lim : INT32_MIN;
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) {
-                const bool act = apos < lim;
+                const bool act = apos < limx && (!RD || j < rem);
                 if (__builtin_amdgcn_ballot_w64(act) == 0) break;
                 if (act) {
                     // the source's ring offset, kept inside the ring (a zero run's may have left it)
@@ -2936,7 +2972,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                     if (j < e && j >= f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & (kLwLine - 1))) = w[j];
             }
             W += e;
-            if (__builtin_amdgcn_ballot_w64(apos < lim) == 0) break;
+            if (__builtin_amdgcn_ballot_w64(apos < lim && W < lim_w) == 0) break;
         }
     }
     // the unit's last line, in part (a full last line went out when it filled)
@@ -2946,13 +2982,43 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
         flush(part, line0 + (uint64_t)kLwLB * L, L == 0 ? s0 : 0u, line_hi_cap(L, hi));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!valid) return;
+    if (!valid || gated) return;
     if (st == kStNeedFull) {  // the long-unit decoders' (launch_decode never lists these here)
         status[unit] = st;
         return;
     }
-    // message.zig:152-191: the walk ends exactly at the input's end with no literal word owed
-    if (take && (po != end_o || run != 0u)) st = ST_EOF;
+    if (RD) {
+        // reader.zig:91-93 / 146-153: the walk stopped at the first record boundary with the framed
+        // length reached (OK, consumed = the bytes it took), inside a run that passes it
+        // (InvalidPackedMessage, unless the run's literal bytes are cut: readNoEof's EndOfStream),
+        // or the stream ended first / cut a record (EndOfStream)
+        const int32_t rend = po + (int32_t)((rsel & 8u) * run);  // the current record's end
+        int32_t rs = st;
+        if (rs == ST_OK && take)
+            rs = (W < lim_w || po > end_o) ? ST_EOS
+                                           : (run != 0u ? (rend > end_o + (int32_t)past ? ST_EOS : ST_OVERSHOOT) : ST_OK);
+        if (rs != ST_OK) {
+            out_len[unit] = 0;
+            consumed[unit] = 0;
+            status[unit] = rs;
+            return;
+        }
+        // aligned-space position: po + 64 per round that moved it back, less the carry's offset
+        consumed[unit] = take ? (uint64_t)((int64_t)po + 64ll * ksh - kLwCarry - s) : 0ull;
+        out_len[unit] = 8ull * W;
+        status[unit] = 8ull * W > cap ? ST_SPACE : ST_OK;
+        return;
+    }
+    // message.zig:152-191: the walk ends exactly at the input's end with no literal word owed;
+    // a unit stopped at capw with input left needs its status and size from the fallback walk
+    if (take && (po != end_o || run != 0u)) {
+        if (W >= lim_w && po <= end_o) {
+            status[unit] = kStNeedFull;  // decode_wave_kernel<kWvMarked>: status and size, no output
+            atomicAdd(bail_count, 1u);
+            return;
+        }
+        st = ST_EOF;
+    }
     if (st != ST_OK) {
         out_len[unit] = 0;
         status[unit] = st;
@@ -2992,6 +3058,7 @@ constexpr uint64_t kSmEncWords = 64;  // encode: units of at most 64 words are s
 constexpr uint64_t kSmDecP = 512;     // decode: small = at most 512 packed bytes ...
 constexpr uint64_t kSmDecCap = 8192;  // ... into a slot of at most 8 KiB
 constexpr uint64_t kMidSplitP = 1280; // decode: mid units of at most this many packed bytes (bins 0 .. 2)
+constexpr uint64_t kWordsCapMax = 8192;  // decode: the words decoder takes slots of at most 8 KiB
 
 __device__ __forceinline__ uint32_t* q_blocks(uint32_t* q, uint32_t n) { return q + kQHead + 3ull * n; }
 
@@ -3018,6 +3085,9 @@ __device__ __forceinline__ uint32_t unit_class(const uint8_t* in, const uint64_t
     const uint64_t cap = out_cap[u];
     if (len <= kSmDecP && cap <= kSmDecCap) return CL_SMALL;
     if (decode_long_unit(in, off, len, out, out_off[u], cap)) return len > kQHuge ? CL_HUGE : CL_LONG;
+    // a slot over kWordsCapMax: the two-pass decoder's bins (its fill expands a unit 64 words per
+    // step; the words decoder steps a word at a time, up to capw of them)
+    if (cap > kWordsCapMax) return CL_MID + (len > 768) + (len > 1024);
     return CL_MID + (len > 768) + (len > 1024) + (len > kMidSplitP) + (len > 1536) + (len > 2048) + (len > 2560) +
            (len > 3072);
 }
@@ -3097,6 +3167,7 @@ __global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t 
         // ~600 steps is long: under a resident grid of units, or at p ~ 0.9, two-pass wins)
         const uint32_t over = mid - q[11 + 3];
         q[20] = words_min == 0 ? 0u : (over >= words_min ? q[11 + 3] : mid);
+        q[21] = 0;  // decode_words_kernel's count of units stopped at their slot's capacity
     }
 }
 
@@ -4831,13 +4902,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 //   1. read_header_kernel: lane per unit, decodes records until the segment table
 //      is complete (one record for a 1-segment message) and writes the framed
 //      length to out_len, or the header error to status;
-//   2. decode_index_kernel<false, kRdOne>: the coalesced tag walk, stopped at the framed
-//      length, writing the piece records as it goes; writes consumed (packed bytes of the
-//      message) and the EndOfStream / InvalidPackedMessage / OutOfSpace outcome. Units
-//      whose bytes the fill pass could not stage go on (kStNeedWalk) to
-//   3. decode_index_kernel<true, kRdWalk> (the walk alone) and decode_index_kernel<false,
-//      kRdGate> (the records over in_len = consumed), as round 2 did for every unit;
-//   4. the fill pass and the full-path fallback over in_len = consumed, for OK units.
+//      (ROUTE: messages of at most kRdWordsMax framed words kStWords, longer ones kStNeedWalk);
+//   2. messages of more than kRdWordsMax words: decode_index_kernel<true, kRdWalk> (the walk
+//      alone, consumed) and decode_index_kernel<false, kRdGate> (the records over in_len =
+//      consumed), then the fill pass and the full-path fallback over in_len = consumed;
+//   3. the others: decode_words_kernel<true> (round 6), which stops each lane's walk at the
+//      first record boundary that reaches the framed length and applies the reader's
+//      overshoot / end-of-stream rules there; consumed = the bytes it walked.
 constexpr uint64_t kMaxTotalWords = 8ull * 1024 * 1024;  // reader.zig:6
 constexpr uint64_t kMaxSegments = 512;                   // message.zig:310
 constexpr uint64_t kHdrMaxWords = 257;                   // (1 + 512 + pad) u32 = 257 words
@@ -4905,6 +4976,9 @@ __device__ int32_t packed_header(const uint8_t* __restrict__ p, uint64_t P, uint
     }
 }
 
+// ROUTE (launch_read_message): a message of at most kRdWordsMax framed words goes to the words
+// decoder (kStWords), a longer one to the walk passes (kStNeedWalk); errors stand.
+template <bool ROUTE>
 __global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __restrict__ in,
                                                              const uint64_t* __restrict__ in_off,
                                                              const uint64_t* __restrict__ in_len, uint32_t n,
@@ -4915,7 +4989,7 @@ __global__ __launch_bounds__(kBlock) void read_header_kernel(const uint8_t* __re
     if (unit >= n) return;
     uint64_t needed = 0;
     const int32_t st = packed_header(in + in_off[unit], in_len[unit], needed);
-    status[unit] = st;
+    status[unit] = (ROUTE && st == ST_OK) ? ((needed >> 3) <= kRdWordsMax ? kStWords : kStNeedWalk) : st;
     out_len[unit] = st == ST_OK ? needed : 0;
     consumed[unit] = 0;
 }
@@ -5450,9 +5524,9 @@ class SideLaunch {
 
 // Drop the library's context of a caller stream (its side stream, events and queues, also
 // those captured graphs used): after the stream's work is done and before it is destroyed.
-hipError_t release_stream(hipStream_t stream) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
+hipError_t release_stream(hipStream_t stream, int dev) {
+    hipError_t e = hipSuccess;
+    if (dev < 0) e = hipGetDevice(&dev);  // contexts are keyed by (device, stream)
     if (e != hipSuccess) return e;
     std::shared_ptr<StreamCtx> c;
     {
@@ -5652,7 +5726,7 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
     // leave a failed unit's prefix, so all-or-nothing decodes take the two-pass decoder only.
     const bool words = (decoder_variant() == CAPNP_PACKED_DECODER_AUTO ||
                         decoder_variant() == CAPNP_PACKED_DECODER_WORDS) && small_variant() != 0;
-    static const uint32_t words_min = resident_blocks(decode_words_kernel, kLwWaves * kWave, 6) * kLwWaves * kWave;
+    static const uint32_t words_min = resident_blocks(decode_words_kernel<false>, kLwWaves * kWave, 6) * kLwWaves * kWave;
     SideLaunch side(stream, ws, ws_bytes);
     uint32_t* const q = side.queue(n);
     if (!q) return ws ? hipErrorInvalidValue : hipErrorOutOfMemory;
@@ -5700,8 +5774,13 @@ hipError_t launch_decode(const uint8_t* in, const uint64_t* in_off, const uint64
             in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mid, q + 20, rec);
         decode_fill_kernel<<<fill_blocks(n), kFlWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off,
                                                                            out_len, out_cap, status, mid, q + 20, rec);
-        decode_words_kernel<<<lw_blocks, kLwWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                   out_len, status, mid, q + 4, q + 20);
+        decode_words_kernel<false><<<lw_blocks, kLwWaves * kWave, 0, ms>>>(in, in_off, in_len, n, out, out_off, out_cap,
+                                                                          out_len, status, mid, q + 4, q + 20, q + 21,
+                                                                          nullptr);
+        // the words decoder's units stopped at their slot's capacity with input left (q[21] of them,
+        // usually none: the kernel returns at once)
+        decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, ms>>>(in, in_off, in_len, n, out, out_off,
+                                                                            out_cap, out_len, status, q + 21);
     } else
     {
         uint8_t* const rec = reinterpret_cast<uint8_t*>(q) + rec_region_off(n);  // piece records, off the output slots
@@ -5784,12 +5863,10 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint64_t* out_len,
                                uint64_t* consumed, int32_t* status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    read_header_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
-                                                                         status);
-    // one walk for the units the fill pass can take: records and the stop at the framed length
-    decode_index_kernel<false, kRdOne><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
-                                                                  out_len, status, consumed);
-    // the rest (kStNeedWalk): the walk to the framed length, then the gated write pass
+    read_header_kernel<true><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
+                                                                        status);
+    // messages of more than kRdWordsMax words (kStNeedWalk): the walk to the framed length, then
+    // the gated write pass, the fill pass and the fallback (each takes only the statuses it owns)
     decode_index_kernel<true, kRdWalk><<<ix_blocks_for(n), kWave * kIxBw, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap,
                                                                   out_len, status, consumed);
     // the message's own bytes from here on: in_len = consumed
@@ -5799,6 +5876,10 @@ hipError_t launch_read_message(const uint8_t* in, const uint64_t* in_off, const 
                                                                        out_len, out_cap, status);
     decode_wave_kernel<kWvMarked><<<fallback_blocks(n), kWvBlock, 0, stream>>>(in, in_off, consumed, n, out, out_off,
                                                                         out_cap, out_len, status, nullptr);
+    // the rest (kStWords): the words decoder, stopped at the framed length; last, so that the fill
+    // pass above (it takes OK units) never sees the units it finishes
+    decode_words_kernel<true><<<(n + kLwWaves * kWave - 1) / (kLwWaves * kWave), kLwWaves * kWave, 0, stream>>>(
+        in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, nullptr, nullptr, nullptr, consumed);
     return hipGetLastError();
 }
 
@@ -5811,7 +5892,7 @@ hipError_t launch_copy_jobs(const uint64_t* jobs, uint32_t nj, hipStream_t strea
 hipError_t launch_read_header(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                               uint64_t* out_len, uint64_t* consumed, int32_t* status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    read_header_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
+    read_header_kernel<false><<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(in, in_off, in_len, n, out_len, consumed,
                                                                          status);
     return hipGetLastError();
 }
@@ -5941,3 +6022,4 @@ hipError_t launch_scan(const uint64_t* len, uint32_t n, uint64_t base, uint64_t*
 }  // namespace cpk
 
 // Diagnostic builds only: read and clear the phase cycle sums.
+

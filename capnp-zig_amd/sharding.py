@@ -22,10 +22,12 @@ def shard_range(rank: int, world: int, n_units: int) -> tuple[int, int]:
     return lo, lo + q + (1 if rank < r else 0)
 
 
-def gather_packed_totals(local_total, group=None) -> torch.Tensor:
+def gather_packed_totals(local_total, group=None, collective_at_world1: bool = False) -> torch.Tensor:
     """All-gather each rank's packed byte total. `local_total` is an int or a
     0-d/1-element int64 tensor (device tensor for RCCL, CPU tensor for gloo).
-    Returns a (world,) int64 tensor on the same device."""
+    Returns a (world,) int64 tensor on the same device. A world of one is a copy
+    unless `collective_at_world1` (the test that puts RCCL's all-gather on the GPU,
+    tests/test_gpu_rccl.py)."""
     if isinstance(local_total, torch.Tensor):
         t = local_total.reshape(1).to(torch.int64)
     else:
@@ -34,7 +36,7 @@ def gather_packed_totals(local_total, group=None) -> torch.Tensor:
         t = torch.tensor([int(local_total)], dtype=torch.int64, device=dev)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     out = torch.empty(world, dtype=torch.int64, device=t.device)
-    if world == 1:
+    if world == 1 and not (collective_at_world1 and dist.is_initialized()):
         out.copy_(t)
     else:
         dist.all_gather_into_tensor(out, t, group=group)

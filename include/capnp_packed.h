@@ -39,8 +39,9 @@ extern "C" {
 /* ABI version (INTEGRATION.md §5 lists what changed):
  *   2 (round 5): capnp_packed_framer_* and capnp_packed_set_launch_flags (added in round 4),
  *     capnp_packed_stream_contexts, CAPNP_PACKED_DECODER_WORDS; CAPNP_PACKED_DECODER_FUSED /
- *     _STREAM answer INVALID_ARGUMENT outside dev builds, and the CPK_DECODE environment
- *     variable is gone (capnp_packed_set_decoder is the only selector). */
+ *     _STREAM answer INVALID_ARGUMENT (those decoders were removed from the library in round 5,
+ *     source at 869fccf), and the CPK_DECODE environment variable is gone
+ *     (capnp_packed_set_decoder is the only selector). Round 6 changed no signature. */
 #define CAPNP_PACKED_ABI_VERSION 2u
 
 /* Status codes. The first four mirror the reference's error set
@@ -133,11 +134,14 @@ int capnp_packed_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, s
  *
  * `stream` is a hipStream_t (NULL = default stream). Calls are asynchronous:
  * they enqueue kernels and return. The return value reports launch errors only;
- * per-unit results are in d_status / d_out_len. A decode unit of more than 512
- * packed bytes (or into a slot over 8 KiB) whose status is an error leaves its slot
- * untouched (message.zig:88-145 returns the error before any output); a smaller one,
- * and an encode unit that ends OUT_OF_SPACE, may hold a prefix (never a byte past
- * its capacity). Run capnp_packed_decoded_size_batch first for all-or-nothing there.
+ * per-unit results are in d_status / d_out_len. A unit that fails never has a byte
+ * written past its out_cap, or outside its slot. Inside the slot, at every batch size,
+ * the default contract is: the content of a failed decode unit's [0, out_cap) is
+ * unspecified (the streaming kernels, for small units and for the words decoder's mid
+ * units, may leave a prefix of its output), and likewise for an encode unit that ends
+ * OUT_OF_SPACE. capnp_packed_set_all_or_nothing(1) makes every failed decode unit leave
+ * its slot untouched, as unpackPacked does (message.zig:88-145 returns the error before
+ * any output); or run capnp_packed_decoded_size_batch first.
  *
  * Workspace: encode / encoded_size / decode batches need a class workspace of
  * capnp_packed_batch_workspace_bytes(n) bytes (~750 B per unit + ~6 MiB: the small / mid /
@@ -370,16 +374,16 @@ int capnp_packed_generate(uint8_t* d_out, uint64_t n_units, uint64_t unit_bytes,
  *                                  (round 5; a failed unit may hold a prefix
  *                                  of its output unless capnp_packed_set_all_or_nothing(1));
  *   CAPNP_PACKED_DECODER_AUTO      the library's default: the words decoder for the mid units of
- *                                  more than 1280 packed bytes when a batch has at least a
- *                                  resident grid of them (~196K units on MI355X), the two-pass
- *                                  decoder for the rest; all two-pass under
- *                                  capnp_packed_set_all_or_nothing(1).
- * Dev builds only (built with CPK_DEV_DECODERS=1; the shipped library returns
- * CAPNP_PACKED_INVALID_ARGUMENT for them): the single-read decoders, both measured slower
- * than the two-pass decoder on every density:
- *   CAPNP_PACKED_DECODER_FUSED     single pass: per-lane 8-state entry maps, one read;
- *   CAPNP_PACKED_DECODER_STREAM    single pass: lane-per-unit walk by 64-B windows, stores
- *                                  by many lanes per unit (a failed unit may hold a prefix).
+ *                                  more than 1280 packed bytes into slots of at most 8 KiB when a
+ *                                  batch has at least a resident grid of them (~196K units on
+ *                                  MI355X), the two-pass decoder for the rest;
+ *                                  all two-pass under capnp_packed_set_all_or_nothing(1).
+ * The words decoder steps one output word at a time and stops a unit at its slot's capacity
+ * (its size then comes from a record walk), so no unit costs it more than out_cap / 8 steps.
+ * Removed in round 5 (source at 869fccf), both measured slower than the
+ * two-pass decoder: CAPNP_PACKED_DECODER_FUSED (per-lane 8-state entry maps) and
+ * CAPNP_PACKED_DECODER_STREAM (lane-per-unit walk by 64-B windows); the library returns
+ * CAPNP_PACKED_INVALID_ARGUMENT for them.
  * Returns the previous value; applies to batches enqueued after the call (process-wide). */
 enum {
     CAPNP_PACKED_DECODER_AUTO = 0,
@@ -396,7 +400,7 @@ int capnp_packed_set_decoder(int decoder);
  * output). Small units (<= 512 packed bytes into <= 8-KiB slots) are by default decoded a lane
  * each in one streaming pass, and mid units the words decoder takes (see
  * capnp_packed_set_decoder) stream their output out as they go: a failed one may keep a prefix
- * of its output (never a byte past out_cap). With on != 0, small units are decoded through LDS
+ * of its output (never a byte past out_cap), at any batch size (the default contract above). With on != 0, small units are decoded through LDS
  * and stored only when OK, and every mid unit goes to the two-pass decoder, at a cost (C5
  * decode 0.69 -> 0.79 ms; the headline decode 2.0 -> 2.5 ms). */
 int capnp_packed_set_all_or_nothing(int on);

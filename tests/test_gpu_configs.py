@@ -422,3 +422,76 @@ def test_c5_launch_flags(flags):
         test_c5_full_size_1M_units("twopass")
         with cp.decoder("words"):
             test_c5_skewed_sizes_every_unit(128, "words")
+
+
+def _segment_pool_end_to_end(messages, rng):
+    """Each message's segments laid end to end (a MessageBuilder arena's layout), the message's
+    first segment at 0 or 8 mod 16 of the pool; returns what _segment_pool returns."""
+    offs, pos = [], 0
+    for i, m in enumerate(messages):
+        pos = (pos + 15) // 16 * 16 + 8 * (i % 2) + 16 * int(rng.integers(0, 3))
+        for s in m:
+            offs.append(pos)
+            pos += len(s)
+    flat = [s for m in messages for s in m]
+    host = np.zeros(pos + 16, dtype=np.uint8)
+    for o, s in zip(offs, flat):
+        host[o:o + len(s)] = np.frombuffer(s, dtype=np.uint8)
+    pool = torch.from_numpy(host).to(DEV)
+    base = pool.data_ptr()
+    assert base % 16 == 0
+    seg_ptr = torch.tensor([base + o for o in offs] or [0], dtype=torch.int64, device=DEV)
+    seg_len = torch.tensor([len(s) for s in flat] or [0], dtype=torch.int64, device=DEV)
+    first, k = [], 0
+    for m in messages:
+        first.append(k)
+        k += len(m)
+    return (pool, seg_ptr, seg_len, torch.tensor(first, dtype=torch.int32, device=DEV),
+            torch.tensor([len(m) for m in messages], dtype=torch.int32, device=DEV))
+
+
+def test_encode_message_segments_end_to_end():
+    """The one-tile encoder's end-to-end path (encode_message_tile1_body: one staged run after
+    header words computed per lane) against toPackedBytes (message.zig:2123-2179, the oracle):
+    1 .. 64 segments (even and odd counts: the padding word), empty segments, bases at 0 and
+    8 mod 16, and framed lengths up to and around the one-tile limit of 512 words."""
+    rng = np.random.default_rng(0xE2E)
+
+    def seg(words, p):
+        b = rng.integers(1, 256, 8 * words, dtype=np.uint8)
+        b[rng.random(8 * words) < p] = 0
+        return b.tobytes()
+
+    messages = []
+    for count in list(range(1, 17)) + [31, 32, 33, 63, 64]:
+        for target in (8, 200, 480, 505, 512, 530):  # framed words aimed at around the tile limit
+            hw = (1 + count + (0 if count % 2 else 1)) // 2
+            room = max(target - hw, 0)
+            cuts = np.sort(rng.integers(0, room + 1, count - 1)) if count > 1 else np.zeros(0, dtype=np.int64)
+            sizes = np.diff(np.concatenate([[0], cuts, [room]])).astype(int)
+            if count > 2:
+                sizes[int(rng.integers(0, count))] += sizes[0] if rng.random() < 0.3 else 0
+                sizes[0] = 0 if rng.random() < 0.3 else sizes[0]  # empty segments
+            p = float(rng.choice([0.1, 0.5, 0.9]))
+            messages.append([seg(int(w), p) for w in sizes])
+    pool, seg_ptr, seg_len, first, count = _segment_pool_end_to_end(messages, rng)
+    n = len(messages)
+    caps = [cp.encode_bound(len(_frame(m))) for m in messages]
+    offs, q = [], 0
+    for c in caps:
+        offs.append(q)
+        q += (c + 15) // 16 * 16
+    t = lambda xs: torch.tensor(xs, dtype=torch.int64, device=DEV)  # noqa: E731
+    d_out = torch.zeros(q + 16, dtype=torch.uint8, device=DEV)
+    out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_message_batch(seg_ptr, seg_len, first, count, d_out, t(offs), t(caps), out_len, status)
+    torch.cuda.synchronize()
+    h, lens, sts = d_out.cpu().numpy(), out_len.cpu().numpy(), status.cpu().numpy()
+    one_tile = 0
+    for i, m in enumerate(messages):
+        st, exp = oracle.pack(_frame(m))
+        assert st == oracle.OK
+        one_tile += len(_frame(m)) // 8 <= 512
+        assert sts[i] == cp.OK and h[offs[i]:offs[i] + lens[i]].tobytes() == exp, f"message {i}: {len(m)} segments"
+    assert one_tile >= n // 2

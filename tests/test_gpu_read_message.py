@@ -243,3 +243,51 @@ def test_single_buffer_unbounded_cap():
                                             ctypes.byref(used))
     assert st == cp.OK and n.value == len(exp) and used.value == len(a)
     assert out.raw[:len(exp)] == exp and out.raw[len(exp):] == b"\xab" * 64
+
+
+def _overshoot_stream(rng, body_words, tail):
+    """A one-segment message of body_words words whose packed body ends with `tail`: a record
+    that ends exactly at the framed length, or a zero / literal run that passes it (its
+    literal bytes whole or cut), so the reader stops inside a run (reader.zig:146-153)."""
+    head = pyref.pack(struct.pack("<II", 0, body_words))
+    body = bytearray()
+    words = 0
+    room = body_words - 2
+    while words < room:
+        t = rng.randrange(1, 255)
+        body += bytes([t]) + bytes(rng.randrange(1, 256) for _ in range(bin(t).count("1")))
+        words += 1
+    if tail == "exact":
+        body += b"\x00\x01"                      # two zero words: ends at the framed length
+    elif tail == "zero_run_over":
+        body += bytes([0, rng.randrange(2, 40)])  # passes it inside a zero run
+    else:
+        c = rng.randrange(2, 40)
+        lit = bytes(rng.randrange(256) for _ in range(8 * c))
+        if tail == "literal_cut":
+            lit = lit[:rng.randrange(len(lit))]
+        body += b"\xff" + bytes(rng.randrange(256) for _ in range(8)) + bytes([c]) + lit
+    return bytes(head) + bytes(body) + bytes(rng.randrange(256) for _ in range(rng.randrange(0, 24)))
+
+
+def test_overshoot_inside_runs_and_the_words_bound():
+    """Messages of 1020 .. 1030 framed words (kRdWordsMax = 1024 on the words decoder, longer ones
+    on the walk passes), each ending exactly, or passing the framed length inside a zero run, a
+    whole literal run (InvalidPackedMessage) or a cut literal run (EndOfStream), at every
+    alignment of the stream; status, framed bytes and consumed against the oracle."""
+    rng = random.Random(0x0E5)
+    streams = []
+    for body_words in range(1019, 1030):
+        for tail in ("exact", "zero_run_over", "literal_over", "literal_cut"):
+            streams.append(_overshoot_stream(rng, body_words, tail))
+    got_codes = set()
+    for pad in range(0, 16, 3):
+        check(streams, pad_front=pad, caps=[9000] * len(streams))
+        got_codes |= {expected(s)[0] for s in streams}
+    assert got_codes == {cp.OK, cp.INVALID_PACKED_MESSAGE, cp.END_OF_STREAM}
+    # slots 8 B short: OUT_OF_SPACE with the framed length and the packed length
+    ok = [s for s in streams if expected(s)[0] == cp.OK]
+    short = gpu_read(ok, caps=[len(expected(s)[1]) - 8 for s in ok])
+    for s, g in zip(ok, short):
+        st, framed, used = expected(s)
+        assert g[0] == cp.OUT_OF_SPACE and g[2] == used

@@ -165,10 +165,16 @@ pub const gpu_unpack_min_bytes: usize = 64 * 1024;
 /// Framer dispatch (INTEGRATION.md §1.8; scripts/framer_crossover.py,
 /// profiles/r05_framer_crossover.json, MI355X + EPYC 9575F host, p = 0.5): one read call of the
 /// device framer session (capnp_packed_framer_readv: gather, H2D, walk, decode, D2H) against
-/// the Zig Framer + readPackedMessage loop on one core, host buffers both sides.
-///   N connections x 16 messages of 4 KiB framed per call: the device is faster from 4
-///     connections (164 KB packed: 587 vs 611 us; 4096 connections: 13.5 vs 655 ms); one
-///     connection (41 KB): 518 vs 142 us, so small batches stay on the CPU.
+/// the CPU reader on one core, host buffers both sides. The CPU side measured is the C oracle
+/// port of the reader (oracle_read_stream: a readPackedMessage loop per connection, called
+/// through ctypes; in the split case the Python driver appends each read to a bytearray), not
+/// the Zig Framer itself: no Zig toolchain on the build host, so Zig parity of these CPU times
+/// is unpinned.
+///   N connections x 16 messages of 4 KiB framed per call: the two cross at 4 connections
+///     (164 KB packed: 587 vs 611 us, 4% apart on one box); from 8 connections (328 KB) the
+///     device is 2x faster (605 vs 1253 us; 4096 connections: 13.5 vs 655 ms); one connection
+///     (41 KB): 518 vs 142 us. The threshold sits at the 8-connection row, with a 2x margin
+///     over the crossover, not at the crossover itself.
 ///   one connection, a message arriving in 64 KiB reads: faster from 256 KiB framed (503 vs
 ///     1342 us; 16 MiB: 17.9 vs 3361 ms), since the device walk resumes across reads while the
 ///     CPU framer re-decodes the buffered prefix on every read.
@@ -176,7 +182,7 @@ pub const gpu_unpack_min_bytes: usize = 64 * 1024;
 /// or when a connection's message in progress (capnp_packed_framer_expected) is at least
 /// gpu_framer_min_message_bytes; a connection moves between the two framers only while it holds
 /// no partial message, so no framer state ever has to be handed over.
-pub const gpu_framer_min_read_bytes: usize = 160 * 1024;
+pub const gpu_framer_min_read_bytes: usize = 320 * 1024;
 pub const gpu_framer_min_message_bytes: usize = 256 * 1024;
 
 /// The reference's error names, plus the two the device can add. `NoDevice`
