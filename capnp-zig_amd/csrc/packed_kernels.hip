@@ -2914,6 +2914,10 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) rec[j] = 0u;  // steps not taken: ring offset 0, tag 00
             uint32_t e = 0;
+            // the chain is every lane's critical path: raised wave priority lets it issue ahead of
+            // the other waves' phase-B expansion on the SIMD (A/B in profiles/r06_experiments/
+            // words_setprio_ab.log: 1-2 % at every density)
+            __builtin_amdgcn_s_setprio(1);
             // a decode stops a lane at the first sub-round that ends at or past its capacity (words
             // past out_cap are never stored); a read stops at the framed length exactly
             const uint32_t rem = W < lim_w ? lim_w - W : 0u;
@@ -2941,6 +2945,7 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                     e = j + 1;
                 }
             }
+            __builtin_amdgcn_s_setprio(0);
             // ---- B: the words (selectors looked up and applied off the chain) ----
             uint64_t w[kLwS];
 #pragma unroll
@@ -2964,8 +2969,10 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
                 if (j < e && j < f) *reinterpret_cast<uint64_t*>(myline + 8 * ((sl + j) & (kLwLine - 1))) = w[j];
             const bool full = e >= f && e != 0u;
             if (__builtin_amdgcn_ballot_w64(full) != 0) {
+                __builtin_amdgcn_s_setprio(1);  // so is the flush the block waits for
                 const uint32_t L = (s0 + W) / kLwLine;
                 flush(full, line0 + (uint64_t)kLwLB * L, L == 0 ? s0 : 0u, line_hi_cap(L, kLwLine));
+                __builtin_amdgcn_s_setprio(0);
                 wave_lds_sync();  // the flush's line reads come before the next line's words
 #pragma unroll
                 for (uint32_t j = 0; j < kLwS; ++j)
