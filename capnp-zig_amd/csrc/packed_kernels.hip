@@ -107,6 +107,12 @@ constexpr int32_t kStPending = CAPNP_PACKED_DEVICE_ERROR;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// 16 readable bytes for load lanes that have nothing to stage, and 16 writable
+// bytes for the piece-record stores of lanes without a unit.
+__device__ __attribute__((aligned(16))) uint8_t cpk_dummy16[16];
+__device__ __attribute__((aligned(16))) uint8_t cpk_sink16[16];
+__device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
+
 // 16-B load of data read for the last time (non-temporal). The fill pass's piece loads
 // use it (decode 2.42 -> 2.40 ms); encode's staging loads were slower with it.
 __device__ __forceinline__ uint4 load_nt(const void* p) {
@@ -123,6 +129,19 @@ __device__ __forceinline__ uint4 load_nt(const void* p) {
 // the wait (cdna_hip_programming.md §5.7 item 1, form ii).
 __device__ __forceinline__ void ds_gload16(u32x4& d, const void* p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+
+// LDS-DMA: each lane's 16 B at gsrc straight into LDS at lds_base + 16 * lane (no VGPR
+// destination; count it with vmcnt, then a barrier before other waves read it). M0 is written
+// and restored in the same statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_base) : "memory");
+}
+// the LDS byte address of a __shared__ object
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)p);
 }
 
 // Order LDS traffic between lanes of ONE wave (the wave owns its LDS slice).
@@ -247,7 +266,7 @@ __device__ __forceinline__ uint64_t perm64(uint64_t d, uint64_t sel) {
 //   compact: gathers the nonzero bytes of a word with tag t into bytes 0..popc-1
 //            (0x0C = zero above them);
 //   expand:  scatters popc(t) packed bytes back to the set-bit positions of t.
-struct SelLut {
+struct alignas(16) SelLut {
     uint64_t v[256];
 };
 constexpr SelLut make_sel_lut(bool expand) {
@@ -273,6 +292,13 @@ __device__ constexpr SelLut kExpandLut = make_sel_lut(true);
 // The compact selector moved up one byte (byte 0 selects a zero byte): perm64(w, it) is the
 // tag's record payload at bytes 1..popc, ready to OR with the tag (encode_tile).
 __device__ __forceinline__ uint64_t compact_selector(uint32_t t) { return (kCompactLut.v[t] << 8) | 0x0Cull; }
+// the same as a table, for a copy into LDS by LDS-DMA (encode_kernel)
+constexpr SelLut make_compact_sel() {
+    SelLut l = make_sel_lut(false);
+    for (uint32_t t = 0; t < 256; ++t) l.v[t] = (l.v[t] << 8) | 0x0Cull;
+    return l;
+}
+__device__ constexpr SelLut kCompactSel = make_compact_sel();
 __device__ __forceinline__ uint64_t expand_selector(uint32_t t) { return kExpandLut.v[t]; }
 
 // Unaligned 8-byte read from an LDS byte array (two aligned ds_read_b64 + funnel).
@@ -558,14 +584,20 @@ template <bool WRITE, bool SINGLE, bool FULL = false>
 __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lut, uint32_t lane, uint32_t words,
                                                 uint32_t tb, uint32_t& cz_c, uint32_t& cf_c, uint32_t nbz,
                                                 uint32_t nbf, uint8_t* dst, uint64_t room,
-                                                const uint8_t* direct = nullptr) {
+                                                const uint8_t* direct = nullptr, const uint4* pre = nullptr) {
     const uint32_t wend = tb + words;  // absolute end of the tile
     // ---- lane j owns words [tb + 8j, tb + 8j + 8) --------------------------------
     const uint32_t base = tb + lane * 8;
     // FULL: a 512-word tile, every lane owns 8 words (the per-word range tests fold away)
     const uint32_t nw = FULL ? 8u : (lane * 8 < words ? min(8u, words - lane * 8) : 0u);
     uint64_t w[8];
-    if (FULL && direct) {  // a 16-B aligned full tile: the lane's 64 B straight from memory
+    if (FULL && pre) {  // the lane's 64 B, loaded by the caller before the block's barrier
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[2 * q] = (uint64_t)pre[q].x | ((uint64_t)pre[q].y << 32);
+            w[2 * q + 1] = (uint64_t)pre[q].z | ((uint64_t)pre[q].w << 32);
+        }
+    } else if (FULL && direct) {  // a 16-B aligned full tile: the lane's 64 B straight from memory
         const uint4* row = reinterpret_cast<const uint4*>(direct + 64 * lane);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -750,24 +782,29 @@ __device__ __forceinline__ uint32_t encode_tile(uint8_t* lds, const uint64_t* lu
     return P;
 }
 
-// One unit of encode_kernel (wave-uniform `unit`).
-template <bool WRITE>
-__device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
-                                                      const uint64_t* __restrict__ in_off,
-                                                      const uint64_t* __restrict__ in_len, uint8_t* __restrict__ out,
+// A unit's input offset and length, and, for an aligned 512-word unit (every unit of the
+// headline: DIRECT), the lane's 64 B, loaded by encode_kernel before its selector-table barrier.
+struct EncPre {
+    uint64_t b0, nbytes;
+    uint4 r[4];
+};
+
+// One unit of encode_kernel (wave-uniform `unit`), from its prefetched metadata.
+template <bool WRITE, bool DIRECT>
+__device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       const uint64_t* __restrict__ out_off,
                                                       const uint64_t* __restrict__ out_cap,
                                                       uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                       uint32_t unit, uint8_t* lds, const uint64_t* lut,
-                                                      uint32_t lane) {
-    const uint64_t b0 = in_off[unit];
-    const uint64_t nbytes = in_len[unit];
+                                                      uint32_t lane, const EncPre& pre) {
+    const uint64_t b0 = pre.b0;
+    const uint64_t nbytes = pre.nbytes;
     uint64_t ob = 0, cap = 0;
-    int32_t st = ST_OK;
     if (WRITE) {
         ob = out_off[unit];
         cap = out_cap[unit];
     }
+    int32_t st = ST_OK;
     if (reinterpret_cast<uintptr_t>(in + b0) & 7) st = ST_ARG;
     if (st == ST_OK && (nbytes & 7)) st = ST_SIZE;  // message.zig:201
     if (st != ST_OK) {
@@ -790,13 +827,11 @@ __device__ __forceinline__ void encode_unit(const uint8_t* __restrict__ in,
     }
     const uint32_t words = (uint32_t)(nbytes >> 3);
     if (words <= kEncMaxWords) {  // one tile (the headline 4-KiB units)
-        const bool direct = words == kEncMaxWords && !(reinterpret_cast<uintptr_t>(src) & 15);
-        wave_lds_sync();          // the previous unit's write-back read the slice
-        if (!direct) encode_stage(lds, src, words, lane);
+        if (!DIRECT) encode_stage(lds, src, words, lane);  // DIRECT: loaded in pre.r
         wave_lds_sync();
         uint32_t cz = 0, cf = 0;
-        const uint32_t P = direct ? encode_tile<WRITE, true, true>(lds, lut, lane, words, 0, cz, cf, words, words,
-                                                                   out + ob, cap, src)
+        const uint32_t P = DIRECT ? encode_tile<WRITE, true, true>(lds, lut, lane, words, 0, cz, cf, words, words,
+                                                                   out + ob, cap, src, pre.r)
                                   : encode_tile<WRITE, true>(lds, lut, lane, words, 0, cz, cf, words, words, out + ob, cap);
         if (lane == 0) {
             out_len[unit] = P;
@@ -825,18 +860,50 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     __shared__ uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WRITE) {
-        lut[threadIdx.x] = compact_selector(threadIdx.x);
-        __syncthreads();
-    }
+    // The selector table goes out first (LDS-DMA by waves 0 and 1, 1 KiB each), then (an aligned
+    // 512-word unit, the headline's) the lane's 64 B of the unit; the block barrier waits only for
+    // the table, so a block's units are in flight while it lands. The unit's loads are inline asm
+    // counted here (a load hipcc knew of would get the barrier's vmcnt(0)); their registers are
+    // named in the wait statement itself (cdna_hip_programming.md §5.7 item 1, form ii).
+    if (WRITE && wave < 2)
+        glds16(reinterpret_cast<const uint8_t*>(&kCompactSel) + 1024u * wave + 16u * lane,
+               __builtin_amdgcn_readfirstlane(lds_addr(lut) + 1024u * wave));
     uint8_t* lds = smem + wave * kEncLds;
     // a wave per list entry; a list as long as the batch is the identity (class lists keep
     // batch order), so the headline's all-mid batches skip the list read
     const uint32_t count = list ? *list_count : n;
     const uint32_t slot = blockIdx.x * kWavesPerBlock + wave;
-    if (slot >= count) return;
-    const uint32_t unit = (list && count != n) ? __builtin_amdgcn_readfirstlane(list[slot]) : slot;
-    encode_unit<WRITE>(in, in_off, in_len, out, out_off, out_cap, out_len, status, unit, lds, lut, lane);
+    const bool live = slot < count;  // wave-uniform
+    const uint32_t unit = !live ? 0u : (list && count != n) ? __builtin_amdgcn_readfirstlane(list[slot]) : slot;
+    EncPre pre;
+    pre.b0 = live ? in_off[unit] : 0ull;
+    pre.nbytes = live ? in_len[unit] : 0ull;
+    const uint8_t* const src = in + pre.b0;
+    if (live && pre.nbytes == 8ull * kEncMaxWords && !(reinterpret_cast<uintptr_t>(src) & 15)) {
+        const uint4* const row = reinterpret_cast<const uint4*>(src + 64 * lane);
+        u32x4 r0, r1, r2, r3;
+        ds_gload16(r0, row);
+        ds_gload16(r1, row + 1);
+        ds_gload16(r2, row + 2);
+        ds_gload16(r3, row + 3);
+        if (WRITE) {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the table's DMA, not the unit's loads
+            __syncthreads();
+        }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3) : : "memory");
+        pre.r[0] = make_uint4(r0.x, r0.y, r0.z, r0.w);
+        pre.r[1] = make_uint4(r1.x, r1.y, r1.z, r1.w);
+        pre.r[2] = make_uint4(r2.x, r2.y, r2.z, r2.w);
+        pre.r[3] = make_uint4(r3.x, r3.y, r3.z, r3.w);
+        encode_unit<WRITE, true>(in, out, out_off, out_cap, out_len, status, unit, lds, lut, lane, pre);
+        return;
+    }
+    if (WRITE) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (!live) return;
+    encode_unit<WRITE, false>(in, out, out_off, out_cap, out_len, status, unit, lds, lut, lane, pre);
 }
 
 // The units encode_tiled_kernel owns: valid word streams (8-aligned start, whole
@@ -2047,11 +2114,6 @@ __device__ __forceinline__ bool decode_long_unit(const uint8_t* in, uint64_t in_
 }
 
 
-// 16 readable bytes for load lanes that have nothing to stage, and 16 writable
-// bytes for the piece-record stores of lanes without a unit.
-__device__ __attribute__((aligned(16))) uint8_t cpk_dummy16[16];
-__device__ __attribute__((aligned(16))) uint8_t cpk_sink16[16];
-__device__ __attribute__((aligned(64))) uint8_t cpk_sink64[64];
 
 // Pass 1, decode_index_kernel: lane l of a wave owns unit l and walks its record
 // chain once (message.zig:152-191), lockstep by 64-B input block. Every byte is
