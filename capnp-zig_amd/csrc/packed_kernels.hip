@@ -857,7 +857,7 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
                                                         const uint32_t* __restrict__ list,
                                                         const uint32_t* __restrict__ list_count) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // The selector table goes out first (LDS-DMA by waves 0 and 1, 1 KiB each), then (an aligned
@@ -865,13 +865,15 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const uint8_t* __restric
     // the table, so a block's units are in flight while it lands. The unit's loads are inline asm
     // counted here (a load hipcc knew of would get the barrier's vmcnt(0)); their registers are
     // named in the wait statement itself (cdna_hip_programming.md §5.7 item 1, form ii).
+    // a wave per list entry; a list as long as the batch is the identity (class lists keep
+    // batch order), so the headline's all-mid batches skip the list read. The grid is sized by
+    // the batch, so a short list leaves whole blocks without a unit: they leave at once.
+    const uint32_t count = list ? *list_count : n;
+    if (blockIdx.x * kWavesPerBlock >= count) return;  // block-uniform
     if (WRITE && wave < 2)
         glds16(reinterpret_cast<const uint8_t*>(&kCompactSel) + 1024u * wave + 16u * lane,
                __builtin_amdgcn_readfirstlane(lds_addr(lut) + 1024u * wave));
     uint8_t* lds = smem + wave * kEncLds;
-    // a wave per list entry; a list as long as the batch is the identity (class lists keep
-    // batch order), so the headline's all-mid batches skip the list read
-    const uint32_t count = list ? *list_count : n;
     const uint32_t slot = blockIdx.x * kWavesPerBlock + wave;
     const bool live = slot < count;  // wave-uniform
     const uint32_t unit = !live ? 0u : (list && count != n) ? __builtin_amdgcn_readfirstlane(list[slot]) : slot;
@@ -942,7 +944,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiled_kernel(const uint8_t* __r
                                                               uint64_t* __restrict__ out_len,
                                                               int32_t* __restrict__ status, uint32_t* q) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (q[5] == 0) return;  // no serial units (block-uniform)
@@ -1438,7 +1440,7 @@ __global__ __launch_bounds__(kBlock) void encode_message_kernel(const uint64_t* 
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
     __shared__ uint32_t woff_all[TILED ? kWavesPerBlock * (kMsgMaxSegs + 1) : 1];
     __shared__ uint64_t base_all[TILED ? kWavesPerBlock * kMsgMaxSegs : 1];
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (WRITE) {
@@ -1590,7 +1592,7 @@ __global__ __launch_bounds__(kBlock) void decode_lane_kernel(const uint8_t* __re
                                                              const uint64_t* __restrict__ out_cap,
                                                              uint64_t* __restrict__ out_len,
                                                              int32_t* __restrict__ status) {
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     if (WRITE) {
         lut[threadIdx.x] = expand_selector(threadIdx.x);
         __syncthreads();
@@ -3409,7 +3411,7 @@ __global__ __launch_bounds__(kBlock) void tile_encode_kernel(const uint8_t* __re
                                                              uint64_t* __restrict__ out_len,
                                                              int32_t* __restrict__ status, uint32_t* q) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kEncLds];
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const TileTab t = tile_tab(q, n);
@@ -3842,7 +3844,7 @@ __global__ __launch_bounds__(kEsWaves * kWave) void encode_stream_kernel(
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
     const uint32_t* __restrict__ q) {
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     __shared__ __attribute__((aligned(16))) uint8_t ring_blk[kEsWaves * kWave * kEsRing];
     if (WRITE)
         for (uint32_t t = threadIdx.x; t < 256; t += kEsWaves * kWave) lut[t] = compact_selector(t);
@@ -4066,7 +4068,7 @@ __global__ __launch_bounds__(kSmBlock) void decode_small_kernel(const uint8_t* _
                                                                 const uint64_t* __restrict__ out_cap,
                                                                 uint64_t* __restrict__ out_len,
                                                                 int32_t* __restrict__ status, const uint32_t* q) {
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[kSmBlock * kSdRing];
     // each lane's output words by absolutely aligned 8-word (64-B) chunks; a full chunk is
     // stored by a quad of the wave (4 x 16 B), 16 chunks per store instruction
@@ -4368,7 +4370,7 @@ __global__ __launch_bounds__(kSgWaves * kWave) void decode_small_group_kernel(
     uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
     const uint64_t* __restrict__ out_cap, uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
     const uint32_t* q) {
-    __shared__ uint64_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint64_t lut[256];
     __shared__ __attribute__((aligned(16))) uint8_t pin_all[kSgWaves][kSgP + kSgPad];
     __shared__ __attribute__((aligned(16))) uint64_t pout_all[kSgWaves][kSgW];
     __shared__ uint32_t pfx_all[kSgWaves][2][kWave];  // exclusive prefix: pieces, output pairs
