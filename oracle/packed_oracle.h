@@ -76,6 +76,13 @@ void oracle_unpack_batch(const uint8_t* in, const uint64_t* in_off, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, uint64_t* out_len,
                          int32_t* status, int threads);
 
+/* packed_fast.c: the same batch drivers on a word-at-a-time port (bench.py's cpu_baseline
+ * only; units it cannot take go through oracle_pack / oracle_unpack). */
+void fast_pack_batch(const uint8_t* in, const uint64_t* in_off, uint32_t n, uint8_t* out, const uint64_t* out_off,
+                     uint64_t* out_len, int32_t* status, int threads);
+void fast_unpack_batch(const uint8_t* in, const uint64_t* in_off, uint32_t n, uint8_t* out, const uint64_t* out_off,
+                       uint64_t* out_len, int32_t* status, int threads);
+
 /* Host twin of capnp_packed_generate (include/capnp_packed.h). */
 void oracle_generate(uint8_t* out, uint64_t n_units, uint64_t unit_bytes, uint64_t unit_base,
                      uint64_t seed, uint32_t zero_thresh, int threads);

@@ -39,6 +39,8 @@ def lib():
                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_pack_batch.argtypes = batch
         L.oracle_unpack_batch.argtypes = batch
+        L.fast_pack_batch.argtypes = batch    # oracle/packed_fast.c (bench.py's cpu_baseline)
+        L.fast_unpack_batch.argtypes = batch
         L.oracle_generate.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int]
         L.oracle_mix64.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
@@ -134,6 +136,27 @@ def unpack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threa
     status = np.zeros(n, dtype=np.int32)
     lib().oracle_unpack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len),
                               _ptr(status), threads)
+    return out, out_len, status
+
+
+def fast_pack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0):
+    """pack_batch on oracle/packed_fast.c (the CPU baseline's word-at-a-time port)."""
+    n = len(in_off) - 1
+    out = np.zeros(int(out_off[-1]) + 16, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    lib().fast_pack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len), _ptr(status), threads)
+    return out, out_len, status
+
+
+def fast_unpack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0):
+    """unpack_batch on oracle/packed_fast.c."""
+    n = len(in_off) - 1
+    out = np.zeros(int(out_off[-1]) + 16, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    lib().fast_unpack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len), _ptr(status),
+                            threads)
     return out, out_len, status
 
 
