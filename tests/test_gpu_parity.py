@@ -225,6 +225,62 @@ def test_batch_encode_misaligned_word_side_is_rejected():
     assert int(st.item()) == cp.INVALID_ARGUMENT
 
 
+@pytest.mark.parametrize("with_small", [False, True])
+def test_batch_encode_kernel_prologue_paths_mixed_in_blocks(with_small):
+    """encode_kernel's two entry paths side by side in its 4-wave blocks (round 6: an aligned
+    512-word unit's loads go out before the block's selector-table barrier, every other unit is
+    staged after it): 4 KiB units at 16-B and 8-B mod 16 starts, shorter mid units, an empty unit,
+    and (with_small) lane-per-unit small units so the mid list is not the identity, plus units
+    the kernel reports (InvalidMessageSize, a misaligned start). Every byte against the oracle;
+    output slots are guarded by 0xEE canaries."""
+    rng = random.Random(61 + with_small)
+    specs = []
+    for i in range(96):
+        k = i % 8
+        if k in (0, 3, 6):
+            specs.append((4096, 0))          # direct: 16-B aligned 512 words
+        elif k in (1, 5):
+            specs.append((4096, 8))          # 512 words at 8 mod 16: staged
+        elif k == 2:
+            specs.append((8 * rng.randrange(65, 512), rng.choice((0, 8))))
+        elif k == 4:
+            specs.append((8 * rng.randrange(1, 64) if with_small else 0, 0))
+        else:
+            specs.append((8 * rng.randrange(100, 512), 8))
+    specs[7] = (4093, 0)   # InvalidMessageSize (message.zig:201)
+    specs[15] = (4096, 4)  # a start that is not word aligned: INVALID_ARGUMENT
+    units, offs, pos = [], [], 0
+    for ln, mod in specs:
+        pos = (pos + 15) // 16 * 16 + mod
+        offs.append(pos)
+        p = rng.choice((0.1, 0.5, 0.9))
+        units.append(bytes(0 if rng.random() < p else rng.randrange(1, 256) for _ in range(ln)))
+        pos += ln
+    host = np.zeros(pos + 64, dtype=np.uint8)
+    for o, u in zip(offs, units):
+        host[o:o + len(u)] = np.frombuffer(u, dtype=np.uint8)
+    d_in = torch.from_numpy(host).to(DEV)
+    n = len(units)
+    caps = [cp.encode_bound(len(u)) + 16 for u in units]
+    out_off, out_cap, total = slots(caps, align=16)
+    d_out = torch.full((total + 64,), 0xEE, dtype=torch.uint8, device=DEV)
+    out_len = torch.zeros(n, dtype=torch.int64, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    cp.encode_batch(d_in, t64(offs), t64(len(u) for u in units), d_out, out_off, out_cap, out_len, status)
+    torch.cuda.synchronize()
+    sts, lens, oo = status.cpu().numpy(), out_len.cpu().numpy(), out_off.cpu().numpy()
+    out = d_out.cpu().numpy().tobytes()
+    for i, u in enumerate(units):
+        if i == 15:
+            assert sts[i] == cp.INVALID_ARGUMENT
+            continue
+        st, p = oracle.pack(u)
+        assert sts[i] == st, f"unit {i}: status {sts[i]} vs {st}"
+        if st == oracle.OK:
+            assert out[oo[i]:oo[i] + lens[i]] == p, f"unit {i} ({len(u)} B at {offs[i] % 16} mod 16)"
+            assert out[oo[i] + lens[i]:oo[i] + caps[i]] == b"\xee" * (caps[i] - int(lens[i])), f"unit {i} canary"
+
+
 def test_batch_encode_dense_unaligned_output():
     """Dense packed output: sizes -> scan -> encode at unaligned byte offsets."""
     rng = random.Random(13)
