@@ -2948,6 +2948,10 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
             wave_lds_sync();
         }
         const int32_t lim = min(64, end_o);  // sources of this round: ring offsets < lim
+        // A lane whose sources below lim are done may go on to ring offsets 64..66 while other
+        // lanes finish the round (a source's 10 bytes still lie in the ring; the carry keeps
+        // offsets 64.. for the next round), so its next round starts further on
+        const int32_t slim = min(67, end_o);
         for (;;) {  // sub-rounds
             // ---- long zero runs: whole zero lines straight to the slot, not a step per word (an
             // expansion-heavy unit, 00 FF: 256 words per 2 bytes, would hold its wave's round) ----
@@ -2985,14 +2989,14 @@ __global__ __launch_bounds__(kLwWaves * kWave) void decode_words_kernel(
             // a decode stops a lane at the first sub-round that ends at or past its capacity (words
             // past out_cap are never stored); a read stops at the framed length exactly
             const uint32_t rem = W < lim_w ? lim_w - W : 0u;
-            const int32_t limx = rem != 0u ? lim : INT32_MIN;
+            const int32_t limx = rem != 0u ? slim : INT32_MIN;
 #pragma unroll
             for (uint32_t j = 0; j < kLwS; ++j) {
                 const bool act = apos < limx && (!RD || j < rem);
                 if (__builtin_amdgcn_ballot_w64(act) == 0) break;
                 if (act) {
                     // the source's ring offset, kept inside the ring (a zero run's may have left it)
-                    const uint32_t o = (uint32_t)min(max(po, 0), 64);
+                    const uint32_t o = (uint32_t)min(max(po, 0), 66);
                     const uint8_t* const a = ring + o;
                     uint32_t t = a[0], b1 = a[1], c9 = a[9];
                     asm volatile("" : "+v"(t), "+v"(b1), "+v"(c9));  // one LDS round trip per step
