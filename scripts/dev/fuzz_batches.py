@@ -24,6 +24,7 @@ import capnp_packed as cp  # noqa: E402
 import oracle  # noqa: E402
 
 DEV = torch.device("cuda", 0)
+BIG = False
 
 
 def t64(a):
@@ -43,6 +44,9 @@ def one_round(rng, n, stats):
     kind = rng.integers(0, 10, n)
     words = np.where(kind < 5, rng.integers(0, 65, n),
                      np.where(kind < 9, rng.integers(65, 513, n), rng.integers(513, 4097, n)))
+    if BIG:  # C5's tail: 0.5% of units of 64 KiB .. 256 KiB (the huge class and long windows)
+        huge = rng.random(n) < 0.005
+        words[huge] = rng.integers(8192, 32769, int(huge.sum()))
     words[rng.random(n) < 0.3] = 512
     sizes = words * 8
     odd = rng.random(n) < 0.005
@@ -150,7 +154,10 @@ def main():
     ap.add_argument("--seconds", type=float, default=240)
     ap.add_argument("--units", type=int, default=20000)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--big", action="store_true", help="add units of 64-256 KiB")
     a = ap.parse_args()
+    global BIG
+    BIG = a.big
     rng = np.random.default_rng(a.seed)
     stats = {"rounds": 0, "enc_units": 0, "dec_units": 0}
     bad, t0 = [], time.time()
