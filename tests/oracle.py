@@ -119,42 +119,41 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def pack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0):
+def _batch_bufs(n, out_off):
+    """(out, out_len, status) for a batch call; pass them back as bufs= to reuse them (the CPU
+    baseline does, so that its timed calls do not fault in fresh pages)."""
+    return (np.zeros(int(out_off[-1]) + 16, dtype=np.uint8), np.zeros(n, dtype=np.uint64),
+            np.zeros(n, dtype=np.int32))
+
+
+def pack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0, bufs=None):
     n = len(in_off) - 1
-    out = np.zeros(int(out_off[-1]) + 16, dtype=np.uint8)
-    out_len = np.zeros(n, dtype=np.uint64)
-    status = np.zeros(n, dtype=np.int32)
+    out, out_len, status = bufs if bufs is not None else _batch_bufs(n, out_off)
     lib().oracle_pack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len),
                             _ptr(status), threads)
     return out, out_len, status
 
 
-def unpack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0):
+def unpack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0, bufs=None):
     n = len(in_off) - 1
-    out = np.zeros(int(out_off[-1]) + 16, dtype=np.uint8)
-    out_len = np.zeros(n, dtype=np.uint64)
-    status = np.zeros(n, dtype=np.int32)
+    out, out_len, status = bufs if bufs is not None else _batch_bufs(n, out_off)
     lib().oracle_unpack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len),
                               _ptr(status), threads)
     return out, out_len, status
 
 
-def fast_pack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0):
+def fast_pack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0, bufs=None):
     """pack_batch on oracle/packed_fast.c (the CPU baseline's word-at-a-time port)."""
     n = len(in_off) - 1
-    out = np.zeros(int(out_off[-1]) + 16, dtype=np.uint8)
-    out_len = np.zeros(n, dtype=np.uint64)
-    status = np.zeros(n, dtype=np.int32)
+    out, out_len, status = bufs if bufs is not None else _batch_bufs(n, out_off)
     lib().fast_pack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len), _ptr(status), threads)
     return out, out_len, status
 
 
-def fast_unpack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0):
+def fast_unpack_batch(inp: np.ndarray, in_off: np.ndarray, out_off: np.ndarray, threads=0, bufs=None):
     """unpack_batch on oracle/packed_fast.c."""
     n = len(in_off) - 1
-    out = np.zeros(int(out_off[-1]) + 16, dtype=np.uint8)
-    out_len = np.zeros(n, dtype=np.uint64)
-    status = np.zeros(n, dtype=np.int32)
+    out, out_len, status = bufs if bufs is not None else _batch_bufs(n, out_off)
     lib().fast_unpack_batch(_ptr(inp), _ptr(in_off), n, _ptr(out), _ptr(out_off), _ptr(out_len), _ptr(status),
                             threads)
     return out, out_len, status
