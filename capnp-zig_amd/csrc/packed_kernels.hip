@@ -3200,6 +3200,10 @@ __global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t 
     uint32_t* const bl = q_blocks(q, n);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x < kClassK) carry[threadIdx.x] = 0;
+    // the workspace head: every counter and cursor zero before the entries below are set (was a
+    // memset on the caller's stream, one more launch per batch; nothing reads the head between
+    // the workspace's hand-out and this kernel)
+    if (threadIdx.x < kQHead) q[threadIdx.x] = 0u;
     __syncthreads();
     for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
         const uint32_t b = b0 + threadIdx.x;
@@ -5513,8 +5517,9 @@ class SideLaunch {
         if (e == hipSuccess) forked_ = true;
         return e;
     }
-    // The class workspace for a batch of n units (queue_bytes), its counters cleared on
-    // the caller's stream; nullptr when the side stream or the queue cannot be set up.
+    // The class workspace for a batch of n units (queue_bytes); launch_classes must run on it
+    // next (class_scan_kernel clears its counters); nullptr when the side stream or the queue
+    // cannot be set up.
     uint32_t* queue(uint32_t n) {
         if (!ok_) return nullptr;
         uint32_t* q = nullptr;
@@ -5549,8 +5554,7 @@ class SideLaunch {
             ctx_->q_captured |= capturing;
             q = ctx_->q;
         }
-        if (hipMemsetAsync(q, 0, kQHead * sizeof(uint32_t), main_) != hipSuccess) return nullptr;
-        return q;
+        return q;  // its head (counters, cursors) is cleared by class_scan_kernel
     }
     // A second side stream, forked like the first (after fork()); the caller's stream when it
     // cannot be set up.
