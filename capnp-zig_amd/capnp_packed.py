@@ -228,6 +228,7 @@ DECODERS = {"auto": 0, "twopass": 1, "fused": 2, "stream": 3, "words": 4}
 # capnp_packed_set_launch_flags bits (include/capnp_packed.h)
 LAUNCH_LONG_INLINE = 0x1
 LAUNCH_MID_SIDE_STREAM = 0x2
+LAUNCH_CLASS_SCAN = 0x4
 
 
 def lib():
@@ -830,7 +831,7 @@ def set_all_or_nothing(on: bool) -> bool:
 
 def set_launch_flags(flags: int) -> int:
     """Launch policy bits (capnp_packed_set_launch_flags: LAUNCH_LONG_INLINE,
-    LAUNCH_MID_SIDE_STREAM); returns the previous flags. No result depends on them."""
+    LAUNCH_MID_SIDE_STREAM, LAUNCH_CLASS_SCAN); returns the previous flags. No result depends on them."""
     return int(lib().capnp_packed_set_launch_flags(int(flags)))
 
 

@@ -359,7 +359,8 @@ int capnp_packed_set_decoder(int decoder) {
 int capnp_packed_set_all_or_nothing(int on) { return cpk::set_all_or_nothing(on); }
 
 uint32_t capnp_packed_set_launch_flags(uint32_t flags) {
-    return cpk::set_launch_flags(flags & (CAPNP_PACKED_LAUNCH_LONG_INLINE | CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM));
+    return cpk::set_launch_flags(flags & (CAPNP_PACKED_LAUNCH_LONG_INLINE | CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM |
+                                          CAPNP_PACKED_LAUNCH_CLASS_SCAN));
 }
 
 int capnp_packed_stream_release(void* stream) {

@@ -3251,17 +3251,43 @@ __global__ __launch_bounds__(1024) void class_scan_kernel(uint32_t* q, uint32_t 
 }
 
 // Pass 3: every unit to its place in its class list (batch order within a class).
+// fused (a batch of at most kClassBlock class blocks): class_scan_kernel is not launched; every
+// block sums the per-block counts itself (a thread per class block: the counts of the blocks
+// before it and the totals), and block 0 writes the workspace head the scan would have. One
+// launch and its dependency gap fewer per batch call for ~48 KB of L2 reads per block.
 template <int KIND>
 __global__ __launch_bounds__(kClassBlock) void class_scatter_kernel(const uint8_t* __restrict__ in,
                                                                     const uint64_t* __restrict__ in_off,
                                                                     const uint64_t* __restrict__ in_len, uint32_t n,
                                                                     uint8_t* __restrict__ out,
                                                                     const uint64_t* __restrict__ out_off,
-                                                                    const uint64_t* __restrict__ out_cap, uint32_t* q) {
+                                                                    const uint64_t* __restrict__ out_cap, uint32_t* q,
+                                                                    uint32_t fused, uint32_t words_min) {
     __shared__ uint32_t wcnt[16][kClassK];
+    __shared__ uint32_t wtot[16][kClassK];
+    __shared__ uint32_t pre_s[kClassK], own_s[kClassK], tot_s[kClassK], midb_s[CL_MID_BINS + 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t u = blockIdx.x * kClassBlock + threadIdx.x;
+    const uint32_t nb = gridDim.x;
+    // fused: thread t holds class block t's counts, loaded beside the unit's own metadata
+    uint32_t v[kClassK];
+    if (fused) {  // block-uniform; nb <= kClassBlock (launch_classes)
+        const uint32_t* const bl = q_blocks(q, n);
+#pragma unroll
+        for (uint32_t k = 0; k < kClassK; ++k) v[k] = threadIdx.x < nb ? bl[threadIdx.x * kClassK + k] : 0u;
+    }
     const uint32_t c = u < n ? unit_class<KIND>(in, in_off, in_len, out, out_off, out_cap, u) : kClassK;
+    if (fused) {  // one block-wide inclusive scan per class: this block's exclusive prefix, the totals
+#pragma unroll
+        for (uint32_t k = 0; k < kClassK; ++k) {
+            const uint32_t a = wave_incl_sum(v[k], lane);
+            if (lane == 63) wtot[w][k] = a;
+            if (threadIdx.x == blockIdx.x) {
+                own_s[k] = v[k];
+                pre_s[k] = a - v[k];  // within its wave; the waves before it are added below
+            }
+        }
+    }
     uint32_t rank = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kClassK; ++k) {
@@ -3270,31 +3296,71 @@ __global__ __launch_bounds__(kClassBlock) void class_scatter_kernel(const uint8_
         if (c == k) rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     }
     __syncthreads();
+    if (fused) {
+        if (threadIdx.x < kClassK) {
+            const uint32_t wb = blockIdx.x >> 6;  // the wave holding this block's counts
+            uint32_t a = 0, b = 0;
+            for (uint32_t j = 0; j < 16; ++j) {
+                a += wtot[j][threadIdx.x];
+                b += j < wb ? wtot[j][threadIdx.x] : 0u;
+            }
+            tot_s[threadIdx.x] = a;
+            pre_s[threadIdx.x] += b;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // q[11 + b]: mid units in the bins before bin b (class_scan_kernel)
+            uint32_t mid = 0;
+            for (uint32_t b = 0; b < CL_MID_BINS; ++b) {
+                midb_s[b] = mid;
+                mid += tot_s[CL_MID + b];
+            }
+            midb_s[CL_MID_BINS] = mid;
+        }
+        __syncthreads();
+        if (blockIdx.x == 0 && threadIdx.x < kQHead) {  // the head, as class_scan_kernel writes it
+            const uint32_t t = threadIdx.x, mid = midb_s[CL_MID_BINS];
+            uint32_t v = 0;
+            if (t == 0) v = tot_s[CL_LONG];
+            else if (t == 2) v = tot_s[CL_HUGE];
+            else if (t == 3) v = tot_s[CL_SMALL];
+            else if (t == 4) v = mid;
+            else if (t >= 11 && t < 11 + CL_MID_BINS) v = midb_s[t - 11];
+            else if (t == 20) v = words_min == 0 ? 0u : (mid - midb_s[3] >= words_min ? midb_s[3] : mid);
+            q[t] = v;
+        }
+    }
     if (c >= kClassK) return;
-    uint32_t idx = q_blocks(q, n)[blockIdx.x * kClassK + c] + rank;
+    const uint32_t* const P = q_blocks(q, n);  // exclusive prefixes over blocks, per class (scanned)
+    const uint32_t pc = fused ? pre_s[c] : P[blockIdx.x * kClassK + c];
+    uint32_t idx = pc + rank;
     for (uint32_t j = 0; j < w; ++j) idx += wcnt[j][c];
     if (KIND == 4 && c >= CL_MID + CL_MID_BINS - kEsBinsQ) {
         // encode's small units ordered by (class block, length bin) instead of (bin, batch order):
         // a unit's neighbours in memory (other bins) are then coded by waves of the same block,
         // at about the same time, so the lines they share are read once
-        const uint32_t* const P = q_blocks(q, n);  // exclusive prefixes over blocks, per class
-        const uint32_t nb = gridDim.x;
         uint32_t before = 0;  // small units of earlier blocks, and of lower bins in this block
         for (uint32_t cc = CL_MID + CL_MID_BINS - kEsBinsQ; cc < CL_MID + CL_MID_BINS; ++cc) {
             const uint32_t b = cc - CL_MID;
-            const uint32_t tot = (b + 1 < CL_MID_BINS ? q[12 + b] : q[4]) - q[11 + b];
-            const uint32_t pb = P[blockIdx.x * kClassK + cc];
-            const uint32_t pn = blockIdx.x + 1 < nb ? P[(blockIdx.x + 1) * kClassK + cc] : tot;
+            uint32_t pb, pn;
+            if (fused) {
+                pb = pre_s[cc];
+                pn = pb + own_s[cc];
+            } else {
+                const uint32_t tot = (b + 1 < CL_MID_BINS ? q[12 + b] : q[4]) - q[11 + b];
+                pb = P[blockIdx.x * kClassK + cc];
+                pn = blockIdx.x + 1 < nb ? P[(blockIdx.x + 1) * kClassK + cc] : tot;
+            }
             before += pb + (cc < c ? pn - pb : 0u);
         }
-        idx = before + (idx - P[blockIdx.x * kClassK + c]);
-        q[kQHead + 2ull * n + q[11 + CL_MID_BINS - kEsBinsQ] + idx] = u;
+        idx = before + (idx - pc);
+        const uint32_t base = fused ? midb_s[CL_MID_BINS - kEsBinsQ] : q[11 + CL_MID_BINS - kEsBinsQ];
+        q[kQHead + 2ull * n + base + idx] = u;
         return;
     }
     if (c == CL_LONG) q[kQHead + idx] = u;
     else if (c == CL_HUGE) q[kQHead + n - 1 - idx] = u;
     else if (c == CL_SMALL) q[kQHead + 1ull * n + idx] = u;
-    else q[kQHead + 2ull * n + q[11 + (c - CL_MID)] + idx] = u;
+    else q[kQHead + 2ull * n + (fused ? midb_s[c - CL_MID] : q[11 + (c - CL_MID)]) + idx] = u;
 }
 
 // ---- long units, tile-parallel encode ---------------------------------
@@ -5452,15 +5518,20 @@ static uint32_t resident_blocks(K kernel, int block, uint32_t fallback_per_cu) {
     return (uint32_t)(cus * per);
 }
 
+static bool class_scan_launched();  // CAPNP_PACKED_LAUNCH_CLASS_SCAN (below)
+
 // Class the batch's units (class_count / class_scan / class_scatter) on the caller's stream.
 template <int KIND>
 static void launch_classes(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint32_t n,
                            uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, uint32_t* q,
                            int32_t* status, hipStream_t stream, uint32_t words_min = ~0u) {
     const uint32_t nb = (n + kClassBlock - 1) / kClassBlock;
+    // up to kClassBlock class blocks (1M units), the scatter does the scan itself
+    const uint32_t fused = nb >= 1 && nb <= kClassBlock && !class_scan_launched() ? 1u : 0u;
     class_count_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q, status);
-    class_scan_kernel<<<1, 1024, 0, stream>>>(q, n, nb, words_min);
-    class_scatter_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q);
+    if (!fused) class_scan_kernel<<<1, 1024, 0, stream>>>(q, n, nb, words_min);
+    class_scatter_kernel<KIND><<<nb, kClassBlock, 0, stream>>>(in, in_off, in_len, n, out, out_off, out_cap, q, fused,
+                                                               words_min);
 }
 
 // Launch policy (capnp_packed_set_launch_flags, process-wide; no result depends on it):
@@ -5471,9 +5542,13 @@ static void launch_classes(const uint8_t* in, const uint64_t* in_off, const uint
 //                                        takes 85% of its resident size. Round 3:
 //                                        C5 decode 0.678 -> 0.660 ms, but the headline (all mid
 //                                        units) 2.474 -> 2.499 ms from the extra fork and join.
+//   CAPNP_PACKED_LAUNCH_CLASS_SCAN       the class pass's scan as its own kernel (class_scan_kernel)
+//                                        also for batches of at most 1M units, whose scatter
+//                                        otherwise does it (the path larger batches always take).
 static std::atomic<uint32_t> g_launch_flags{0};
 uint32_t set_launch_flags(uint32_t f) { return g_launch_flags.exchange(f); }
 static bool mid_side_stream() { return g_launch_flags.load(std::memory_order_relaxed) & CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM; }
+static bool class_scan_launched() { return g_launch_flags.load(std::memory_order_relaxed) & CAPNP_PACKED_LAUNCH_CLASS_SCAN; }
 
 class SideLaunch {
   public:

@@ -412,9 +412,13 @@ int capnp_packed_set_all_or_nothing(int on);
  *   CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM  encode and decode: mid units on a second side stream beside
  *                                        the small units' kernel (helps batches of mostly small units
  *                                        with a few mid ones; costs a fork/join
- *                                        otherwise). */
+ *                                        otherwise);
+ *   CAPNP_PACKED_LAUNCH_CLASS_SCAN       the class pass's scan as a kernel of its own also for
+ *                                        batches of at most 1M units (by default their scatter
+ *                                        kernel does it; larger batches always launch it). */
 #define CAPNP_PACKED_LAUNCH_LONG_INLINE 0x1u
 #define CAPNP_PACKED_LAUNCH_MID_SIDE_STREAM 0x2u
+#define CAPNP_PACKED_LAUNCH_CLASS_SCAN 0x4u
 uint32_t capnp_packed_set_launch_flags(uint32_t flags);
 
 #ifdef __cplusplus

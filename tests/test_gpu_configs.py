@@ -410,12 +410,14 @@ def struct_u32(v):
 
 
 @pytest.mark.parametrize("flags", [cp.LAUNCH_MID_SIDE_STREAM, cp.LAUNCH_LONG_INLINE,
-                                   cp.LAUNCH_MID_SIDE_STREAM | cp.LAUNCH_LONG_INLINE],
-                         ids=["mid_side_stream", "long_inline", "both"])
+                                   cp.LAUNCH_MID_SIDE_STREAM | cp.LAUNCH_LONG_INLINE, cp.LAUNCH_CLASS_SCAN],
+                         ids=["mid_side_stream", "long_inline", "both", "class_scan"])
 def test_c5_launch_flags(flags):
     """The launch policy (capnp_packed_set_launch_flags): the second side
-    stream for a decode batch's mid units (the small decoder's grid then at 85%), and the long
-    units after the main grid instead of on the side stream. The C5 tests above under each."""
+    stream for a decode batch's mid units (the small decoder's grid then at 85%), the long
+    units after the main grid instead of on the side stream, and the class pass's scan as its
+    own kernel (the path of batches over 1M units; at most 1M, the scatter kernel scans). The
+    C5 tests above under each."""
     with cp.launch_flags(flags):
         for thr in (26, 128, 230):
             test_c5_skewed_sizes_every_unit(thr, "twopass")
